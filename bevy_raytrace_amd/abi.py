@@ -1,0 +1,150 @@
+"""ctypes binding of the C-ABI in include/rt_hip.h (librt_hip.so).
+
+The numpy dtypes below are byte-for-byte the reference's GPU layouts:
+  SPHERE_DTYPE   = SphereGPU   (src/sphere.rs:12-17), 32 B
+  MATERIAL_DTYPE = MaterialGPU (src/ray_trace_materials.rs:33-43), 32 B
+  CAMERA_DTYPE   = CameraGPU   (src/ray_trace_camera.rs:14-25), 128 B std140
+
+The library is loaded from the package directory only (built in-tree by
+`__graft_entry__.build()`); if it is missing, `load()` raises — there is no CPU
+fallback in the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "librt_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "rt_hip.h")
+
+RT_OK = 0
+RT_ERR_INVALID_ARG = -1
+RT_ERR_NO_SCENE = -2
+RT_ERR_DEVICE = -3
+RT_ERR_OUT_OF_MEMORY = -4
+RT_ERR_BAD_SCENE = -5
+
+RT_LAMBERTIAN = 0
+RT_METALLIC = 1
+RT_DIELECTRIC = 2
+
+RT_SAMPLE_BLOCK = 8
+RT_FLAG_NO_PRIMARY_CACHE = 0x1
+
+SPHERE_DTYPE = np.dtype(
+    [("center", "<f4", (3,)), ("radius", "<f4"), ("material", "<u4"), ("_pad", "<u4", (3,))]
+)
+MATERIAL_DTYPE = np.dtype(
+    [("color", "<f4", (4,)), ("reflectance", "<i4"), ("fuzziness", "<f4"),
+     ("index_of_refraction", "<f4"), ("_pad", "<i4")]
+)
+CAMERA_DTYPE = np.dtype(
+    [("transform", "<f4", (16,)),
+     ("forward", "<f4", (3,)), ("fov", "<f4"),
+     ("up", "<f4", (3,)), ("image_plane_distance", "<f4"),
+     ("right", "<f4", (3,)), ("lens_focal_length", "<f4"),
+     ("position", "<f4", (3,)), ("fstop", "<f4")]
+)
+assert SPHERE_DTYPE.itemsize == 32 and MATERIAL_DTYPE.itemsize == 32
+assert CAMERA_DTYPE.itemsize == 128
+
+
+class RtParams(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_uint32), ("height", ctypes.c_uint32),
+                ("spp", ctypes.c_uint32), ("max_depth", ctypes.c_uint32),
+                ("frame0", ctypes.c_uint32), ("row_block", ctypes.c_uint32),
+                ("shard_count", ctypes.c_uint32), ("shard_index", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32), ("_reserved", ctypes.c_uint32 * 3)]
+
+
+class RtStats(ctypes.Structure):
+    _fields_ = [("segments", ctypes.c_uint64), ("traced_segments", ctypes.c_uint64),
+                ("sphere_tests", ctypes.c_uint64), ("paths", ctypes.c_uint64),
+                ("kernel_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
+                ("kernel_launches", ctypes.c_uint32), ("_pad", ctypes.c_uint32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if not k.startswith("_")}
+
+
+assert ctypes.sizeof(RtParams) == 48
+assert ctypes.sizeof(RtStats) == 56
+
+
+class RayTraceError(RuntimeError):
+    """Raised for a negative status from the C-ABI (message from rt_last_error)."""
+
+    def __init__(self, status, message):
+        super().__init__(f"rt status {status}: {message}")
+        self.status = status
+
+
+def make_params(width, height, spp, max_depth, frame0=0, row_block=8, shard_count=1,
+                shard_index=0, flags=0):
+    p = RtParams()
+    p.width, p.height, p.spp, p.max_depth = int(width), int(height), int(spp), int(max_depth)
+    p.frame0, p.row_block = int(frame0), int(row_block)
+    p.shard_count, p.shard_index, p.flags = int(shard_count), int(shard_index), int(flags)
+    return p
+
+
+def shard_rows(height, row_block, shard_count, shard_index):
+    """Rows owned by a shard, increasing y (mirror of rt_shard_rows)."""
+    B = max(1, int(row_block))
+    K = max(1, int(shard_count))
+    return [y for y in range(int(height)) if (y // B) % K == int(shard_index)]
+
+
+_VP = ctypes.c_void_p
+_U32 = ctypes.c_uint32
+_PROTOS = {
+    "rt_version": (ctypes.c_int, []),
+    "rt_shard_rows": (_U32, [_U32, _U32, _U32, _U32]),
+    "rt_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_VP)]),
+    "rt_destroy": (None, [_VP]),
+    "rt_set_scene": (ctypes.c_int, [_VP, _VP, _U32, _VP, _U32]),
+    "rt_render": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(RtParams), _VP, ctypes.POINTER(RtStats)]),
+    "rt_render_device": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(RtParams), _VP, _VP]),
+    "rt_render_async": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(RtParams), _VP]),
+    "rt_wait": (ctypes.c_int, [_VP, ctypes.POINTER(RtStats)]),
+    "rt_assemble_shards": (ctypes.c_int, [_VP, _VP, _U32, _VP, _U32, _U32, _U32, _U32, _VP]),
+    "rt_last_error": (ctypes.c_char_p, [_VP]),
+}
+
+_lib = None
+
+
+def header_symbols(path=HEADER_PATH):
+    """Function names declared in include/rt_hip.h."""
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rt_[a-z_]+)\s*\(", text)))
+
+
+def load(path=LIB_PATH):
+    """Load librt_hip.so (raises if it was not built — no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"{path} is missing: build the HIP library first (python -c "
+            "'import __graft_entry__ as g; g.build()'). There is no CPU fallback.")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in _PROTOS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(lib, ctx, status):
+    if status != RT_OK:
+        msg = lib.rt_last_error(ctx)
+        raise RayTraceError(status, msg.decode() if msg else "")
+    return status

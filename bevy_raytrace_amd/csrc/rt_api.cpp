@@ -1,0 +1,442 @@
+// rt_api.cpp — the C-ABI (include/rt_hip.h) over the gfx950 kernels.
+//
+// Replaces the reference's host-side schedule: RayTracePlugin::build and
+// RayTracePipeline::from_world (src/plugin.rs:25-47, src/ray_trace_pipeline.rs
+// :171-211) become rt_create; the per-frame `prepare` uploads
+// (src/ray_trace_camera.rs:43-68, src/ray_trace_globals.rs:56-68,
+// src/sphere.rs:180-197, src/ray_trace_materials.rs:129-164) become
+// rt_set_scene + the by-value kernel parameters; RayTraceNode::run
+// (src/ray_trace_node.rs:195-224) becomes rt_render*.
+//
+// Per call: memset the work/segment counters, then per sample-block pass one
+// persistent render launch + one collect launch (a single pass unless the
+// block-sum scratch would exceed RT_SCRATCH_BYTES), timed with HIP events on
+// the stream they run on.
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rt_internal.h"
+
+namespace {
+
+thread_local std::string g_err;  // errors with no context
+
+struct Pass {
+    uint32_t block_begin, nblocks;
+};
+
+}  // namespace
+
+struct rt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    int cu_count = 0;
+    int blocks_per_cu = 0;
+
+    // scene
+    bool has_scene = false;
+    uint32_t n = 0, m = 0;
+    float4* d_sph = nullptr;        // (cx, cy, cz, r*r)
+    float2* d_sph_rm = nullptr;     // (radius, material bits)
+    rt_material* d_mats = nullptr;
+    size_t sph_cap = 0, sph_rm_cap = 0, mat_cap = 0;
+
+    // work buffers
+    float4* d_block_sums = nullptr;
+    size_t bs_cap = 0;
+    float4* d_acc = nullptr;
+    size_t acc_cap = 0;
+    float4* d_out = nullptr;        // host-output path staging
+    size_t out_cap = 0;
+    uint32_t* d_counters = nullptr; // [0..1] u64 segment counter, [2..] per-pass work counters
+    size_t counters_cap = 0;        // in u32 words
+    unsigned long long* h_segs = nullptr;  // pinned
+    std::vector<hipEvent_t> ev;     // 2 per pass
+    hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;
+
+    // pending call (async)
+    bool pending = false;
+    hipStream_t pending_stream = nullptr;
+    uint32_t pending_passes = 0;
+    float* pending_host_out = nullptr;
+    size_t pending_out_bytes = 0;
+    uint64_t pending_paths = 0;
+};
+
+static int fail(rt_ctx* ctx, int code, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
+static int fail(rt_ctx* ctx, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (ctx)
+        ctx->err = buf;
+    else
+        g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(ctx, call)                                                                     \
+    do {                                                                                       \
+        hipError_t e_ = (call);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return fail((ctx), e_ == hipErrorOutOfMemory ? RT_ERR_OUT_OF_MEMORY : RT_ERR_DEVICE, \
+                        "%s failed: %s", #call, hipGetErrorString(e_));                        \
+    } while (0)
+
+template <typename T>
+static int ensure(rt_ctx* ctx, T** p, size_t* cap, size_t bytes) {
+    if (bytes <= *cap && *p) return RT_OK;
+    if (*p) {
+        hipFree(*p);
+        *p = nullptr;
+        *cap = 0;
+    }
+    if (bytes == 0) return RT_OK;
+    HIP_TRY(ctx, hipMalloc((void**)p, bytes));
+    *cap = bytes;
+    return RT_OK;
+}
+
+static size_t scratch_limit() {
+    const char* s = getenv("RT_SCRATCH_BYTES");
+    if (s && *s) {
+        unsigned long long v = strtoull(s, nullptr, 10);
+        if (v >= 16) return (size_t)v;
+    }
+    return (size_t)4 << 30;  // 4 GiB of block sums per pass
+}
+
+extern "C" {
+
+int rt_version(void) { return RT_ABI_VERSION; }
+
+uint32_t rt_shard_rows(uint32_t height, uint32_t row_block, uint32_t shard_count,
+                       uint32_t shard_index) {
+    if (row_block == 0) row_block = 1;
+    if (shard_count == 0) shard_count = 1;
+    if (shard_index >= shard_count) return 0;
+    uint32_t rows = 0;
+    const uint32_t nblk = (height + row_block - 1) / row_block;
+    for (uint32_t b = shard_index; b < nblk; b += shard_count) {
+        const uint32_t y0 = b * row_block;
+        const uint32_t y1 = y0 + row_block < height ? y0 + row_block : height;
+        rows += y1 - y0;
+    }
+    return rows;
+}
+
+int rt_create(int device, rt_ctx** out_ctx) {
+    if (!out_ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_create: out_ctx is NULL");
+    *out_ctx = nullptr;
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev == 0)
+        return fail(nullptr, RT_ERR_DEVICE, "rt_create: no HIP device (%s)",
+                    e != hipSuccess ? hipGetErrorString(e) : "count 0");
+    if (device < 0 || device >= ndev)
+        return fail(nullptr, RT_ERR_INVALID_ARG, "rt_create: device %d out of range [0,%d)",
+                    device, ndev);
+    rt_ctx* ctx = new rt_ctx();
+    ctx->device = device;
+    int rc = RT_OK;
+    do {
+        if ((e = hipSetDevice(device)) != hipSuccess) break;
+        if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) break;
+        if ((e = hipDeviceGetAttribute(&ctx->cu_count, hipDeviceAttributeMultiprocessorCount,
+                                       device)) != hipSuccess)
+            break;
+        if ((e = rt_render_occupancy(&ctx->blocks_per_cu)) != hipSuccess) break;
+        if ((e = hipHostMalloc((void**)&ctx->h_segs, sizeof(unsigned long long))) != hipSuccess) break;
+        if ((e = hipEventCreate(&ctx->ev_t0)) != hipSuccess) break;
+        if ((e = hipEventCreate(&ctx->ev_t1)) != hipSuccess) break;
+    } while (0);
+    if (e != hipSuccess) {
+        rc = fail(nullptr, RT_ERR_DEVICE, "rt_create: %s", hipGetErrorString(e));
+        rt_destroy(ctx);
+        return rc;
+    }
+    if (ctx->blocks_per_cu < 1) ctx->blocks_per_cu = 1;
+    *out_ctx = ctx;
+    return RT_OK;
+}
+
+void rt_destroy(rt_ctx* ctx) {
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    if (ctx->pending && ctx->pending_stream) hipStreamSynchronize(ctx->pending_stream);
+    hipFree(ctx->d_sph);
+    hipFree(ctx->d_sph_rm);
+    hipFree(ctx->d_mats);
+    hipFree(ctx->d_block_sums);
+    hipFree(ctx->d_acc);
+    hipFree(ctx->d_out);
+    hipFree(ctx->d_counters);
+    if (ctx->h_segs) hipHostFree(ctx->h_segs);
+    for (hipEvent_t e : ctx->ev) hipEventDestroy(e);
+    if (ctx->ev_t0) hipEventDestroy(ctx->ev_t0);
+    if (ctx->ev_t1) hipEventDestroy(ctx->ev_t1);
+    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n, const rt_material* materials,
+                 uint32_t m) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_set_scene: ctx is NULL");
+    if (n && !spheres) return fail(ctx, RT_ERR_INVALID_ARG, "rt_set_scene: spheres is NULL, n=%u", n);
+    if (m && !materials)
+        return fail(ctx, RT_ERR_INVALID_ARG, "rt_set_scene: materials is NULL, m=%u", m);
+    for (uint32_t j = 0; j < m; ++j) {
+        const int r = materials[j].reflectance;
+        if (r < RT_LAMBERTIAN || r > RT_DIELECTRIC)
+            return fail(ctx, RT_ERR_BAD_SCENE, "material %u: reflectance %d not in {0,1,2}", j, r);
+    }
+    std::vector<float4> sph(n);
+    std::vector<float2> rm(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        const rt_sphere& s = spheres[i];
+        if (s.material >= m)
+            return fail(ctx, RT_ERR_BAD_SCENE, "sphere %u: material %u >= material count %u", i,
+                        s.material, m);
+        const float r = s.radius;
+        sph[i] = make_float4(s.center[0], s.center[1], s.center[2], r * r);  // sqr(s.radius)
+        float mbits;
+        std::memcpy(&mbits, &s.material, 4);
+        rm[i] = make_float2(r, mbits);
+    }
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->pending && ctx->pending_stream) HIP_TRY(ctx, hipStreamSynchronize(ctx->pending_stream));
+    int rc = ensure(ctx, &ctx->d_sph, &ctx->sph_cap, sizeof(float4) * (size_t)n);
+    if (rc) return rc;
+    rc = ensure(ctx, &ctx->d_sph_rm, &ctx->sph_rm_cap, sizeof(float2) * (size_t)n);
+    if (rc) return rc;
+    rc = ensure(ctx, &ctx->d_mats, &ctx->mat_cap, sizeof(rt_material) * (size_t)m);
+    if (rc) return rc;
+    if (n) {
+        HIP_TRY(ctx, hipMemcpy(ctx->d_sph, sph.data(), sizeof(float4) * n, hipMemcpyHostToDevice));
+        HIP_TRY(ctx, hipMemcpy(ctx->d_sph_rm, rm.data(), sizeof(float2) * n, hipMemcpyHostToDevice));
+    }
+    if (m)
+        HIP_TRY(ctx, hipMemcpy(ctx->d_mats, materials, sizeof(rt_material) * m, hipMemcpyHostToDevice));
+    ctx->n = n;
+    ctx->m = m;
+    ctx->has_scene = true;
+    return RT_OK;
+}
+
+// Validate and enqueue a whole frame on `stream`, writing float4 pixels to d_out.
+static int enqueue(rt_ctx* ctx, const rt_camera* cam, const rt_params* prm, float4* d_out,
+                   hipStream_t stream, uint32_t* out_passes, uint64_t* out_paths) {
+    if (!cam || !prm) return fail(ctx, RT_ERR_INVALID_ARG, "camera or params is NULL");
+    if (!ctx->has_scene) return fail(ctx, RT_ERR_NO_SCENE, "rt_render before rt_set_scene");
+    if (ctx->pending) return fail(ctx, RT_ERR_INVALID_ARG, "a previous async call was not waited for");
+    const rt_params p = *prm;
+    if (p.width == 0 || p.height == 0 || p.spp == 0 || p.max_depth == 0)
+        return fail(ctx, RT_ERR_INVALID_ARG, "width/height/spp/max_depth must be > 0 (%u,%u,%u,%u)",
+                    p.width, p.height, p.spp, p.max_depth);
+    const uint32_t K = p.shard_count ? p.shard_count : 1;
+    const uint32_t B = p.row_block ? p.row_block : 1;
+    if (p.shard_index >= K)
+        return fail(ctx, RT_ERR_INVALID_ARG, "shard_index %u >= shard_count %u", p.shard_index, K);
+    if ((uint64_t)p.width * p.height > 0xFFFFFFFFull)
+        return fail(ctx, RT_ERR_INVALID_ARG, "image of %u x %u pixels exceeds 2^32", p.width, p.height);
+    const uint32_t rows = rt_shard_rows(p.height, B, K, p.shard_index);
+    const uint32_t npix = rows * p.width;
+    const uint32_t blocks_total = (p.spp + RT_SAMPLE_BLOCK - 1) / RT_SAMPLE_BLOCK;
+    if (!d_out) return fail(ctx, RT_ERR_INVALID_ARG, "output pointer is NULL");
+
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    std::vector<Pass> passes;
+    if (npix) {
+        const size_t per_block = (size_t)npix * sizeof(float4);
+        uint64_t pb = scratch_limit() / per_block;
+        const uint64_t by_index = 0x7FFFFFFFull / npix;  // work items fit in u32
+        if (pb > by_index) pb = by_index;
+        if (pb < 1) pb = 1;
+        if (pb > blocks_total) pb = blocks_total;
+        for (uint32_t b = 0; b < blocks_total; b += (uint32_t)pb) {
+            const uint32_t nb = (uint32_t)((blocks_total - b) < pb ? (blocks_total - b) : pb);
+            passes.push_back(Pass{b, nb});
+        }
+        int rc = ensure(ctx, &ctx->d_block_sums, &ctx->bs_cap, per_block * (size_t)pb);
+        if (rc) return rc;
+        if (passes.size() > 1) {
+            rc = ensure(ctx, &ctx->d_acc, &ctx->acc_cap, per_block);
+            if (rc) return rc;
+        }
+    }
+    const size_t words = 2 + passes.size();
+    const size_t words_pad = (words + 3) & ~(size_t)3;  // 16-B multiple
+    {
+        int rc = ensure(ctx, &ctx->d_counters, &ctx->counters_cap, words_pad * sizeof(uint32_t));
+        if (rc) return rc;
+    }
+    while (ctx->ev.size() < 2 * passes.size()) {
+        hipEvent_t e;
+        HIP_TRY(ctx, hipEventCreate(&e));
+        ctx->ev.push_back(e);
+    }
+
+    KParams K_{};
+    K_.width = p.width;
+    K_.height = p.height;
+    K_.spp = p.spp;
+    K_.max_depth = p.max_depth;
+    K_.frame0 = p.frame0;
+    K_.row_block = B;
+    K_.shard_count = K;
+    K_.shard_index = p.shard_index;
+    K_.npix = npix;
+    K_.nspheres = ctx->n;
+    K_.flags = p.flags;
+    std::memcpy(K_.T, cam->transform, sizeof(K_.T));
+    K_.tan_half = (float)std::tan((double)(cam->fov / 2.0f));                 // generate.wgsl:67
+    K_.focus_plane = (cam->image_plane_distance * cam->lens_focal_length) /  // generate.wgsl:94-95
+                     (cam->image_plane_distance - cam->lens_focal_length);
+    K_.aspect = (float)p.width;
+    K_.half_w = (float)p.width / 2.0f;
+    K_.half_h = (float)p.height / 2.0f;
+
+    HIP_TRY(ctx, hipEventRecord(ctx->ev_t0, stream));
+    HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, words_pad * sizeof(uint32_t), stream));
+    const uint32_t grid_full = (uint32_t)(ctx->cu_count * ctx->blocks_per_cu);
+    for (size_t i = 0; i < passes.size(); ++i) {
+        K_.block_begin = passes[i].block_begin;
+        K_.nblocks = passes[i].nblocks;
+        const uint64_t items = (uint64_t)npix * K_.nblocks;
+        const uint64_t chunks = (items + RT_WAVE_CHUNK - 1) / RT_WAVE_CHUNK;
+        const uint64_t need_blocks = (chunks + (RT_BLOCK_THREADS / 64) - 1) / (RT_BLOCK_THREADS / 64);
+        const uint32_t grid = (uint32_t)(need_blocks < grid_full ? need_blocks : grid_full);
+        HIP_TRY(ctx, hipEventRecord(ctx->ev[2 * i], stream));
+        HIP_TRY(ctx, rt_launch_render(&K_, ctx->d_sph, ctx->d_sph_rm, ctx->d_mats, ctx->d_block_sums,
+                                      ctx->d_counters + 2 + i,
+                                      reinterpret_cast<unsigned long long*>(ctx->d_counters),
+                                      grid, stream));
+        HIP_TRY(ctx, hipEventRecord(ctx->ev[2 * i + 1], stream));
+        HIP_TRY(ctx, rt_launch_collect(ctx->d_block_sums, npix, K_.nblocks, ctx->d_acc, i == 0,
+                                       i + 1 == passes.size(), (float)p.spp, d_out, stream));
+    }
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_segs, ctx->d_counters, sizeof(unsigned long long),
+                                hipMemcpyDeviceToHost, stream));
+    *out_passes = (uint32_t)passes.size();
+    *out_paths = (uint64_t)npix * p.spp;
+    return RT_OK;
+}
+
+// ev_t1 has been recorded by the caller after its last operation.
+static int finish(rt_ctx* ctx, uint32_t passes, uint64_t paths, rt_stats* st) {
+    HIP_TRY(ctx, hipEventSynchronize(ctx->ev_t1));
+    if (!st) return RT_OK;
+    std::memset(st, 0, sizeof(*st));
+    double kms = 0.0;
+    for (uint32_t i = 0; i < passes; ++i) {
+        float ms = 0.0f;
+        HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->ev[2 * i], ctx->ev[2 * i + 1]));
+        kms += ms;
+    }
+    float tms = 0.0f;
+    HIP_TRY(ctx, hipEventElapsedTime(&tms, ctx->ev_t0, ctx->ev_t1));
+    st->traced_segments = *ctx->h_segs;
+    st->segments = *ctx->h_segs;
+    st->sphere_tests = st->traced_segments * (uint64_t)ctx->n;
+    st->paths = paths;
+    st->kernel_ms = kms;
+    st->total_ms = tms;
+    st->kernel_launches = passes;
+    return RT_OK;
+}
+
+int rt_render_device(rt_ctx* ctx, const rt_camera* camera, const rt_params* params,
+                     float* out_rgba_device, void* stream) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_render_device: ctx is NULL");
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    uint32_t passes = 0;
+    uint64_t paths = 0;
+    int rc = enqueue(ctx, camera, params, reinterpret_cast<float4*>(out_rgba_device), s, &passes,
+                     &paths);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipEventRecord(ctx->ev_t1, s));
+    ctx->pending = true;
+    ctx->pending_stream = s;
+    ctx->pending_passes = passes;
+    ctx->pending_host_out = nullptr;
+    ctx->pending_paths = paths;
+    return RT_OK;
+}
+
+int rt_render_async(rt_ctx* ctx, const rt_camera* camera, const rt_params* params, float* out_rgba) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_render_async: ctx is NULL");
+    if (!out_rgba) return fail(ctx, RT_ERR_INVALID_ARG, "rt_render_async: out_rgba is NULL");
+    if (!params) return fail(ctx, RT_ERR_INVALID_ARG, "rt_render_async: params is NULL");
+    const uint32_t K = params->shard_count ? params->shard_count : 1;
+    const uint32_t rows = rt_shard_rows(params->height, params->row_block, K, params->shard_index);
+    const size_t bytes = (size_t)rows * params->width * sizeof(float4);
+    if (ctx->pending) return fail(ctx, RT_ERR_INVALID_ARG, "a previous async call was not waited for");
+    int rc = ensure(ctx, &ctx->d_out, &ctx->out_cap, bytes ? bytes : 16);
+    if (rc) return rc;
+    uint32_t passes = 0;
+    uint64_t paths = 0;
+    rc = enqueue(ctx, camera, params, ctx->d_out, ctx->stream, &passes, &paths);
+    if (rc) return rc;
+    if (bytes)
+        HIP_TRY(ctx, hipMemcpyAsync(out_rgba, ctx->d_out, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipEventRecord(ctx->ev_t1, ctx->stream));
+    ctx->pending = true;
+    ctx->pending_stream = ctx->stream;
+    ctx->pending_passes = passes;
+    ctx->pending_host_out = out_rgba;
+    ctx->pending_out_bytes = bytes;
+    ctx->pending_paths = paths;
+    return RT_OK;
+}
+
+int rt_wait(rt_ctx* ctx, rt_stats* stats) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_wait: ctx is NULL");
+    if (!ctx->pending) return fail(ctx, RT_ERR_INVALID_ARG, "rt_wait: nothing pending");
+    ctx->pending = false;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    return finish(ctx, ctx->pending_passes, ctx->pending_paths, stats);
+}
+
+int rt_render(rt_ctx* ctx, const rt_camera* camera, const rt_params* params, float* out_rgba,
+              rt_stats* stats) {
+    int rc = rt_render_async(ctx, camera, params, out_rgba);
+    if (rc) return rc;
+    return rt_wait(ctx, stats);
+}
+
+int rt_assemble_shards(rt_ctx* ctx, const float* gathered_device, uint32_t max_rows,
+                       float* image_device, uint32_t width, uint32_t height, uint32_t row_block,
+                       uint32_t shard_count, void* stream) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_assemble_shards: ctx is NULL");
+    if (!gathered_device || !image_device || width == 0 || height == 0 || shard_count == 0)
+        return fail(ctx, RT_ERR_INVALID_ARG, "rt_assemble_shards: bad arguments");
+    const uint32_t B = row_block ? row_block : 1;
+    for (uint32_t k = 0; k < shard_count; ++k)
+        if (rt_shard_rows(height, B, shard_count, k) > max_rows)
+            return fail(ctx, RT_ERR_INVALID_ARG, "rt_assemble_shards: shard %u has more than %u rows",
+                        k, max_rows);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    HIP_TRY(ctx, rt_launch_assemble(reinterpret_cast<const float4*>(gathered_device), max_rows,
+                                    reinterpret_cast<float4*>(image_device), width, height, B,
+                                    shard_count, s));
+    if (!stream) HIP_TRY(ctx, hipStreamSynchronize(s));
+    return RT_OK;
+}
+
+const char* rt_last_error(const rt_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+}  // extern "C"

@@ -1,0 +1,37 @@
+// rt_internal.h — shared between the C-ABI host code and the kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rt_hip.h"
+
+#define RT_BLOCK_THREADS 256  // 4 waves per workgroup
+#define RT_WAVE_CHUNK 64      // work items a wave takes per atomic
+
+// Kernel parameters (by value; lands in SGPRs). Camera constants are
+// precomputed on the host exactly as generate.wgsl:67-95 computes them.
+struct KParams {
+    uint32_t width, height, spp, max_depth, frame0;
+    uint32_t row_block, shard_count, shard_index;
+    uint32_t npix;         // pixels of this shard (rows * width)
+    uint32_t block_begin;  // first sample block of this pass
+    uint32_t nblocks;      // sample blocks in this pass
+    uint32_t nspheres;
+    uint32_t flags;
+    float T[16];           // camera transform, column-major
+    float tan_half, focus_plane, aspect, half_w, half_h;
+};
+
+extern "C" {
+hipError_t rt_launch_render(const KParams* P, const float4* sph, const float2* sph_rm,
+                            const rt_material* mats, float4* block_sums, uint32_t* work_counter,
+                            unsigned long long* seg_counter, uint32_t grid, hipStream_t stream);
+hipError_t rt_launch_collect(const float4* block_sums, uint32_t npix, uint32_t nblocks,
+                             float4* acc, int first_pass, int last_pass, float spp, float4* out,
+                             hipStream_t stream);
+hipError_t rt_launch_assemble(const float4* gathered, uint32_t max_rows, float4* image,
+                              uint32_t width, uint32_t height, uint32_t row_block,
+                              uint32_t shard_count, hipStream_t stream);
+hipError_t rt_render_occupancy(int* blocks_per_cu);
+}

@@ -1,0 +1,421 @@
+// rt_kernels.hip — the MI355X (gfx950) path-tracer kernels.
+//
+// ONE persistent kernel replaces the reference's whole WGSL chain
+//   clear.wgsl:71-87 -> generate.wgsl:109-130 -> 3 x (prepass.wgsl:55-63,
+//   intersect.wgsl:145-163, shade.wgsl:199-258) -> collect.wgsl:99-125
+// dispatched by RayTraceNode::run (src/ray_trace_node.rs:195-224). Nothing is
+// exchanged through HBM between stages: each lane keeps its whole path state
+// (ray, throughput, seed, sample-block sum) in VGPRs.
+//
+// Work decomposition: an *item* is (pixel, sample block of RT_SAMPLE_BLOCK
+// samples). Items are dealt to lanes from a global counter in chunks of 64 per
+// wave; a lane whose path ends starts the next sample of its block, and a lane
+// whose block ends writes the block sum and takes the next item (wave-ballot
+// refill), so lanes do not idle while the wave's longest path finishes.
+//
+// Intersection (the hot loop, intersect.wgsl:133-143): every sphere of the
+// list is tested for every live ray (brute force, list order). The sphere
+// records (cx, cy, cz, r^2) are wave-uniform, so they are read with scalar
+// loads (s_load_dwordx4 through the scalar cache) and fed to v_fma_f32 as SGPR
+// operands: no LDS or VGPR traffic per sphere. Each test is a conservative
+// FMA-form filter (11 VALU ops + 1 compare; see DESIGN.md "Exact filter"):
+//   G = (oc.dn)^2 + r^2 - (1 - 2^-16) |oc|^2,  dn = d/|d|
+// G < 0 proves the reference's discriminant (intersect.wgsl:102) is negative,
+// so the sphere cannot hit. Only the rare candidates (G >= 0) are re-evaluated
+// with the reference's exact op sequence (intersect.wgsl:97-115), in list
+// order, with the strict `<` tie-break (:137). The result is therefore
+// bit-identical to the brute-force reference loop.
+//
+// Floating point: compiled with -ffp-contract=off; every expression below
+// except the explicit __builtin_fmaf calls of the filter is one IEEE f32
+// round-to-nearest op, with correctly rounded div / sqrt (hipcc default), in
+// the same order as oracle/rt_oracle.c.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rt_internal.h"
+
+#define VERY_FAR 1e20f
+#define EPSILON 0.001f
+
+namespace {
+
+struct v3 {
+    float x, y, z;
+};
+
+__device__ __forceinline__ v3 mk(float x, float y, float z) { return v3{x, y, z}; }
+__device__ __forceinline__ v3 add(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ v3 sub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ v3 mul(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ v3 scale(v3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ v3 neg(v3 a) { return mk(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ float dot(v3 a, v3 b) {
+    float r = a.x * b.x;
+    r = r + a.y * b.y;
+    r = r + a.z * b.z;
+    return r;
+}
+__device__ __forceinline__ float length(v3 a) { return sqrtf(dot(a, a)); }
+__device__ __forceinline__ v3 normalize(v3 a) {
+    float l = length(a);
+    return mk(a.x / l, a.y / l, a.z / l);
+}
+
+// shade.wgsl:105-116
+__device__ __forceinline__ v3 hash3(uint32_t n) {
+    n = (n << 13) ^ n;
+    n = n * (n * n * 15731u + 789221u) + 1376312589u;
+    uint32_t kx = n * n;
+    uint32_t ky = n * (n * 16807u);
+    uint32_t kz = n * (n * 48271u);
+    const float den = 2147483648.0f;
+    return mk((float)(kx & 0x7fffffffu) / den, (float)(ky & 0x7fffffffu) / den,
+              (float)(kz & 0x7fffffffu) / den);
+}
+
+// generate.wgsl:66-129 (lens offset 0: origin = camera translation).
+__device__ __forceinline__ void primary_ray(const KParams& P, uint32_t x, uint32_t y, v3& o,
+                                            v3& d) {
+    float px = (float)x, py = (float)y;
+    v3 dir = mk(((px - P.half_w) * P.tan_half) / P.aspect,
+                ((-py + P.half_h) * P.tan_half) / P.aspect, -1.0f);
+    dir = normalize(dir);
+    float denom = dot(dir, mk(0.0f, 0.0f, -1.0f));
+    v3 fpnt = scale(dir, P.focus_plane / denom);
+    v3 origin = mk(0.0f, 0.0f, 0.0f);
+    dir = normalize(sub(fpnt, origin));
+    const float* T = P.T;
+    o = add(origin, mk(T[12], T[13], T[14]));
+    d.x = ((T[0] * dir.x + T[4] * dir.y) + T[8] * dir.z) + T[12] * 0.0f;
+    d.y = ((T[1] * dir.x + T[5] * dir.y) + T[9] * dir.z) + T[13] * 0.0f;
+    d.z = ((T[2] * dir.x + T[6] * dir.y) + T[10] * dir.z) + T[14] * 0.0f;
+}
+
+// shade.wgsl:189-197
+__device__ __forceinline__ v3 sky(v3 d) {
+    v3 unit = normalize(d);
+    float t = 0.5f * unit.y + 1.0f;
+    float omt = (1.0f - t) * 1.0f;
+    return mk(omt + t * 0.5f, omt + t * 0.7f, omt + t * 1.0f);
+}
+
+__device__ __forceinline__ v3 reflect(v3 v, v3 n) {  // shade.wgsl:132-134
+    float k = 2.0f * dot(v, n);
+    return sub(v, scale(n, k));
+}
+
+// Exact reference test of one sphere (intersect.wgsl:97-115 + :137).
+__device__ __forceinline__ void exact_test(float4 s, int idx, v3 o, v3 d, float a,
+                                           float& best_t, int& best_i) {
+    v3 oc = mk(o.x - s.x, o.y - s.y, o.z - s.z);
+    float half_b = dot(oc, d);
+    float lo = length(oc);
+    float c = lo * lo - s.w;  // s.w = RN(radius*radius) = sqr(s.radius)
+    float dis = half_b * half_b - a * c;
+    if (dis < 0.0f) return;
+    float sqrtd = sqrtf(dis);
+    float root = (-half_b - sqrtd) / a;
+    if (root < EPSILON || VERY_FAR < root) {
+        root = (-half_b + sqrtd) / a;
+        if (root < EPSILON || VERY_FAR < root) return;
+    }
+    if (root < best_t) {
+        best_t = root;
+        best_i = idx;
+    }
+}
+
+// Conservative filter value; G < 0 => certain miss (see file header).
+__device__ __forceinline__ float filter_g(float4 s, v3 o, v3 dn, float negk) {
+    float ocx = o.x - s.x, ocy = o.y - s.y, ocz = o.z - s.z;
+    float hb = __builtin_fmaf(ocz, dn.z, __builtin_fmaf(ocy, dn.y, ocx * dn.x));
+    float q = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx));
+    return __builtin_fmaf(negk, q, __builtin_fmaf(hb, hb, s.w));
+}
+
+// Closest hit over the whole list. Returns best index (-1 = miss) and t.
+__device__ __forceinline__ int intersect_world(const float4* __restrict__ sph, uint32_t n, v3 o,
+                                               v3 d, float& t_out) {
+    const float dd = dot(d, d);
+    const float l = sqrtf(dd);
+    const float a = l * l;                        // sqr(length(r.dir)), intersect.wgsl:98
+    const float rs = __builtin_amdgcn_rsqf(dd);  // filter only: approximate 1/|d|
+    const v3 dn = mk(d.x * rs, d.y * rs, d.z * rs);
+    const float negk = -(1.0f - 0x1p-16f);
+    float best_t = VERY_FAR;
+    int best_i = -1;
+    uint32_t i = 0;
+    for (; i + 4 <= n; i += 4) {
+        const float4 s0 = sph[i], s1 = sph[i + 1], s2 = sph[i + 2], s3 = sph[i + 3];
+        const float g0 = filter_g(s0, o, dn, negk);
+        const float g1 = filter_g(s1, o, dn, negk);
+        const float g2 = filter_g(s2, o, dn, negk);
+        const float g3 = filter_g(s3, o, dn, negk);
+        const bool c0 = !(g0 < 0.0f), c1 = !(g1 < 0.0f), c2 = !(g2 < 0.0f), c3 = !(g3 < 0.0f);
+        if (c0 | c1 | c2 | c3) {
+            if (c0) exact_test(s0, (int)i, o, d, a, best_t, best_i);
+            if (c1) exact_test(s1, (int)i + 1, o, d, a, best_t, best_i);
+            if (c2) exact_test(s2, (int)i + 2, o, d, a, best_t, best_i);
+            if (c3) exact_test(s3, (int)i + 3, o, d, a, best_t, best_i);
+        }
+    }
+    for (; i < n; ++i) {
+        const float4 s = sph[i];
+        if (!(filter_g(s, o, dn, negk) < 0.0f)) exact_test(s, (int)i, o, d, a, best_t, best_i);
+    }
+    t_out = best_t;
+    return best_i;
+}
+
+__device__ __forceinline__ uint32_t lanemask_lt_count(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+}  // namespace
+
+// Lane state of one in-flight path.
+struct PathState {
+    v3 o, d;            // current ray
+    v3 color;           // throughput (intersection.color, clear.wgsl:86)
+    v3 bsum;            // sum of finished samples of the current block
+    v3 nseed;           // normalize(seed)
+    float seedx;        // seed.x (dielectric Schlick test)
+    uint32_t x, y;      // global pixel
+    uint32_t item;      // work item = (block - block_begin) * npix + pixel
+    uint32_t s, s_end;  // current sample, end of the block
+    uint32_t bounce;
+};
+
+__device__ __forceinline__ void start_sample(const KParams& P, PathState& st) {
+    const uint32_t frame = P.frame0 + st.s;
+    const v3 seed = hash3(st.x + P.width * st.y + (P.width * P.height) * frame);
+    st.seedx = seed.x;
+    st.nseed = normalize(seed);
+    primary_ray(P, st.x, st.y, st.o, st.d);
+    st.color = mk(1.0f, 1.0f, 1.0f);
+    st.bounce = 0;
+}
+
+__device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint32_t item) {
+    st.item = item;
+    const uint32_t bl = item / P.npix;
+    const uint32_t p = item - bl * P.npix;
+    const uint32_t r = p / P.width;
+    st.x = p - r * P.width;
+    const uint32_t B = P.row_block;
+    st.y = ((r / B) * P.shard_count + P.shard_index) * B + (r % B);
+    const uint32_t b = P.block_begin + bl;
+    st.s = b * RT_SAMPLE_BLOCK;
+    st.s_end = min(P.spp, st.s + RT_SAMPLE_BLOCK);
+    st.bsum = mk(0.0f, 0.0f, 0.0f);
+    start_sample(P, st);
+}
+
+__global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_render_kernel(
+    KParams P, const float4* __restrict__ sph, const float2* __restrict__ sph_rm,
+    const rt_material* __restrict__ mats, float4* __restrict__ block_sums,
+    uint32_t* __restrict__ work_counter, unsigned long long* __restrict__ seg_counter) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t total = P.npix * P.nblocks;
+    const uint32_t D = P.max_depth;
+
+    PathState st;
+    bool has_item = false;
+    uint32_t q_next = 0, q_end = 0;  // wave-uniform chunk of work items
+    bool exhausted = false;
+    uint32_t segs = 0;
+
+    for (;;) {
+        // ---- refill: lanes without an item take the next ones (wave ballot)
+        uint64_t need = __ballot(!has_item);
+        while (need != 0 && !exhausted) {
+            if (q_next >= q_end) {
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(work_counter, (uint32_t)RT_WAVE_CHUNK);
+                base = __shfl(base, 0);
+                if (base >= total) {
+                    exhausted = true;
+                    break;
+                }
+                q_next = base;
+                q_end = min(base + (uint32_t)RT_WAVE_CHUNK, total);
+            }
+            const uint32_t avail = q_end - q_next;
+            const uint32_t rank = lanemask_lt_count(need);
+            const uint32_t cnt = (uint32_t)__popcll(need);
+            if (!has_item && rank < avail) {
+                start_item(P, st, q_next + rank);
+                has_item = true;
+            }
+            q_next += min(avail, cnt);
+            need = __ballot(!has_item);
+        }
+        if (__ballot(has_item) == 0) break;
+
+        if (has_item) {
+            // ---- intersect (intersect.wgsl:145-163)
+            float t;
+            const int hi = intersect_world(sph, P.nspheres, st.o, st.d, t);
+            ++segs;
+            bool done = false;
+            // ---- shade (shade.wgsl:199-258)
+            if (hi < 0) {
+                st.color = mul(st.color, sky(st.d));
+                done = true;
+            } else if (st.bounce == D - 1) {
+                st.color = mk(0.0f, 0.0f, 0.0f);
+                done = true;
+            } else {
+                const float4 s = sph[hi];
+                const float2 rm = sph_rm[hi];
+                const float radius = rm.x;
+                const uint32_t mi = __float_as_uint(rm.y);
+                // hit record, intersect.wgsl:117-127
+                const v3 pos = add(st.o, scale(st.d, t));
+                const v3 q = sub(pos, mk(s.x, s.y, s.z));
+                v3 nrm = normalize(mk(q.x / radius, q.y / radius, q.z / radius));
+                bool front = true;
+                if (dot(st.d, nrm) > 0.0f) {
+                    nrm = neg(nrm);
+                    front = false;
+                }
+                const float4 mc = *reinterpret_cast<const float4*>(mats[mi].color);
+                const int refl = mats[mi].reflectance;
+                if (refl == 0) {  // lambertian, shade.wgsl:118-130
+                    const v3 dest = add(add(pos, nrm), st.nseed);
+                    st.d = normalize(sub(dest, pos));
+                    st.o = pos;
+                    st.color = mul(st.color, mk(mc.x, mc.y, mc.z));
+                } else if (refl == 1) {  // metallic, shade.wgsl:136-146
+                    const v3 e_origin = add(pos, scale(nrm, EPSILON));
+                    const v3 reflected = normalize(reflect(st.d, nrm));
+                    const v3 noise = scale(st.nseed, mats[mi].fuzziness);
+                    st.d = normalize(add(reflected, noise));
+                    st.o = e_origin;
+                    st.color = mul(st.color, mk(mc.x, mc.y, mc.z));
+                } else {  // dielectric, shade.wgsl:163-187
+                    const float ior = mats[mi].index_of_refraction;
+                    float ratio = ior;
+                    if (front) ratio = 1.0f / ior;
+                    const v3 unit_dir = normalize(st.d);
+                    const float cos_theta = fminf(dot(neg(unit_dir), nrm), 1.0f);
+                    const float sin_theta = sqrtf(1.0f - cos_theta * cos_theta);
+                    const bool cannot_refract = ratio * sin_theta > 1.0f;
+                    float r0 = (1.0f - ratio) / (1.0f + ratio);
+                    r0 = r0 * r0;
+                    const float xr = 1.0f - cos_theta;
+                    const float x2 = xr * xr;
+                    const float refl_p = r0 + (1.0f - r0) * ((x2 * x2) * xr);
+                    v3 e_dir;
+                    if (cannot_refract || refl_p > st.seedx) {
+                        e_dir = reflect(st.d, nrm);
+                    } else {  // refract, shade.wgsl:148-154
+                        const float ct = fminf(dot(neg(unit_dir), nrm), 1.0f);
+                        const v3 perp = scale(add(unit_dir, scale(nrm, ct)), ratio);
+                        const float lp = length(perp);
+                        const float par = -sqrtf(fabsf(1.0f - (lp * lp)));
+                        e_dir = normalize(add(perp, scale(nrm, par)));
+                    }
+                    st.o = add(pos, scale(nrm, EPSILON));
+                    st.d = e_dir;
+                }
+                ++st.bounce;
+            }
+            if (done) {
+                // path finished: accumulate (collect.wgsl:115-120, blocked)
+                st.bsum = add(st.bsum, st.color);
+                ++st.s;
+                if (st.s < st.s_end) {
+                    start_sample(P, st);
+                } else {
+                    block_sums[st.item] = make_float4(st.bsum.x, st.bsum.y, st.bsum.z, 0.0f);
+                    has_item = false;
+                }
+            }
+        }
+    }
+
+    // ---- segment count: wave reduce, one atomic per wave
+    unsigned long long v = segs;
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if (lane == 0) atomicAdd(seg_counter, v);
+}
+
+// Fold this pass's block sums into acc (block order) and, on the last pass,
+// write out = acc / spp with alpha 1 (collect.wgsl:115-125).
+__global__ void rt_collect_kernel(const float4* __restrict__ block_sums, uint32_t npix,
+                                  uint32_t nblocks, float4* __restrict__ acc, int first_pass,
+                                  int last_pass, float spp, float4* __restrict__ out) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npix) return;
+    float ax, ay, az;
+    uint32_t b0 = 0;
+    if (first_pass) {
+        const float4 v = block_sums[p];
+        ax = v.x; ay = v.y; az = v.z;
+        b0 = 1;
+    } else {
+        const float4 v = acc[p];
+        ax = v.x; ay = v.y; az = v.z;
+    }
+    for (uint32_t b = b0; b < nblocks; ++b) {
+        const float4 v = block_sums[(size_t)b * npix + p];
+        ax = ax + v.x; ay = ay + v.y; az = az + v.z;
+    }
+    if (last_pass)
+        out[p] = make_float4(ax / spp, ay / spp, az / spp, 1.0f);
+    else
+        acc[p] = make_float4(ax, ay, az, 0.0f);
+}
+
+// gathered: shard_count slabs of max_rows*W float4; image: H*W float4.
+__global__ void rt_assemble_kernel(const float4* __restrict__ gathered, uint32_t max_rows,
+                                   float4* __restrict__ image, uint32_t width, uint32_t height,
+                                   uint32_t row_block, uint32_t shard_count) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)width * height) return;
+    const uint32_t y = (uint32_t)(i / width);
+    const uint32_t x = (uint32_t)(i - (size_t)y * width);
+    const uint32_t blk = y / row_block;
+    const uint32_t k = blk % shard_count;
+    const uint32_t r = (blk / shard_count) * row_block + (y % row_block);
+    image[i] = gathered[((size_t)k * max_rows + r) * width + x];
+}
+
+extern "C" {
+
+hipError_t rt_launch_render(const KParams* P, const float4* sph, const float2* sph_rm,
+                            const rt_material* mats, float4* block_sums, uint32_t* work_counter,
+                            unsigned long long* seg_counter, uint32_t grid, hipStream_t stream) {
+    hipLaunchKernelGGL(rt_render_kernel, dim3(grid), dim3(RT_BLOCK_THREADS), 0, stream, *P, sph,
+                       sph_rm, mats, block_sums, work_counter, seg_counter);
+    return hipGetLastError();
+}
+
+hipError_t rt_launch_collect(const float4* block_sums, uint32_t npix, uint32_t nblocks,
+                             float4* acc, int first_pass, int last_pass, float spp, float4* out,
+                             hipStream_t stream) {
+    const uint32_t T = 256;
+    hipLaunchKernelGGL(rt_collect_kernel, dim3((npix + T - 1) / T), dim3(T), 0, stream,
+                       block_sums, npix, nblocks, acc, first_pass, last_pass, spp, out);
+    return hipGetLastError();
+}
+
+hipError_t rt_launch_assemble(const float4* gathered, uint32_t max_rows, float4* image,
+                              uint32_t width, uint32_t height, uint32_t row_block,
+                              uint32_t shard_count, hipStream_t stream) {
+    const uint32_t T = 256;
+    const size_t n = (size_t)width * height;
+    hipLaunchKernelGGL(rt_assemble_kernel, dim3((uint32_t)((n + T - 1) / T)), dim3(T), 0, stream,
+                       gathered, max_rows, image, width, height, row_block, shard_count);
+    return hipGetLastError();
+}
+
+hipError_t rt_render_occupancy(int* blocks_per_cu) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_render_kernel,
+                                                        RT_BLOCK_THREADS, 0);
+}
+
+}  // extern "C"

@@ -1,0 +1,99 @@
+"""Host-side handle on one GPU: a thin owner of an `rt_ctx*` (include/rt_hip.h).
+
+This is the Python mirror of what the reference's render-world resources and
+RayTraceNode do per frame (src/plugin.rs:25-122, src/ray_trace_node.rs:195-224):
+upload the scene once, then render frames from a camera block + parameters.
+All compute happens in librt_hip.so on the GPU; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import abi
+from .abi import RtStats, check, make_params
+
+
+class Renderer:
+    def __init__(self, device: int = 0):
+        self.lib = abi.load()
+        ctx = ctypes.c_void_p()
+        rc = self.lib.rt_create(int(device), ctypes.byref(ctx))
+        check(self.lib, None, rc)
+        self.ctx = ctx
+        self.device = int(device)
+        self._keep = None
+        self.n_spheres = 0
+
+    def close(self):
+        if self.ctx:
+            self.lib.rt_destroy(self.ctx)
+            self.ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------------- scene
+    def set_scene(self, spheres: np.ndarray, materials: np.ndarray):
+        sp = np.ascontiguousarray(spheres, dtype=abi.SPHERE_DTYPE)
+        mt = np.ascontiguousarray(materials, dtype=abi.MATERIAL_DTYPE)
+        rc = self.lib.rt_set_scene(self.ctx, sp.ctypes.data_as(ctypes.c_void_p) if sp.size else None,
+                                   sp.size, mt.ctypes.data_as(ctypes.c_void_p) if mt.size else None,
+                                   mt.size)
+        check(self.lib, self.ctx, rc)
+        self.n_spheres = int(sp.size)
+
+    # --------------------------------------------------------------- render
+    def render(self, camera: np.ndarray, width, height, spp, max_depth, frame0=0, row_block=8,
+               shard_count=1, shard_index=0, flags=0):
+        """Synchronous render to a host array (rows, W, 4) float32 + stats dict."""
+        cam = np.ascontiguousarray(camera, dtype=abi.CAMERA_DTYPE)
+        p = make_params(width, height, spp, max_depth, frame0, row_block, shard_count, shard_index,
+                        flags)
+        rows = self.lib.rt_shard_rows(p.height, p.row_block, max(1, p.shard_count), p.shard_index)
+        out = np.empty((rows, int(width), 4), dtype=np.float32)
+        st = RtStats()
+        rc = self.lib.rt_render(self.ctx, cam.ctypes.data_as(ctypes.c_void_p), ctypes.byref(p),
+                                out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st))
+        check(self.lib, self.ctx, rc)
+        return out, st.as_dict()
+
+    def render_device(self, camera: np.ndarray, out_ptr: int, width, height, spp, max_depth,
+                      frame0=0, row_block=8, shard_count=1, shard_index=0, flags=0, stream=None):
+        """Enqueue a render into a device buffer (e.g. a torch tensor's data_ptr()).
+
+        `stream` is a raw hipStream_t handle (int) or None for the ctx stream.
+        Call wait() for the stats.
+        """
+        cam = np.ascontiguousarray(camera, dtype=abi.CAMERA_DTYPE)
+        p = make_params(width, height, spp, max_depth, frame0, row_block, shard_count, shard_index,
+                        flags)
+        self._keep = (cam, p)
+        rc = self.lib.rt_render_device(self.ctx, cam.ctypes.data_as(ctypes.c_void_p),
+                                       ctypes.byref(p), ctypes.c_void_p(int(out_ptr)),
+                                       ctypes.c_void_p(int(stream)) if stream else None)
+        check(self.lib, self.ctx, rc)
+
+    def wait(self):
+        st = RtStats()
+        rc = self.lib.rt_wait(self.ctx, ctypes.byref(st))
+        check(self.lib, self.ctx, rc)
+        return st.as_dict()
+
+    def assemble_shards(self, gathered_ptr: int, max_rows, image_ptr: int, width, height,
+                        row_block, shard_count, stream=None):
+        rc = self.lib.rt_assemble_shards(self.ctx, ctypes.c_void_p(int(gathered_ptr)), max_rows,
+                                         ctypes.c_void_p(int(image_ptr)), width, height,
+                                         row_block, shard_count,
+                                         ctypes.c_void_p(int(stream)) if stream else None)
+        check(self.lib, self.ctx, rc)

@@ -1,0 +1,195 @@
+/*
+ * rt_hip.h — C-ABI of the MI355X-native per-pixel path tracer.
+ *
+ * This is the drop-in boundary that replaces the reference's WGSL dispatch
+ * schedule. In brandon-reinhart/bevy_raytrace the per-frame work is recorded by
+ *   impl render_graph::Node for RayTraceNode { fn update(..); fn run(..) }
+ *   (src/ray_trace_node.rs:173-224)
+ * which dispatches clear / generate / 3x(prepass, intersect, shade) / collect
+ * (assets/shaders/{clear,generate,intersect,shade,collect}.wgsl) over buffers packed by the `prepare` systems of
+ * src/ray_trace_camera.rs:43-68, src/ray_trace_globals.rs:56-68,
+ * src/sphere.rs:166-197 and src/ray_trace_materials.rs:129-164.
+ *
+ * Here the whole chain is ONE persistent HIP kernel on gfx950 behind the entry
+ * points below. Plain pointers and sizes only; no torch / HIP types appear in
+ * the signatures (streams are passed as `void*` = hipStream_t).
+ *
+ * Byte layouts mirror the reference's encase/std430/std140 layouts exactly,
+ * so a Rust shim can hand over `encase`-packed bytes unchanged:
+ *   rt_sphere   = SphereGPU   (src/sphere.rs:12-17; intersect.wgsl:56-60), 32 B
+ *   rt_material = MaterialGPU (src/ray_trace_materials.rs:33-43; shade.wgsl:67-73), 32 B
+ *   rt_camera   = CameraGPU   (src/ray_trace_camera.rs:14-25; generate.wgsl:5-15), 128 B std140
+ *
+ * Error convention: every entry point returns an int status (RT_OK = 0,
+ * negative = error class) and never throws or aborts across the ABI; the
+ * message of the last failing call on a context is rt_last_error(ctx).
+ * (The reference panics via unwrap(), src/ray_trace_node.rs:51-53.)
+ *
+ * Threading: one rt_ctx per device; calls on one ctx must be serialised by the
+ * caller; distinct contexts may be used concurrently from different threads.
+ */
+#ifndef RT_HIP_H
+#define RT_HIP_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* status codes */
+#define RT_OK                 0
+#define RT_ERR_INVALID_ARG   -1   /* bad pointer / size / parameter            */
+#define RT_ERR_NO_SCENE      -2   /* rt_render before rt_set_scene             */
+#define RT_ERR_DEVICE        -3   /* HIP runtime error (message has details)   */
+#define RT_ERR_OUT_OF_MEMORY -4   /* device allocation failed                  */
+#define RT_ERR_BAD_SCENE     -5   /* material index / reflectance out of range */
+
+/* Reflectance codes, src/ray_trace_materials.rs:144-153 (Lambertian=0,
+ * Metallic=1, Dielectric=2), consumed by shade.wgsl:240-252. */
+#define RT_LAMBERTIAN 0
+#define RT_METALLIC   1
+#define RT_DIELECTRIC 2
+
+/* SphereGPU {center: Vec3, radius: f32, material: u32} in a std430 runtime
+ * array: 32-byte stride (src/sphere.rs:12-17). */
+typedef struct rt_sphere {
+    float    center[3];
+    float    radius;
+    uint32_t material;
+    uint32_t _pad[3];
+} rt_sphere;
+
+/* MaterialGPU {color: Vec4, reflectance: i32, fuzziness: f32,
+ * index_of_refraction: f32, pad2: i32} (src/ray_trace_materials.rs:33-43). */
+typedef struct rt_material {
+    float   color[4];
+    int32_t reflectance;
+    float   fuzziness;
+    float   index_of_refraction;
+    int32_t _pad;
+} rt_material;
+
+/* CameraGPU, std140, 128 B (src/ray_trace_camera.rs:14-25).
+ * transform is column-major (glam Mat4): transform[col*4 + row]. Only
+ * transform, fov, image_plane_distance and lens_focal_length are read by the
+ * path (generate.wgsl:67-126); forward/up/right/position/fstop are carried. */
+typedef struct rt_camera {
+    float transform[16];
+    float forward[3];  float fov;
+    float up[3];       float image_plane_distance;
+    float right[3];    float lens_focal_length;
+    float position[3]; float fstop;
+} rt_camera;
+
+/* Render parameters (replaces GlobalsGPU, src/ray_trace_globals.rs:11-24, and
+ * the compile-time schedule constants of src/lib.rs:25-26 and
+ * src/ray_trace_node.rs:213).
+ *   width, height : full image size (pixel/seed addressing is always global)
+ *   spp           : samples per pixel; sample s uses globals.frame = frame0+s
+ *   max_depth     : number of (intersect, shade) iterations D (reference: 3);
+ *                   a hit at bounce D-1 is killed black (shade.wgsl:236)
+ *   frame0        : frame index of sample 0 (the RNG seed input)
+ *   row_block, shard_count, shard_index :
+ *                   row tiling for multi-GPU. Rows are grouped in blocks of
+ *                   row_block rows; shard k owns blocks b with b % shard_count
+ *                   == k. The output of a call holds only the owned rows, in
+ *                   increasing y, packed. shard_count = 1 -> whole image.
+ *   flags         : RT_FLAG_* bits.                                          */
+typedef struct rt_params {
+    uint32_t width;
+    uint32_t height;
+    uint32_t spp;
+    uint32_t max_depth;
+    uint32_t frame0;
+    uint32_t row_block;
+    uint32_t shard_count;
+    uint32_t shard_index;
+    uint32_t flags;
+    uint32_t _reserved[3];
+} rt_params;
+
+/* Sample accumulation order (part of the result definition, not a tuning
+ * knob): the S per-sample colours of a pixel are summed in f32 sequentially
+ * inside blocks of RT_SAMPLE_BLOCK consecutive samples; the block sums are
+ * folded in f32 in block order; the pixel is that sum / f32(S)
+ * (collect.wgsl:114-122 generalised to S > 1). */
+#define RT_SAMPLE_BLOCK 8
+
+/* flags */
+#define RT_FLAG_NO_PRIMARY_CACHE 0x1u  /* trace the primary ray for every sample
+                                          (off by default: the primary ray is
+                                          pixel-only, Appendix B Q1/Q3, so its
+                                          hit is reused across the samples of a
+                                          sample block; results are identical) */
+
+/* Per-call statistics. */
+typedef struct rt_stats {
+    uint64_t segments;         /* algorithmic ray segments = intersect_world calls
+                                  on live rays (intersect.wgsl:154-158)          */
+    uint64_t traced_segments;  /* segments actually intersected on the GPU       */
+    uint64_t sphere_tests;     /* traced_segments * sphere_count                  */
+    uint64_t paths;            /* pixels * spp                                    */
+    double   kernel_ms;        /* sum of render-kernel durations (HIP events)     */
+    double   total_ms;         /* whole call incl. collect / copies               */
+    uint32_t kernel_launches;  /* number of render-kernel launches                */
+    uint32_t _pad;
+} rt_stats;
+
+typedef struct rt_ctx rt_ctx;
+
+/* Library / ABI version (RT_ABI_VERSION). */
+int rt_version(void);
+
+/* Number of rows owned by a shard (see rt_params). Pure host arithmetic. */
+uint32_t rt_shard_rows(uint32_t height, uint32_t row_block,
+                       uint32_t shard_count, uint32_t shard_index);
+
+/* Create a context on HIP device `device` (replaces RayTracePlugin::build +
+ * RayTracePipeline::from_world, src/plugin.rs:25-47, ray_trace_pipeline.rs:171-211). */
+int rt_create(int device, rt_ctx** out_ctx);
+void rt_destroy(rt_ctx* ctx);
+
+/* Upload the scene (replaces sphere.rs:180-197 and ray_trace_materials.rs:129-164).
+ * Arrays are borrowed and copied during the call. Sphere order = list order =
+ * tie-break order of intersect_world (intersect.wgsl:135-139). n may be 0. */
+int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n,
+                 const rt_material* materials, uint32_t m);
+
+/* Render one frame (replaces RayTraceNode::run, src/ray_trace_node.rs:195-224).
+ * Synchronous. out_rgba: caller-owned HOST buffer of
+ * rt_shard_rows(...) * width * 4 floats (Rgba32Float, row-major, alpha 1,
+ * linear; collect.wgsl:122). stats may be NULL. */
+int rt_render(rt_ctx* ctx, const rt_camera* camera, const rt_params* params,
+              float* out_rgba, rt_stats* stats);
+
+/* Same, but the output is a DEVICE pointer on this ctx's device and the work
+ * is enqueued on `stream` (hipStream_t, NULL = the ctx's own stream).
+ * Returns after enqueueing; call rt_wait() before reading stats. */
+int rt_render_device(rt_ctx* ctx, const rt_camera* camera, const rt_params* params,
+                     float* out_rgba_device, void* stream);
+
+/* Asynchronous host-output variant: enqueue, return; rt_wait() completes the
+ * device->host copy into out_rgba and fills stats. */
+int rt_render_async(rt_ctx* ctx, const rt_camera* camera, const rt_params* params,
+                    float* out_rgba);
+int rt_wait(rt_ctx* ctx, rt_stats* stats);
+
+/* Re-assemble gathered shard outputs into the full image on the device:
+ * gathered = shard_count consecutive slabs of max_rows*width*4 floats (slab k =
+ * shard k's output, padded to max_rows rows); image = height*width*4 floats. */
+int rt_assemble_shards(rt_ctx* ctx, const float* gathered_device, uint32_t max_rows,
+                       float* image_device, uint32_t width, uint32_t height,
+                       uint32_t row_block, uint32_t shard_count, void* stream);
+
+/* Message for the last failing call on ctx (or on the library when ctx is NULL). */
+const char* rt_last_error(const rt_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_HIP_H */
