@@ -44,7 +44,7 @@ struct rt_ctx {
 
     // scene
     bool has_scene = false;
-    uint32_t n = 0, m = 0;
+    uint32_t n = 0, ngroups = 0, m = 0;
     float4* d_sph = nullptr;        // (cx, cy, cz, r*r)
     float2* d_sph_rm = nullptr;     // (radius, material bits)
     rt_material* d_mats = nullptr;
@@ -57,9 +57,9 @@ struct rt_ctx {
     size_t acc_cap = 0;
     float4* d_out = nullptr;        // host-output path staging
     size_t out_cap = 0;
-    uint32_t* d_counters = nullptr; // [0..1] u64 segment counter, [2..] per-pass work counters
+    uint32_t* d_counters = nullptr; // [0..3] 2 x u64 segment counters, [4..] per-pass work counters
     size_t counters_cap = 0;        // in u32 words
-    unsigned long long* h_segs = nullptr;  // pinned
+    unsigned long long* h_segs = nullptr;  // pinned, 2 counters
     std::vector<hipEvent_t> ev;     // 2 per pass
     hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;
 
@@ -157,7 +157,7 @@ int rt_create(int device, rt_ctx** out_ctx) {
                                        device)) != hipSuccess)
             break;
         if ((e = rt_render_occupancy(&ctx->blocks_per_cu)) != hipSuccess) break;
-        if ((e = hipHostMalloc((void**)&ctx->h_segs, sizeof(unsigned long long))) != hipSuccess) break;
+        if ((e = hipHostMalloc((void**)&ctx->h_segs, 2 * sizeof(unsigned long long))) != hipSuccess) break;
         if ((e = hipEventCreate(&ctx->ev_t0)) != hipSuccess) break;
         if ((e = hipEventCreate(&ctx->ev_t1)) != hipSuccess) break;
     } while (0);
@@ -202,8 +202,13 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n, const rt_mat
         if (r < RT_LAMBERTIAN || r > RT_DIELECTRIC)
             return fail(ctx, RT_ERR_BAD_SCENE, "material %u: reflectance %d not in {0,1,2}", j, r);
     }
-    std::vector<float4> sph(n);
-    std::vector<float2> rm(n);
+    // Sphere stream for the kernel's scalar-load loop: (cx, cy, cz, r*r) records
+    // padded to a whole number of groups of 4 plus one extra group (prefetch
+    // reach); pad records have r^2 = -inf, which the filter never passes.
+    const uint32_t ngroups = (n + 3) / 4;
+    const size_t nrec = (size_t)(ngroups + 1) * 4;
+    std::vector<float4> sph(nrec, make_float4(0.0f, 0.0f, 0.0f, -INFINITY));
+    std::vector<float2> rm(n ? n : 1, make_float2(0.0f, 0.0f));
     for (uint32_t i = 0; i < n; ++i) {
         const rt_sphere& s = spheres[i];
         if (s.material >= m)
@@ -218,19 +223,18 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n, const rt_mat
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if (ctx->pending && ctx->pending_stream) HIP_TRY(ctx, hipStreamSynchronize(ctx->pending_stream));
-    int rc = ensure(ctx, &ctx->d_sph, &ctx->sph_cap, sizeof(float4) * (size_t)n);
+    int rc = ensure(ctx, &ctx->d_sph, &ctx->sph_cap, sizeof(float4) * nrec);
     if (rc) return rc;
-    rc = ensure(ctx, &ctx->d_sph_rm, &ctx->sph_rm_cap, sizeof(float2) * (size_t)n);
+    rc = ensure(ctx, &ctx->d_sph_rm, &ctx->sph_rm_cap, sizeof(float2) * rm.size());
     if (rc) return rc;
     rc = ensure(ctx, &ctx->d_mats, &ctx->mat_cap, sizeof(rt_material) * (size_t)m);
     if (rc) return rc;
-    if (n) {
-        HIP_TRY(ctx, hipMemcpy(ctx->d_sph, sph.data(), sizeof(float4) * n, hipMemcpyHostToDevice));
-        HIP_TRY(ctx, hipMemcpy(ctx->d_sph_rm, rm.data(), sizeof(float2) * n, hipMemcpyHostToDevice));
-    }
+    HIP_TRY(ctx, hipMemcpy(ctx->d_sph, sph.data(), sizeof(float4) * nrec, hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(ctx->d_sph_rm, rm.data(), sizeof(float2) * rm.size(), hipMemcpyHostToDevice));
     if (m)
         HIP_TRY(ctx, hipMemcpy(ctx->d_mats, materials, sizeof(rt_material) * m, hipMemcpyHostToDevice));
     ctx->n = n;
+    ctx->ngroups = ngroups;
     ctx->m = m;
     ctx->has_scene = true;
     return RT_OK;
@@ -277,7 +281,7 @@ static int enqueue(rt_ctx* ctx, const rt_camera* cam, const rt_params* prm, floa
             if (rc) return rc;
         }
     }
-    const size_t words = 2 + passes.size();
+    const size_t words = 4 + passes.size();
     const size_t words_pad = (words + 3) & ~(size_t)3;  // 16-B multiple
     {
         int rc = ensure(ctx, &ctx->d_counters, &ctx->counters_cap, words_pad * sizeof(uint32_t));
@@ -300,6 +304,7 @@ static int enqueue(rt_ctx* ctx, const rt_camera* cam, const rt_params* prm, floa
     K_.shard_index = p.shard_index;
     K_.npix = npix;
     K_.nspheres = ctx->n;
+    K_.ngroups = ctx->ngroups;
     K_.flags = p.flags;
     std::memcpy(K_.T, cam->transform, sizeof(K_.T));
     K_.tan_half = (float)std::tan((double)(cam->fov / 2.0f));                 // generate.wgsl:67
@@ -321,14 +326,14 @@ static int enqueue(rt_ctx* ctx, const rt_camera* cam, const rt_params* prm, floa
         const uint32_t grid = (uint32_t)(need_blocks < grid_full ? need_blocks : grid_full);
         HIP_TRY(ctx, hipEventRecord(ctx->ev[2 * i], stream));
         HIP_TRY(ctx, rt_launch_render(&K_, ctx->d_sph, ctx->d_sph_rm, ctx->d_mats, ctx->d_block_sums,
-                                      ctx->d_counters + 2 + i,
+                                      ctx->d_counters + 4 + i,
                                       reinterpret_cast<unsigned long long*>(ctx->d_counters),
                                       grid, stream));
         HIP_TRY(ctx, hipEventRecord(ctx->ev[2 * i + 1], stream));
         HIP_TRY(ctx, rt_launch_collect(ctx->d_block_sums, npix, K_.nblocks, ctx->d_acc, i == 0,
                                        i + 1 == passes.size(), (float)p.spp, d_out, stream));
     }
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_segs, ctx->d_counters, sizeof(unsigned long long),
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_segs, ctx->d_counters, 2 * sizeof(unsigned long long),
                                 hipMemcpyDeviceToHost, stream));
     *out_passes = (uint32_t)passes.size();
     *out_paths = (uint64_t)npix * p.spp;
@@ -348,8 +353,8 @@ static int finish(rt_ctx* ctx, uint32_t passes, uint64_t paths, rt_stats* st) {
     }
     float tms = 0.0f;
     HIP_TRY(ctx, hipEventElapsedTime(&tms, ctx->ev_t0, ctx->ev_t1));
-    st->traced_segments = *ctx->h_segs;
-    st->segments = *ctx->h_segs;
+    st->segments = ctx->h_segs[0];
+    st->traced_segments = ctx->h_segs[1];
     st->sphere_tests = st->traced_segments * (uint64_t)ctx->n;
     st->paths = paths;
     st->kernel_ms = kms;

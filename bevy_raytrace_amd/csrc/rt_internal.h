@@ -8,6 +8,9 @@
 
 #define RT_BLOCK_THREADS 256  // 4 waves per workgroup
 #define RT_WAVE_CHUNK 64      // work items a wave takes per atomic
+#ifndef RT_MIN_WAVES_PER_SIMD
+#define RT_MIN_WAVES_PER_SIMD 4
+#endif
 
 // Kernel parameters (by value; lands in SGPRs). Camera constants are
 // precomputed on the host exactly as generate.wgsl:67-95 computes them.
@@ -18,6 +21,7 @@ struct KParams {
     uint32_t block_begin;  // first sample block of this pass
     uint32_t nblocks;      // sample blocks in this pass
     uint32_t nspheres;
+    uint32_t ngroups;      // padded sphere groups of 4 (see rt_set_scene)
     uint32_t flags;
     float T[16];           // camera transform, column-major
     float tan_half, focus_plane, aspect, half_w, half_h;

@@ -107,15 +107,22 @@ __device__ __forceinline__ v3 reflect(v3 v, v3 n) {  // shade.wgsl:132-134
 }
 
 // Exact reference test of one sphere (intersect.wgsl:97-115 + :137).
+// s.w = RN(radius*radius) = sqr(s.radius); r2p = s.w * (1 + 2^-20).
 __device__ __forceinline__ void exact_test(float4 s, int idx, v3 o, v3 d, float a,
                                            float& best_t, int& best_i) {
-    v3 oc = mk(o.x - s.x, o.y - s.y, o.z - s.z);
-    float half_b = dot(oc, d);
-    float lo = length(oc);
-    float c = lo * lo - s.w;  // s.w = RN(radius*radius) = sqr(s.radius)
-    float dis = half_b * half_b - a * c;
+    const v3 oc = mk(o.x - s.x, o.y - s.y, o.z - s.z);
+    const float half_b = dot(oc, d);
+    const float qq = dot(oc, oc);
+    // Cheap certain-miss: centre behind the origin (half_b >= 0) and origin
+    // outside (qq >= r^2 (1 + 2^-20) => c >= 0 after the sqrt/square round
+    // trip). Then dis <= half_b^2, sqrt(dis) <= half_b, and both roots are
+    // <= 0 < EPSILON, exactly as the full evaluation below would find.
+    if (half_b >= 0.0f && qq >= s.w * (1.0f + 0x1p-20f)) return;
+    const float lo = sqrtf(qq);
+    const float c = lo * lo - s.w;
+    const float dis = half_b * half_b - a * c;
     if (dis < 0.0f) return;
-    float sqrtd = sqrtf(dis);
+    const float sqrtd = sqrtf(dis);
     float root = (-half_b - sqrtd) / a;
     if (root < EPSILON || VERY_FAR < root) {
         root = (-half_b + sqrtd) / a;
@@ -129,15 +136,17 @@ __device__ __forceinline__ void exact_test(float4 s, int idx, v3 o, v3 d, float 
 
 // Conservative filter value; G < 0 => certain miss (see file header).
 __device__ __forceinline__ float filter_g(float4 s, v3 o, v3 dn, float negk) {
-    float ocx = o.x - s.x, ocy = o.y - s.y, ocz = o.z - s.z;
-    float hb = __builtin_fmaf(ocz, dn.z, __builtin_fmaf(ocy, dn.y, ocx * dn.x));
-    float q = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx));
+    const float ocx = o.x - s.x, ocy = o.y - s.y, ocz = o.z - s.z;
+    const float hb = __builtin_fmaf(ocz, dn.z, __builtin_fmaf(ocy, dn.y, ocx * dn.x));
+    const float q = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx));
     return __builtin_fmaf(negk, q, __builtin_fmaf(hb, hb, s.w));
 }
 
-// Closest hit over the whole list. Returns best index (-1 = miss) and t.
-__device__ __forceinline__ int intersect_world(const float4* __restrict__ sph, uint32_t n, v3 o,
-                                               v3 d, float& t_out) {
+// Closest hit over the whole list (intersect.wgsl:133-143). `sph` is padded
+// to a multiple of 4 records plus one extra group of 4, the pad records having
+// r^2 = -inf (G = -inf: never candidates). Returns best index (-1 = miss), t.
+__device__ __forceinline__ int intersect_world(const float4* __restrict__ sph, uint32_t ngroups,
+                                               v3 o, v3 d, float& t_out) {
     const float dd = dot(d, d);
     const float l = sqrtf(dd);
     const float a = l * l;                        // sqr(length(r.dir)), intersect.wgsl:98
@@ -146,24 +155,22 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ sph, u
     const float negk = -(1.0f - 0x1p-16f);
     float best_t = VERY_FAR;
     int best_i = -1;
-    uint32_t i = 0;
-    for (; i + 4 <= n; i += 4) {
-        const float4 s0 = sph[i], s1 = sph[i + 1], s2 = sph[i + 2], s3 = sph[i + 3];
-        const float g0 = filter_g(s0, o, dn, negk);
-        const float g1 = filter_g(s1, o, dn, negk);
-        const float g2 = filter_g(s2, o, dn, negk);
-        const float g3 = filter_g(s3, o, dn, negk);
-        const bool c0 = !(g0 < 0.0f), c1 = !(g1 < 0.0f), c2 = !(g2 < 0.0f), c3 = !(g3 < 0.0f);
-        if (c0 | c1 | c2 | c3) {
-            if (c0) exact_test(s0, (int)i, o, d, a, best_t, best_i);
-            if (c1) exact_test(s1, (int)i + 1, o, d, a, best_t, best_i);
-            if (c2) exact_test(s2, (int)i + 2, o, d, a, best_t, best_i);
-            if (c3) exact_test(s3, (int)i + 3, o, d, a, best_t, best_i);
+    float4 n0 = sph[0], n1 = sph[1], n2 = sph[2], n3 = sph[3];
+    for (uint32_t g = 0; g < ngroups; ++g) {
+        const float4 s0 = n0, s1 = n1, s2 = n2, s3 = n3;
+        const uint32_t i = g * 4;
+        n0 = sph[i + 4]; n1 = sph[i + 5]; n2 = sph[i + 6]; n3 = sph[i + 7];  // prefetch
+        const uint64_t m0 = __ballot(!(filter_g(s0, o, dn, negk) < 0.0f));
+        const uint64_t m1 = __ballot(!(filter_g(s1, o, dn, negk) < 0.0f));
+        const uint64_t m2 = __ballot(!(filter_g(s2, o, dn, negk) < 0.0f));
+        const uint64_t m3 = __ballot(!(filter_g(s3, o, dn, negk) < 0.0f));
+        if ((m0 | m1 | m2 | m3) != 0) {
+            const uint64_t me = 1ull << __lane_id();
+            if (m0 & me) exact_test(s0, (int)i, o, d, a, best_t, best_i);
+            if (m1 & me) exact_test(s1, (int)i + 1, o, d, a, best_t, best_i);
+            if (m2 & me) exact_test(s2, (int)i + 2, o, d, a, best_t, best_i);
+            if (m3 & me) exact_test(s3, (int)i + 3, o, d, a, best_t, best_i);
         }
-    }
-    for (; i < n; ++i) {
-        const float4 s = sph[i];
-        if (!(filter_g(s, o, dn, negk) < 0.0f)) exact_test(s, (int)i, o, d, a, best_t, best_i);
     }
     t_out = best_t;
     return best_i;
@@ -213,19 +220,92 @@ __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint
     start_sample(P, st);
 }
 
-__global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_render_kernel(
+// One path step after an intersection: shade.wgsl:199-258 for hit `hi` at t.
+// Returns true when the path has finished (miss, or hit at bounce D-1).
+__device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, float t,
+                                      const float4* __restrict__ sph,
+                                      const float2* __restrict__ sph_rm,
+                                      const rt_material* __restrict__ mats) {
+    if (hi < 0) {  // miss, shade.wgsl:229-233
+        st.color = mul(st.color, sky(st.d));
+        return true;
+    }
+    if (st.bounce == P.max_depth - 1) {  // shade.wgsl:236-238
+        st.color = mk(0.0f, 0.0f, 0.0f);
+        return true;
+    }
+    const float4 s = sph[hi];
+    const float2 rm = sph_rm[hi];
+    const float radius = rm.x;
+    const uint32_t mi = __float_as_uint(rm.y);
+    // hit record, intersect.wgsl:117-127
+    const v3 pos = add(st.o, scale(st.d, t));
+    const v3 q = sub(pos, mk(s.x, s.y, s.z));
+    v3 nrm = normalize(mk(q.x / radius, q.y / radius, q.z / radius));
+    bool front = true;
+    if (dot(st.d, nrm) > 0.0f) {
+        nrm = neg(nrm);
+        front = false;
+    }
+    const rt_material& m = mats[mi];
+    const int refl = m.reflectance;
+    if (refl == RT_LAMBERTIAN) {  // shade.wgsl:118-130
+        const v3 dest = add(add(pos, nrm), st.nseed);
+        st.d = normalize(sub(dest, pos));
+        st.o = pos;
+        st.color = mul(st.color, mk(m.color[0], m.color[1], m.color[2]));
+    } else if (refl == RT_METALLIC) {  // shade.wgsl:136-146
+        const v3 e_origin = add(pos, scale(nrm, EPSILON));
+        const v3 reflected = normalize(reflect(st.d, nrm));
+        const v3 noise = scale(st.nseed, m.fuzziness);
+        st.d = normalize(add(reflected, noise));
+        st.o = e_origin;
+        st.color = mul(st.color, mk(m.color[0], m.color[1], m.color[2]));
+    } else {  // dielectric, shade.wgsl:163-187 (attenuation 1)
+        const float ior = m.index_of_refraction;
+        float ratio = ior;
+        if (front) ratio = 1.0f / ior;
+        const v3 unit_dir = normalize(st.d);
+        const float cos_theta = fminf(dot(neg(unit_dir), nrm), 1.0f);
+        const float sin_theta = sqrtf(1.0f - cos_theta * cos_theta);
+        const bool cannot_refract = ratio * sin_theta > 1.0f;
+        float r0 = (1.0f - ratio) / (1.0f + ratio);  // reflectance(), shade.wgsl:156-161
+        r0 = r0 * r0;
+        const float xr = 1.0f - cos_theta;
+        const float x2 = xr * xr;
+        const float refl_p = r0 + (1.0f - r0) * ((x2 * x2) * xr);
+        v3 e_dir;
+        if (cannot_refract || refl_p > st.seedx) {
+            e_dir = reflect(st.d, nrm);
+        } else {  // refract, shade.wgsl:148-154
+            const float ct = fminf(dot(neg(unit_dir), nrm), 1.0f);
+            const v3 perp = scale(add(unit_dir, scale(nrm, ct)), ratio);
+            const float lp = length(perp);
+            const float par = -sqrtf(fabsf(1.0f - (lp * lp)));
+            e_dir = normalize(add(perp, scale(nrm, par)));
+        }
+        st.o = add(pos, scale(nrm, EPSILON));
+        st.d = e_dir;
+    }
+    ++st.bounce;
+    return false;
+}
+
+__global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_render_kernel(
     KParams P, const float4* __restrict__ sph, const float2* __restrict__ sph_rm,
     const rt_material* __restrict__ mats, float4* __restrict__ block_sums,
     uint32_t* __restrict__ work_counter, unsigned long long* __restrict__ seg_counter) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t total = P.npix * P.nblocks;
-    const uint32_t D = P.max_depth;
+    const bool use_cache = (P.flags & RT_FLAG_NO_PRIMARY_CACHE) == 0;
 
     PathState st;
     bool has_item = false;
     uint32_t q_next = 0, q_end = 0;  // wave-uniform chunk of work items
     bool exhausted = false;
-    uint32_t segs = 0;
+    uint32_t traced = 0, segs = 0;
+    int cache_hi = -1;      // primary hit of this item's pixel (generate.wgsl: pixel-only ray)
+    float cache_t = 0.0f;
 
     for (;;) {
         // ---- refill: lanes without an item take the next ones (wave ballot)
@@ -254,81 +334,36 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_render_kernel(
         }
         if (__ballot(has_item) == 0) break;
 
+        // ---- intersect (intersect.wgsl:145-163): every lane with an item holds
+        // a ray that needs tracing here.
+        int hi = -1;
+        float t = VERY_FAR;
         if (has_item) {
-            // ---- intersect (intersect.wgsl:145-163)
-            float t;
-            const int hi = intersect_world(sph, P.nspheres, st.o, st.d, t);
-            ++segs;
-            bool done = false;
-            // ---- shade (shade.wgsl:199-258)
-            if (hi < 0) {
-                st.color = mul(st.color, sky(st.d));
-                done = true;
-            } else if (st.bounce == D - 1) {
-                st.color = mk(0.0f, 0.0f, 0.0f);
-                done = true;
-            } else {
-                const float4 s = sph[hi];
-                const float2 rm = sph_rm[hi];
-                const float radius = rm.x;
-                const uint32_t mi = __float_as_uint(rm.y);
-                // hit record, intersect.wgsl:117-127
-                const v3 pos = add(st.o, scale(st.d, t));
-                const v3 q = sub(pos, mk(s.x, s.y, s.z));
-                v3 nrm = normalize(mk(q.x / radius, q.y / radius, q.z / radius));
-                bool front = true;
-                if (dot(st.d, nrm) > 0.0f) {
-                    nrm = neg(nrm);
-                    front = false;
-                }
-                const float4 mc = *reinterpret_cast<const float4*>(mats[mi].color);
-                const int refl = mats[mi].reflectance;
-                if (refl == 0) {  // lambertian, shade.wgsl:118-130
-                    const v3 dest = add(add(pos, nrm), st.nseed);
-                    st.d = normalize(sub(dest, pos));
-                    st.o = pos;
-                    st.color = mul(st.color, mk(mc.x, mc.y, mc.z));
-                } else if (refl == 1) {  // metallic, shade.wgsl:136-146
-                    const v3 e_origin = add(pos, scale(nrm, EPSILON));
-                    const v3 reflected = normalize(reflect(st.d, nrm));
-                    const v3 noise = scale(st.nseed, mats[mi].fuzziness);
-                    st.d = normalize(add(reflected, noise));
-                    st.o = e_origin;
-                    st.color = mul(st.color, mk(mc.x, mc.y, mc.z));
-                } else {  // dielectric, shade.wgsl:163-187
-                    const float ior = mats[mi].index_of_refraction;
-                    float ratio = ior;
-                    if (front) ratio = 1.0f / ior;
-                    const v3 unit_dir = normalize(st.d);
-                    const float cos_theta = fminf(dot(neg(unit_dir), nrm), 1.0f);
-                    const float sin_theta = sqrtf(1.0f - cos_theta * cos_theta);
-                    const bool cannot_refract = ratio * sin_theta > 1.0f;
-                    float r0 = (1.0f - ratio) / (1.0f + ratio);
-                    r0 = r0 * r0;
-                    const float xr = 1.0f - cos_theta;
-                    const float x2 = xr * xr;
-                    const float refl_p = r0 + (1.0f - r0) * ((x2 * x2) * xr);
-                    v3 e_dir;
-                    if (cannot_refract || refl_p > st.seedx) {
-                        e_dir = reflect(st.d, nrm);
-                    } else {  // refract, shade.wgsl:148-154
-                        const float ct = fminf(dot(neg(unit_dir), nrm), 1.0f);
-                        const v3 perp = scale(add(unit_dir, scale(nrm, ct)), ratio);
-                        const float lp = length(perp);
-                        const float par = -sqrtf(fabsf(1.0f - (lp * lp)));
-                        e_dir = normalize(add(perp, scale(nrm, par)));
-                    }
-                    st.o = add(pos, scale(nrm, EPSILON));
-                    st.d = e_dir;
-                }
-                ++st.bounce;
+            hi = intersect_world(sph, P.ngroups, st.o, st.d, t);
+            ++traced;
+            if (st.bounce == 0) {  // first sample of the block: remember the primary hit
+                cache_hi = hi;
+                cache_t = t;
             }
+        }
+        // ---- shade; a finished path starts the next sample, whose primary hit
+        // is reused (result-identical) so the lane goes on to its bounce-1 ray.
+        bool shading = has_item;
+        while (shading) {
+            ++segs;
+            const bool done = shade(P, st, hi, t, sph, sph_rm, mats);
+            shading = false;
             if (done) {
                 // path finished: accumulate (collect.wgsl:115-120, blocked)
                 st.bsum = add(st.bsum, st.color);
                 ++st.s;
                 if (st.s < st.s_end) {
                     start_sample(P, st);
+                    if (use_cache) {
+                        hi = cache_hi;
+                        t = cache_t;
+                        shading = true;
+                    }
                 } else {
                     block_sums[st.item] = make_float4(st.bsum.x, st.bsum.y, st.bsum.z, 0.0f);
                     has_item = false;
@@ -337,10 +372,16 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_render_kernel(
         }
     }
 
-    // ---- segment count: wave reduce, one atomic per wave
-    unsigned long long v = segs;
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    if (lane == 0) atomicAdd(seg_counter, v);
+    // ---- segment counts: wave reduce, one atomic per wave
+    unsigned long long v = segs, w = traced;
+    for (int off = 32; off > 0; off >>= 1) {
+        v += __shfl_xor(v, off);
+        w += __shfl_xor(w, off);
+    }
+    if (lane == 0) {
+        atomicAdd(seg_counter, v);
+        atomicAdd(seg_counter + 1, w);
+    }
 }
 
 // Fold this pass's block sums into acc (block order) and, on the last pass,
