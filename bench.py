@@ -1,0 +1,244 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mrays/s + % fp32 roofline, RTIOW final scene 1920x1080 @64spp.
+
+One step = one frame of the hot path: every pixel x spp paths
+through the persistent HIP kernel, depth 16, written to an HBM image. Inputs
+(scene, camera) are resident on the device before timing starts.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config rtiow1080]
+
+N > 1 is launched by torch.distributed.run (one process per GPU): the image
+is row-tiled in interleaved blocks, each rank renders its rows,
+then one RCCL gather over xGMI lands the shards on rank 0, which re-assembles
+the image on the device. Timing: barrier + synchronize around exactly K steps,
+max over ranks. value = algorithmic ray segments of the whole frame (all ranks)
+per second, every segment traced (primary-hit reuse off for the headline;
+its frame time is reported separately as `primary_reuse`).
+
+Roofline: fp32 VALU. achieved = traced segments x 18 x N_spheres flops per
+render launch / that launch's average duration (HIP events on the stream the
+kernel runs on); peak = 157.3 TFLOP/s (MI355X fp32 vector = f32 MFMA peak,
+/opt/skills/guides/MI355X_MICROARCH.md). HBM traffic from rocprofv3 PMC
+counters is read from profiles/ (see DESIGN.md "Measurement").
+
+cpu_baseline: the C oracle (oracle/, a scalar port of the WGSL) timed on this
+host on a bounded row sample of the same frame, rank 0 at N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from bevy_raytrace_amd import abi  # noqa: E402
+from bevy_raytrace_amd.camera import default_camera_block  # noqa: E402
+from bevy_raytrace_amd.configs import HEADLINE, WORKLOADS, pick_row_block  # noqa: E402
+
+METRIC = "Mrays/s + % fp32 roofline, RTIOW final scene 1920×1080 @64spp, 1/2/4/8 GPU"
+PEAK_FP32_TFLOPS = 157.3
+FLOPS_PER_SPHERE_TEST = 18  # intersect.wgsl:97-102, SURVEY §8d
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default=HEADLINE, choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-rows", type=int, default=0,
+                    help="rows of the frame in the CPU sample (0 = auto, ~10 s)")
+    ap.add_argument("--reuse-steps", type=int, default=3,
+                    help="extra frames timed with primary-hit reuse on (0 = skip)")
+    return ap.parse_args()
+
+
+def load_traffic(workload_key):
+    """HBM bytes per render launch from the committed rocprofv3 PMC summary."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(workload_key, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print(f"--gpus {args.gpus} needs torch.distributed.run (one process per GPU)",
+                  file=sys.stderr)
+            sys.exit(2)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from bevy_raytrace_amd.renderer import Renderer
+
+    wl = WORKLOADS[args.config]
+    sc = wl.make_scene()
+    spheres, mats = sc.objects_gpu(), sc.materials_gpu()
+    nsph = len(spheres)
+    cam = default_camera_block()
+    W, H, S, D = wl.width, wl.height, wl.spp, wl.max_depth
+    B = pick_row_block(H, world)
+    rows = abi.shard_rows(H, B, world, rank)
+    max_rows = max(len(abi.shard_rows(H, B, world, k)) for k in range(world))
+
+    r = Renderer(local)
+    r.set_scene(spheres, mats)
+    # All device work of a step runs on ONE dedicated stream (non-null handle,
+    # so the library enqueues on it rather than on its own stream).
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    image = torch.empty((H, W, 4), dtype=torch.float32, device="cuda") if rank == 0 else None
+    # N=1: the single shard is the image; render straight into it.
+    shard = image if world == 1 else torch.empty((max_rows, W, 4), dtype=torch.float32,
+                                                  device="cuda")
+    gathered = (torch.empty((world, max_rows, W, 4), dtype=torch.float32, device="cuda")
+                if (rank == 0 and world > 1) else None)
+
+    def step(flags):
+        r.render_device(cam, shard.data_ptr(), W, H, S, D, 0, B, world, rank, flags,
+                        stream=stream.cuda_stream)
+        if world > 1:
+            dist.gather(shard, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+            if rank == 0:
+                r.assemble_shards(gathered.data_ptr(), max_rows, image.data_ptr(), W, H, B, world,
+                                  stream=stream.cuda_stream)
+        return r.wait()
+
+    NO_REUSE = abi.RT_FLAG_NO_PRIMARY_CACHE
+
+    for _ in range(args.warmup):
+        step(NO_REUSE)
+
+    def timed(nsteps, flags):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        stats = [step(flags) for _ in range(nsteps)]
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        return dt, stats
+
+    dt, stats = timed(args.steps, NO_REUSE)
+    segs_local = sum(s["segments"] for s in stats)
+    traced_local = sum(s["traced_segments"] for s in stats)
+    kms = [s["kernel_ms"] for s in stats]
+    tot = torch.tensor([segs_local, traced_local], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(tot)
+    segs_all, traced_all = float(tot[0].item()), float(tot[1].item())
+
+    reuse = None
+    if args.reuse_steps > 0:
+        step(0)
+        rdt, rstats = timed(args.reuse_steps, 0)
+        reuse = {"frame_ms": round(rdt / args.reuse_steps * 1e3, 3),
+                 "kernel_ms": round(float(np.mean([s["kernel_ms"] for s in rstats])), 3),
+                 "traced_fraction": round(sum(s["traced_segments"] for s in rstats)
+                                          / max(1, sum(s["segments"] for s in rstats)), 4),
+                 "note": "RT_FLAG_NO_PRIMARY_CACHE off: the pixel-only primary hit is reused "
+                         "across a sample block (bit-identical image)"}
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    value = segs_all / dt / 1e6
+    ms_per_step = dt / args.steps * 1e3
+    kernel_ms = float(np.mean(kms))
+    launches = stats[-1]["kernel_launches"]
+    traced_per_launch = traced_local / args.steps / launches
+    flops_per_launch = traced_per_launch * FLOPS_PER_SPHERE_TEST * nsph
+    achieved = flops_per_launch / (kernel_ms / launches * 1e-3) / 1e12
+    traffic = load_traffic(wl.key)
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": f"synthetic: seeded RTIOW final scene ({nsph} spheres), camera (13,2,3)->0",
+        "config": {"workload": f"{wl.key}: {W}x{H} {S}spp depth {D}, {nsph} spheres",
+                   "width": W, "height": H, "spp": S, "max_depth": D, "spheres": nsph,
+                   "parallelism": f"row-tiled x{world} (blocks of {B} rows) + RCCL gather"
+                   if world > 1 else "single GPU"},
+        "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+                     "traffic": traffic,
+                     "kernel": "rt_render_kernel",
+                     "kernel_ms_per_launch": round(kernel_ms / launches, 3),
+                     "flops_per_launch": flops_per_launch,
+                     "basis": "traced segments x 18 x N_spheres (fp32 VALU; no MFMA)"},
+        "segments_per_frame": int(segs_all / args.steps),
+        "traced_segments_per_frame": int(traced_all / args.steps),
+        "primary_reuse": reuse,
+    }
+
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cam, spheres, mats, W, H, S, D, args.cpu_rows,
+                                           image.cpu().numpy())
+    print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(cam, spheres, mats, W, H, S, D, nrows, gpu_image):
+    """Time the C oracle (scalar port of the WGSL) on a bounded row sample."""
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    cores = max(1, min(16, os.cpu_count() or 1))
+    # calibrate on `cores` spread rows (one row per thread), then size the
+    # sample for ~10 s of wall time
+    rows = [int(i * H / cores) for i in range(cores)]
+    t0 = time.perf_counter()
+    _, segs = O.render_rows(cam, spheres, mats, W, H, S, D, rows, nthreads=cores)
+    t1 = time.perf_counter() - t0
+    if nrows <= 0:
+        nrows = int(max(cores, min(H, cores * 10.0 / max(t1, 1e-3))))
+    stride = max(1, H // nrows)
+    rows = list(range(0, H, stride))[:nrows]
+    t0 = time.perf_counter()
+    img, segs = O.render_rows(cam, spheres, mats, W, H, S, D, rows, nthreads=cores)
+    dt = time.perf_counter() - t0
+    exact = bool(np.array_equal(img, gpu_image[rows], equal_nan=True))
+    return {"value": round(segs / dt / 1e6, 3), "unit": "Mrays/s", "cores": cores, "kind": "port",
+            "sample": f"{len(rows)} rows (every {stride}th) of the same {W}x{H} {S}spp frame, "
+                      f"{segs} segments in {dt:.2f} s",
+            "gpu_rows_bit_exact": exact}
+
+
+if __name__ == "__main__":
+    main()

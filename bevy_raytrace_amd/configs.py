@@ -1,0 +1,49 @@
+"""The BASELINE.json workloads."""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+from . import scene as _scene
+
+SCENE_SEED = 20221015
+
+
+@dataclass(frozen=True)
+class Workload:
+    key: str
+    width: int
+    height: int
+    spp: int
+    max_depth: int
+    scene: str        # scene factory name in bevy_raytrace_amd.scene
+    gpus: int = 1
+    note: str = ""
+
+    def make_scene(self):
+        return getattr(_scene, self.scene)(SCENE_SEED) if self.scene != "config1_scene" \
+            else _scene.config1_scene()
+
+
+WORKLOADS = {
+    "config1": Workload("config1", 400, 225, 16, 8, "config1_scene", 1,
+                        "ground + Lambertian + glass + metal; the reference's CPU-runnable case"),
+    "rtiow1080": Workload("rtiow1080", 1920, 1080, 64, 16, "rtiow_final_scene", 1,
+                          "RTIOW final scene, headline metric config (BASELINE.json configs[1])"),
+    "rtiow4k": Workload("rtiow4k", 3840, 2160, 256, 32, "rtiow_final_scene", 1,
+                        "same scene, 4K, 256 spp, depth 32"),
+    "rtiow8k": Workload("rtiow8k", 7680, 4320, 1024, 16, "rtiow_final_scene", 8,
+                        "same scene, 8K, 1024 spp, row-tiled over 8 GPUs"),
+    "spheres10k1080": Workload("spheres10k1080", 1920, 1080, 128, 16, "ten_thousand_scene", 1,
+                               "10,000 spheres, 128 spp (sphere list streamed)"),
+}
+
+HEADLINE = "rtiow1080"
+
+
+def pick_row_block(height: int, shards: int, max_block: int = 8) -> int:
+    """Largest row block <= max_block that splits the image evenly over the
+    shards (interleaved blocks); falls back to max_block."""
+    for b in range(max_block, 0, -1):
+        if height % b == 0 and (height // b) % shards == 0:
+            return b
+    return max_block
