@@ -125,6 +125,21 @@ def header_symbols(path=HEADER_PATH):
     return sorted(set(re.findall(r"\b(rt_[a-z_]+)\s*\(", text)))
 
 
+def _share_torch_hip_runtime():
+    """One HIP runtime per process. PyTorch-ROCm bundles its own libamdhip64
+    (SONAME libamdhip64.so.7, loaded by path from torch/lib); librt_hip.so
+    needs libamdhip64.so.7. Pre-loading torch's copy RTLD_GLOBAL makes our
+    library bind to it, so device pointers, streams and the device list are
+    shared with torch whichever of the two is imported first."""
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return
+    cand = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    if os.path.exists(cand):
+        ctypes.CDLL(cand, mode=ctypes.RTLD_GLOBAL)
+
+
 def load(path=LIB_PATH):
     """Load librt_hip.so (raises if it was not built — no fallback)."""
     global _lib
@@ -134,6 +149,7 @@ def load(path=LIB_PATH):
         raise RuntimeError(
             f"{path} is missing: build the HIP library first (python -c "
             "'import __graft_entry__ as g; g.build()'). There is no CPU fallback.")
+    _share_torch_hip_runtime()
     lib = ctypes.CDLL(path)
     for name, (res, args) in _PROTOS.items():
         fn = getattr(lib, name)

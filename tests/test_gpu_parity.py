@@ -1,0 +1,204 @@
+"""GPU parity: librt_hip.so (the HIP kernel) against the CPU oracle.
+
+The bar is bit-exact: identical f32 images (NaN masks included) and identical
+algorithmic segment counts, on the same seeded inputs. At full BASELINE sizes
+the oracle checks sampled rows, plus size-independent properties
+(determinism, reuse on/off identity, multi-pass identity, shard assembly).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from bevy_raytrace_amd import abi, scene
+from bevy_raytrace_amd.camera import Transform, camera_block, default_camera_block
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+NO_REUSE = abi.RT_FLAG_NO_PRIMARY_CACHE
+
+
+def arrays(sc):
+    return sc.objects_gpu(), sc.materials_gpu()
+
+
+def check_exact(img, ref):
+    assert img.shape == ref.shape
+    same = np.array_equal(img, ref, equal_nan=True)
+    if not same:
+        bad = ~((img == ref) | (np.isnan(img) & np.isnan(ref)))
+        idx = np.argwhere(bad.any(-1))
+        raise AssertionError(f"{len(idx)} pixels differ, first {idx[:5].tolist()}")
+
+
+def glass_scene():
+    mats = scene.MaterialCache()
+    mats.insert("ground", scene.RayTraceMaterial((0.5, 0.5, 0.5, 1), scene.Reflectance.Lambertian, 1.0, 0))
+    mats.insert("glass", scene.RayTraceMaterial((1, 1, 1, 1), scene.Reflectance.Dielectric, 0.0, 1.5))
+    mats.insert("diamond", scene.RayTraceMaterial((1, 1, 1, 1), scene.Reflectance.Dielectric, 0.0, 2.4))
+    mats.insert("fuzz", scene.RayTraceMaterial((0.9, 0.8, 0.7, 1), scene.Reflectance.Metallic, 0.5, 0))
+    sp = [scene.Sphere((0, -1000, -1), 1000, 0), scene.Sphere((0, 1, 0), 1, 1),
+          scene.Sphere((0, 1, 0), -0.9, 1), scene.Sphere((-4, 1, 0), 1, 2),
+          scene.Sphere((4, 1, 0), 1, 3), scene.Sphere((2, 0.5, 2), 0.5, 2)]
+    return scene.Scene(sp, mats, "glass")
+
+
+CASES = [
+    # name, scene, W, H, spp, depth, frame0
+    ("config1_full", scene.config1_scene, 400, 225, 16, 8, 0),   # BASELINE configs[0]
+    ("reference_sched", scene.reference_scene, 320, 180, 1, 3, 11),  # the reference's own schedule
+    ("rtiow", scene.rtiow_final_scene, 192, 108, 12, 16, 0),
+    ("glass", glass_scene, 160, 90, 9, 12, 3),
+    ("ragged", scene.rtiow_final_scene, 67, 33, 5, 7, 2),
+    ("one_pixel", scene.config1_scene, 1, 1, 17, 8, 0),
+    ("depth1", scene.rtiow_final_scene, 64, 36, 3, 1, 0),
+    ("spheres10k", scene.ten_thousand_scene, 96, 54, 2, 8, 0),
+]
+
+
+@pytest.mark.parametrize("flags", [0, NO_REUSE], ids=["reuse", "noreuse"])
+@pytest.mark.parametrize("name,mk,W,H,S,D,f0", CASES, ids=[c[0] for c in CASES])
+def test_bit_exact(renderer, name, mk, W, H, S, D, f0, flags):
+    sp, mt = arrays(mk())
+    cam = default_camera_block()
+    renderer.set_scene(sp, mt)
+    img, st = renderer.render(cam, W, H, S, D, frame0=f0, flags=flags)
+    ref, segs = O.render(cam, sp, mt, W, H, S, D, frame0=f0)
+    check_exact(img, ref)
+    assert st["segments"] == segs
+    if flags & NO_REUSE:
+        assert st["traced_segments"] == segs
+    else:
+        assert st["traced_segments"] <= segs
+    assert (img[..., 3] == 1).all()
+
+
+def test_empty_scene(renderer):
+    from bevy_raytrace_amd.abi import MATERIAL_DTYPE, SPHERE_DTYPE
+    sp, mt = np.zeros(0, SPHERE_DTYPE), np.zeros(0, MATERIAL_DTYPE)
+    cam = default_camera_block()
+    renderer.set_scene(sp, mt)
+    img, st = renderer.render(cam, 33, 17, 3, 4)
+    ref, segs = O.render(cam, sp, mt, 33, 17, 3, 4)
+    check_exact(img, ref)
+    assert st["segments"] == segs == 33 * 17 * 3
+
+
+def test_other_camera(renderer):
+    sp, mt = arrays(scene.rtiow_final_scene())
+    cam = camera_block(Transform.from_xyz(-6.0, 3.0, 9.0).looking_at((1.0, 0.5, -1.0)))
+    renderer.set_scene(sp, mt)
+    img, st = renderer.render(cam, 120, 80, 6, 10)
+    ref, segs = O.render(cam, sp, mt, 120, 80, 6, 10)
+    check_exact(img, ref)
+    assert st["segments"] == segs
+
+
+def test_multi_pass_scratch_identical(renderer, monkeypatch):
+    """Block sums folded over several passes == one pass (sequential fold)."""
+    sp, mt = arrays(scene.config1_scene())
+    cam = default_camera_block()
+    renderer.set_scene(sp, mt)
+    one, st1 = renderer.render(cam, 80, 45, 40, 6)
+    monkeypatch.setenv("RT_SCRATCH_BYTES", str(80 * 45 * 16 * 2))  # 2 blocks per pass
+    many, st2 = renderer.render(cam, 80, 45, 40, 6)
+    assert st2["kernel_launches"] == 3 and st1["kernel_launches"] == 1
+    check_exact(many, one)
+    ref, segs = O.render(cam, sp, mt, 80, 45, 40, 6)
+    check_exact(one, ref)
+
+
+@pytest.mark.parametrize("K,B", [(2, 8), (3, 5), (8, 1)])
+def test_shards_and_device_assembly(renderer, K, B):
+    import torch
+    sp, mt = arrays(scene.rtiow_final_scene())
+    cam = default_camera_block()
+    W, H, S, D = 96, 61, 4, 8
+    renderer.set_scene(sp, mt)
+    full, stf = renderer.render(cam, W, H, S, D)
+    rows = [len(abi.shard_rows(H, B, K, k)) for k in range(K)]
+    mr = max(rows)
+    g = torch.zeros((K, mr, W, 4), dtype=torch.float32, device="cuda")
+    segs = 0
+    for k in range(K):
+        part, st = renderer.render(cam, W, H, S, D, row_block=B, shard_count=K, shard_index=k)
+        g[k, :rows[k]] = torch.from_numpy(part).cuda()
+        segs += st["segments"]
+        # device-output path writes the same shard
+        buf = torch.empty((rows[k], W, 4), dtype=torch.float32, device="cuda")
+        renderer.render_device(cam, buf.data_ptr(), W, H, S, D, 0, B, K, k)
+        renderer.wait()
+        assert torch.equal(buf.cpu(), torch.from_numpy(part)) or np.array_equal(
+            buf.cpu().numpy(), part, equal_nan=True)
+    img = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+    renderer.assemble_shards(g.data_ptr(), mr, img.data_ptr(), W, H, B, K)
+    torch.cuda.synchronize()
+    check_exact(img.cpu().numpy(), full)
+    assert segs == stf["segments"]
+
+
+def test_full_1080p64_properties(renderer):
+    """Headline config at full size: sampled-row parity (incl. NaN-path rows),
+    determinism, reuse on/off identity."""
+    sp, mt = arrays(scene.rtiow_final_scene())
+    cam = default_camera_block()
+    renderer.set_scene(sp, mt)
+    a, sa = renderer.render(cam, 1920, 1080, 64, 16)
+    b, sb = renderer.render(cam, 1920, 1080, 64, 16, flags=NO_REUSE)
+    assert sa["segments"] == sb["segments"] == sb["traced_segments"]
+    check_exact(a, b)
+    c, _ = renderer.render(cam, 1920, 1080, 64, 16)
+    check_exact(a, c)
+    rows = [0, 1, 415, 540, 544, 558, 777, 1079]
+    ref, _ = O.render_rows(cam, sp, mt, 1920, 1080, 64, 16, rows)
+    check_exact(a[rows], ref)
+    nan_px = np.isnan(a[..., 0])
+    assert nan_px[415, 481] and nan_px[544, 866] and nan_px[558, 881]
+    assert nan_px.sum() < 200
+
+
+def test_4k_sampled_rows(renderer):
+    sp, mt = arrays(scene.rtiow_final_scene())
+    cam = default_camera_block()
+    renderer.set_scene(sp, mt)
+    img, st = renderer.render(cam, 3840, 2160, 256, 32)
+    rows = [3, 1500]
+    ref, _ = O.render_rows(cam, sp, mt, 3840, 2160, 256, 32, rows)
+    check_exact(img[rows], ref)
+
+
+def test_errors(renderer):
+    sp, mt = arrays(scene.config1_scene())
+    bad = sp.copy()
+    bad[2]["material"] = 17
+    with pytest.raises(abi.RayTraceError) as e:
+        renderer.set_scene(bad, mt)
+    assert e.value.status == abi.RT_ERR_BAD_SCENE
+    badm = mt.copy()
+    badm[1]["reflectance"] = 5
+    with pytest.raises(abi.RayTraceError) as e:
+        renderer.set_scene(sp, badm)
+    assert e.value.status == abi.RT_ERR_BAD_SCENE
+    renderer.set_scene(sp, mt)
+    cam = default_camera_block()
+    for args in [(0, 4, 1, 1), (4, 4, 0, 1), (4, 4, 1, 0)]:
+        with pytest.raises(abi.RayTraceError) as e:
+            renderer.render(cam, *args)
+        assert e.value.status == abi.RT_ERR_INVALID_ARG
+    with pytest.raises(abi.RayTraceError):
+        renderer.render(cam, 8, 8, 1, 1, shard_count=2, shard_index=2)
+
+
+def test_render_before_scene():
+    from bevy_raytrace_amd.renderer import Renderer
+    with Renderer(0) as r:
+        with pytest.raises(abi.RayTraceError) as e:
+            r.render(default_camera_block(), 8, 8, 1, 1)
+        assert e.value.status == abi.RT_ERR_NO_SCENE
+
+
+def test_native_library_is_in_tree():
+    """The product path runs librt_hip.so from the package directory."""
+    lib = abi.load()
+    assert os.path.dirname(lib._name) == abi.PKG_DIR

@@ -1,0 +1,201 @@
+"""Oracle pinning (CPU): known-answer values, C vs numpy restatements, golden fixtures.
+
+Parity with the reference itself is unpinned (no tests / golden data in the
+reference, WGSL not executable here: SURVEY.md §8c). The oracle is pinned by
+the hand-derived values of SURVEY Appendix C and by two independent
+restatements agreeing bit for bit.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from bevy_raytrace_amd import scene
+from bevy_raytrace_amd.abi import MATERIAL_DTYPE, SPHERE_DTYPE
+from bevy_raytrace_amd.camera import default_camera_block
+from oracle import oracle as O
+from oracle import rt_oracle_np as N
+
+F = np.float32
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def camf(cam):
+    return np.frombuffer(cam.tobytes(), np.float32)
+
+
+# ------------------------------------------------------------ Appendix C KATs
+HASH_KAT = {  # shade.wgsl:105-116
+    0: (0.77879172563552856, 0.15285363793373108, 0.056309748440980911),
+    1: (0.15154574811458588, 0.029333777725696564, 0.26464989781379700),
+    2: (0.27796033024787903, 0.67902785539627075, 0.42240458726882935),
+    12345: (0.91660130023956299, 0.31799834966659546, 0.26120650768280029),
+    2073600: (0.61315089464187622, 0.22740712761878967, 0.40775686502456665),
+}
+
+
+@pytest.mark.parametrize("n", sorted(HASH_KAT))
+def test_hash3_kat(n):
+    exp = np.array(HASH_KAT[n], dtype=np.float32)
+    assert np.array_equal(O.hash3(n), exp)
+    assert np.array_equal(N.hash3(np.array([n], np.uint32))[0], exp)
+
+
+def test_hash3_never_zero():
+    # n is always odd after the mixing step => no all-zero seed => no NaN from normalize
+    ns = np.random.default_rng(1).integers(0, 2**32, 200000, dtype=np.uint64).astype(np.uint32)
+    h = N.hash3(ns)
+    assert (h > 0).all() and (h <= 1).all()
+    assert F(0x7FFFFFFF) == F(2147483648.0)
+
+
+def test_camera_constants_kat():
+    assert O.tan_half(F(1.5708)) == F(1.0000036)
+    cam = default_camera_block()
+    ipd, lfl = cam["image_plane_distance"], cam["lens_focal_length"]
+    assert F((ipd * lfl) / (ipd - lfl)) == F(0.10101011)
+    T = cam["transform"].reshape(4, 4)  # rows = columns of the column-major matrix
+    assert np.array_equal(T[0, :3], np.array([0.2248595, 0, -0.97439116], np.float32))
+    assert np.array_equal(T[1, :3], np.array([-0.14445336, 0.9889499, -0.03333539], np.float32))
+    assert np.array_equal(T[2, :3], np.array([0.96362406, 0.14824986, 0.22237478], np.float32))
+    assert np.array_equal(T[3], np.array([13, 2, 3, 1], np.float32))
+
+
+@pytest.mark.parametrize("xy,d", [((960, 540), (-0.96362406, -0.14824986, -0.22237478)),
+                                  ((0, 0), (-0.9686123, 0.11266974, 0.22157523)),
+                                  ((1919, 1079), (-0.7034691, -0.36952055, -0.60711265))])
+def test_primary_ray_kat(xy, d):
+    cam = default_camera_block()
+    o, dd = O.primary_ray(cam, 1920, 1080, *xy)
+    assert np.array_equal(o, np.array([13, 2, 3], np.float32))
+    # Appendix C prints 8 significant digits: equal within 1 ulp
+    np.testing.assert_array_max_ulp(dd, np.array(d, np.float32), maxulp=1)
+    cc = N.camera_consts(camf(cam), 1920, 1080)
+    o2, d2 = N.primary_rays(cc, np.array([xy[0]]), np.array([xy[1]]))
+    assert np.array_equal(o2[0], o) and np.array_equal(d2[0], dd)
+
+
+@pytest.mark.parametrize("d,exp", [((0, 1, 0), (0.25, 0.55, 1.0)), ((1, 0, 0), (0.5, 0.7, 1.0)),
+                                   ((0, -1, 0), (0.75, 0.85, 1.0))])
+def test_sky_kat(d, exp):
+    s = O.sky(d)
+    np.testing.assert_allclose(s, exp, rtol=0, atol=6e-8)
+    assert np.array_equal(N.sky(np.array([d], np.float32))[0], s)
+
+
+# ------------------------------------------------------- C vs numpy restatement
+def _scene_arrays(sc):
+    return sc.objects_gpu(), sc.materials_gpu()
+
+
+def glass_scene():
+    """Dielectric-heavy scene exercising TIR, Schlick and refraction (shade.wgsl:163-187)."""
+    mats = scene.MaterialCache()
+    mats.insert("ground", scene.RayTraceMaterial((0.5, 0.5, 0.5, 1), scene.Reflectance.Lambertian, 1.0, 0))
+    mats.insert("glass", scene.RayTraceMaterial((1, 1, 1, 1), scene.Reflectance.Dielectric, 0.0, 1.5))
+    mats.insert("diamond", scene.RayTraceMaterial((1, 1, 1, 1), scene.Reflectance.Dielectric, 0.0, 2.4))
+    mats.insert("fuzz", scene.RayTraceMaterial((0.9, 0.8, 0.7, 1), scene.Reflectance.Metallic, 0.5, 0))
+    sp = [scene.Sphere((0, -1000, -1), 1000, 0), scene.Sphere((0, 1, 0), 1, 1),
+          scene.Sphere((0, 1, 0), -0.9, 1), scene.Sphere((-4, 1, 0), 1, 2),
+          scene.Sphere((4, 1, 0), 1, 3), scene.Sphere((2, 0.5, 2), 0.5, 2)]
+    return scene.Scene(sp, mats, "glass")
+
+
+CROSS = [
+    ("config1", scene.config1_scene, 48, 27, 4, 8, 0),
+    ("reference", scene.reference_scene, 40, 24, 2, 3, 3),
+    ("rtiow", scene.rtiow_final_scene, 32, 18, 2, 16, 0),
+    ("glass", glass_scene, 40, 24, 3, 12, 5),
+    ("tiny", scene.config1_scene, 1, 1, 9, 4, 0),
+    ("depth1", scene.config1_scene, 17, 9, 3, 1, 0),
+]
+
+
+@pytest.mark.parametrize("name,mk,W,H,S,D,f0", CROSS, ids=[c[0] for c in CROSS])
+def test_c_vs_numpy(name, mk, W, H, S, D, f0):
+    sp, mt = _scene_arrays(mk())
+    cam = default_camera_block()
+    a, sa = O.render(cam, sp, mt, W, H, S, D, frame0=f0, nthreads=4)
+    b, sb = N.render(camf(cam), sp, mt, W, H, S, D, frame0=f0)
+    assert sa == sb
+    assert np.array_equal(a, b, equal_nan=True)
+
+
+def test_empty_scene_is_sky():
+    cam = default_camera_block()
+    sp = np.zeros(0, SPHERE_DTYPE)
+    mt = np.zeros(0, MATERIAL_DTYPE)
+    img, segs = O.render(cam, sp, mt, 16, 9, 3, 4)
+    assert segs == 16 * 9 * 3  # one segment per path, all misses
+    o, d = O.primary_ray(cam, 16, 9, 5, 4)
+    assert np.array_equal(img[4, 5, :3], O.sky(d))
+    assert (img[..., 3] == 1).all()
+
+
+def test_oracle_rejects_bad_scene():
+    sc = scene.config1_scene()
+    sp, mt = _scene_arrays(sc)
+    sp = sp.copy()
+    sp[1]["material"] = 99
+    with pytest.raises(ValueError):
+        O.render(default_camera_block(), sp, mt, 4, 4, 1, 2)
+
+
+def test_shard_union_equals_full():
+    """Row tiling is exact: the union of shard renders is the full render."""
+    from bevy_raytrace_amd.distributed import ShardLayout, assemble_host
+    sp, mt = _scene_arrays(scene.config1_scene())
+    cam = default_camera_block()
+    W, H, S, D = 24, 23, 2, 6
+    full, segs = O.render(cam, sp, mt, W, H, S, D, nthreads=4)
+    for world, B in [(2, 3), (3, 5), (4, 1)]:
+        lay = ShardLayout(H, B, world)
+        g = np.zeros((world, lay.max_rows, W, 4), np.float32)
+        tot = 0
+        for k in range(world):
+            part, s = O.render(cam, sp, mt, W, H, S, D, row_block=B, shard_count=world,
+                               shard_index=k, nthreads=2)
+            g[k, :part.shape[0]] = part
+            tot += s
+        assert tot == segs
+        assert np.array_equal(assemble_host(g, lay), full, equal_nan=True)
+
+
+def test_nan_paths_are_reference_behaviour():
+    """A Lambertian ray re-hitting its own sphere from inside (no origin offset,
+    shade.wgsl:123) with the per-(pixel,frame) seed reused every bounce
+    (shade.wgsl:216-218) converges to n == -normalize(seed): normalize(0) = NaN.
+    Both restatements agree on these NaN paths."""
+    sc = scene.rtiow_final_scene()
+    sp, mt = _scene_arrays(sc)
+    cam = default_camera_block()
+    c, segs = O.trace_path(cam, sp, mt, 1920, 1080, 481, 415, 7, 16)
+    assert np.isnan(c).all() and segs == 6
+    cc = N.camera_consts(camf(cam), 1920, 1080)
+    mats = dict(index=sp.view(np.uint32).reshape(-1, 8)[:, 4].astype(np.int64),
+                color=mt.view(np.float32).reshape(-1, 8)[:, 0:3], refl=mt.view(np.int32).reshape(-1, 8)[:, 4],
+                fuzz=mt.view(np.float32).reshape(-1, 8)[:, 5], ior=mt.view(np.float32).reshape(-1, 8)[:, 6])
+    sph = sp.view(np.float32).reshape(-1, 8)[:, 0:4].copy()
+    c2, s2 = N.trace(sph, mats, cc, 1920, 1080, np.array([481]), np.array([415]), 7, 16)
+    assert np.isnan(c2).all() and s2 == 6
+
+
+# ------------------------------------------------------------ golden fixtures
+GOLDEN = sorted(glob.glob(os.path.join(HERE, "golden", "*.npz")))
+
+
+@pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p) for p in GOLDEN])
+def test_golden_fixture(path):
+    z = np.load(path, allow_pickle=False)
+    sp = z["spheres"].view(SPHERE_DTYPE)
+    mt = z["materials"].view(MATERIAL_DTYPE)
+    cam = z["camera"].view(np.float32)
+    W, H, S, D, f0 = (int(v) for v in z["params"])
+    img, segs = O.render(cam, sp, mt, W, H, S, D, frame0=f0, nthreads=4)
+    assert segs == int(z["segments"][0])
+    assert np.array_equal(img, z["image"], equal_nan=True)
+
+
+def test_golden_fixtures_present():
+    assert len(GOLDEN) >= 4
