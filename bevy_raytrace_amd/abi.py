@@ -115,7 +115,7 @@ _PROTOS = {
     "rt_last_error": (ctypes.c_char_p, [_VP]),
 }
 
-_lib = None
+_libs = {}
 
 
 def header_symbols(path=HEADER_PATH):
@@ -140,11 +140,12 @@ def _share_torch_hip_runtime():
         ctypes.CDLL(cand, mode=ctypes.RTLD_GLOBAL)
 
 
-def load(path=LIB_PATH):
-    """Load librt_hip.so (raises if it was not built — no fallback)."""
-    global _lib
-    if _lib is not None:
-        return _lib
+def load(path=None):
+    """Load librt_hip.so (raises if it was not built — no fallback).
+    `path` selects another build of the same ABI (e.g. a diagnostic build)."""
+    path = os.path.abspath(path or LIB_PATH)
+    if path in _libs:
+        return _libs[path]
     if not os.path.exists(path):
         raise RuntimeError(
             f"{path} is missing: build the HIP library first (python -c "
@@ -155,7 +156,10 @@ def load(path=LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    _lib = lib
+    if hasattr(lib, "rt_debug_counters"):  # internal diagnostic symbol
+        lib.rt_debug_counters.restype = ctypes.c_int
+        lib.rt_debug_counters.argtypes = [_VP, ctypes.POINTER(ctypes.c_uint64)]
+    _libs[path] = lib
     return lib
 
 

@@ -45,10 +45,11 @@ struct rt_ctx {
     // scene
     bool has_scene = false;
     uint32_t n = 0, ngroups = 0, m = 0;
+    float4* d_grp = nullptr;        // groups of 4 spheres, SoA (cx[4], cy[4], cz[4], r2[4])
     float4* d_sph = nullptr;        // (cx, cy, cz, r*r)
     float2* d_sph_rm = nullptr;     // (radius, material bits)
     rt_material* d_mats = nullptr;
-    size_t sph_cap = 0, sph_rm_cap = 0, mat_cap = 0;
+    size_t grp_cap = 0, sph_cap = 0, sph_rm_cap = 0, mat_cap = 0;
 
     // work buffers
     float4* d_block_sums = nullptr;
@@ -157,7 +158,7 @@ int rt_create(int device, rt_ctx** out_ctx) {
                                        device)) != hipSuccess)
             break;
         if ((e = rt_render_occupancy(&ctx->blocks_per_cu)) != hipSuccess) break;
-        if ((e = hipHostMalloc((void**)&ctx->h_segs, 2 * sizeof(unsigned long long))) != hipSuccess) break;
+        if ((e = hipHostMalloc((void**)&ctx->h_segs, 18 * sizeof(unsigned long long))) != hipSuccess) break;
         if ((e = hipEventCreate(&ctx->ev_t0)) != hipSuccess) break;
         if ((e = hipEventCreate(&ctx->ev_t1)) != hipSuccess) break;
     } while (0);
@@ -176,6 +177,7 @@ void rt_destroy(rt_ctx* ctx) {
     hipSetDevice(ctx->device);
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
     if (ctx->pending && ctx->pending_stream) hipStreamSynchronize(ctx->pending_stream);
+    hipFree(ctx->d_grp);
     hipFree(ctx->d_sph);
     hipFree(ctx->d_sph_rm);
     hipFree(ctx->d_mats);
@@ -220,16 +222,27 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n, const rt_mat
         std::memcpy(&mbits, &s.material, 4);
         rm[i] = make_float2(r, mbits);
     }
+    std::vector<float4> grp(nrec);  // SoA regroup of the padded records
+    for (size_t g = 0; g < nrec / 4; ++g) {
+        const float4* q = &sph[4 * g];
+        grp[4 * g + 0] = make_float4(q[0].x, q[1].x, q[2].x, q[3].x);
+        grp[4 * g + 1] = make_float4(q[0].y, q[1].y, q[2].y, q[3].y);
+        grp[4 * g + 2] = make_float4(q[0].z, q[1].z, q[2].z, q[3].z);
+        grp[4 * g + 3] = make_float4(q[0].w, q[1].w, q[2].w, q[3].w);
+    }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if (ctx->pending && ctx->pending_stream) HIP_TRY(ctx, hipStreamSynchronize(ctx->pending_stream));
     int rc = ensure(ctx, &ctx->d_sph, &ctx->sph_cap, sizeof(float4) * nrec);
+    if (rc) return rc;
+    rc = ensure(ctx, &ctx->d_grp, &ctx->grp_cap, sizeof(float4) * nrec);
     if (rc) return rc;
     rc = ensure(ctx, &ctx->d_sph_rm, &ctx->sph_rm_cap, sizeof(float2) * rm.size());
     if (rc) return rc;
     rc = ensure(ctx, &ctx->d_mats, &ctx->mat_cap, sizeof(rt_material) * (size_t)m);
     if (rc) return rc;
     HIP_TRY(ctx, hipMemcpy(ctx->d_sph, sph.data(), sizeof(float4) * nrec, hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(ctx->d_grp, grp.data(), sizeof(float4) * nrec, hipMemcpyHostToDevice));
     HIP_TRY(ctx, hipMemcpy(ctx->d_sph_rm, rm.data(), sizeof(float2) * rm.size(), hipMemcpyHostToDevice));
     if (m)
         HIP_TRY(ctx, hipMemcpy(ctx->d_mats, materials, sizeof(rt_material) * m, hipMemcpyHostToDevice));
@@ -281,7 +294,7 @@ static int enqueue(rt_ctx* ctx, const rt_camera* cam, const rt_params* prm, floa
             if (rc) return rc;
         }
     }
-    const size_t words = 4 + passes.size();
+    const size_t words = RT_CNT_WORK_OFFSET + passes.size();
     const size_t words_pad = (words + 3) & ~(size_t)3;  // 16-B multiple
     {
         int rc = ensure(ctx, &ctx->d_counters, &ctx->counters_cap, words_pad * sizeof(uint32_t));
@@ -325,15 +338,15 @@ static int enqueue(rt_ctx* ctx, const rt_camera* cam, const rt_params* prm, floa
         const uint64_t need_blocks = (chunks + (RT_BLOCK_THREADS / 64) - 1) / (RT_BLOCK_THREADS / 64);
         const uint32_t grid = (uint32_t)(need_blocks < grid_full ? need_blocks : grid_full);
         HIP_TRY(ctx, hipEventRecord(ctx->ev[2 * i], stream));
-        HIP_TRY(ctx, rt_launch_render(&K_, ctx->d_sph, ctx->d_sph_rm, ctx->d_mats, ctx->d_block_sums,
-                                      ctx->d_counters + 4 + i,
+        HIP_TRY(ctx, rt_launch_render(&K_, ctx->d_grp, ctx->d_sph, ctx->d_sph_rm, ctx->d_mats, ctx->d_block_sums,
+                                      ctx->d_counters + RT_CNT_WORK_OFFSET + i,
                                       reinterpret_cast<unsigned long long*>(ctx->d_counters),
                                       grid, stream));
         HIP_TRY(ctx, hipEventRecord(ctx->ev[2 * i + 1], stream));
         HIP_TRY(ctx, rt_launch_collect(ctx->d_block_sums, npix, K_.nblocks, ctx->d_acc, i == 0,
                                        i + 1 == passes.size(), (float)p.spp, d_out, stream));
     }
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_segs, ctx->d_counters, 2 * sizeof(unsigned long long),
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_segs, ctx->d_counters, 18 * sizeof(unsigned long long),
                                 hipMemcpyDeviceToHost, stream));
     *out_passes = (uint32_t)passes.size();
     *out_paths = (uint64_t)npix * p.spp;
@@ -439,6 +452,14 @@ int rt_assemble_shards(rt_ctx* ctx, const float* gathered_device, uint32_t max_r
                                     reinterpret_cast<float4*>(image_device), width, height, B,
                                     shard_count, s));
     if (!stream) HIP_TRY(ctx, hipStreamSynchronize(s));
+    return RT_OK;
+}
+
+// Internal (not in include/rt_hip.h): the 16 diagnostic counters of the last
+// waited call; all zero unless the library was built with -DRT_PROFILE.
+int rt_debug_counters(const rt_ctx* ctx, uint64_t* out16) {
+    if (!ctx || !out16) return RT_ERR_INVALID_ARG;
+    for (int i = 0; i < 16; ++i) out16[i] = ctx->h_segs[2 + i];
     return RT_OK;
 }
 

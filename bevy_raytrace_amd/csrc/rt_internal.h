@@ -8,6 +8,13 @@
 
 #define RT_BLOCK_THREADS 256  // 4 waves per workgroup
 #define RT_WAVE_CHUNK 64      // work items a wave takes per atomic
+// Counter block at the start of the ctx's counter buffer (u32 words):
+// [0,4) two u64 segment counters, [4,36) 16 u64 diagnostic counters
+// (RT_PROFILE builds), [36, ...) one u32 work counter per pass.
+#define RT_CNT_WORK_OFFSET 36
+#ifndef RT_CQ_CAP
+#define RT_CQ_CAP 8           // candidate-queue entries per lane (LDS)
+#endif
 #ifndef RT_MIN_WAVES_PER_SIMD
 #define RT_MIN_WAVES_PER_SIMD 4
 #endif
@@ -28,9 +35,10 @@ struct KParams {
 };
 
 extern "C" {
-hipError_t rt_launch_render(const KParams* P, const float4* sph, const float2* sph_rm,
-                            const rt_material* mats, float4* block_sums, uint32_t* work_counter,
-                            unsigned long long* seg_counter, uint32_t grid, hipStream_t stream);
+hipError_t rt_launch_render(const KParams* P, const float4* grp, const float4* sph,
+                            const float2* sph_rm, const rt_material* mats, float4* block_sums,
+                            uint32_t* work_counter, unsigned long long* seg_counter, uint32_t grid,
+                            hipStream_t stream);
 hipError_t rt_launch_collect(const float4* block_sums, uint32_t npix, uint32_t nblocks,
                              float4* acc, int first_pass, int last_pass, float spp, float4* out,
                              hipStream_t stream);

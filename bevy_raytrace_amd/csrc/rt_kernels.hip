@@ -106,6 +106,34 @@ __device__ __forceinline__ v3 reflect(v3 v, v3 n) {  // shade.wgsl:132-134
     return sub(v, scale(n, k));
 }
 
+// ---- diagnostic build only (-DRT_PROFILE): per-wave phase clocks (s_memtime)
+// and wave-level event counts, summed into a debug buffer. Never compiled into
+// the product library.
+#ifdef RT_PROFILE
+struct Prof {
+    unsigned long long c[16];
+    unsigned long long last;
+};
+#define PROF_DECL Prof prof_ = {};
+#define PROF_START() (prof_.last = __builtin_amdgcn_s_memtime())
+#define PROF_MARK(i)                                            \
+    do {                                                        \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        prof_.c[i] += t_ - prof_.last;                          \
+        prof_.last = t_;                                        \
+    } while (0)
+#define PROF_ADD(i, v) (prof_.c[i] += (v))
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off));
+    return v;
+}
+#else
+#define PROF_DECL
+#define PROF_START()
+#define PROF_MARK(i)
+#define PROF_ADD(i, v)
+#endif
+
 // Exact reference test of one sphere (intersect.wgsl:97-115 + :137).
 // s.w = RN(radius*radius) = sqr(s.radius); r2p = s.w * (1 + 2^-20).
 __device__ __forceinline__ void exact_test(float4 s, int idx, v3 o, v3 d, float a,
@@ -134,44 +162,100 @@ __device__ __forceinline__ void exact_test(float4 s, int idx, v3 o, v3 d, float 
     }
 }
 
-// Conservative filter value; G < 0 => certain miss (see file header).
-__device__ __forceinline__ float filter_g(float4 s, v3 o, v3 dn, float negk) {
-    const float ocx = o.x - s.x, ocy = o.y - s.y, ocz = o.z - s.z;
-    const float hb = __builtin_fmaf(ocz, dn.z, __builtin_fmaf(ocy, dn.y, ocx * dn.x));
-    const float q = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx));
-    return __builtin_fmaf(negk, q, __builtin_fmaf(hb, hb, s.w));
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 bc(float x) { return f2{x, x}; }
+
+// Conservative filter for two spheres at once (packed fp32: v_pk_add/mul/fma_f32,
+// the only way to the 157.3 TF fp32 peak on gfx950 -- tools/ubench/fma_rate.hip).
+// G < 0 => certain miss (file header); 11 packed ops per sphere pair.
+__device__ __forceinline__ f2 filter2(f2 cx, f2 cy, f2 cz, f2 r2, f2 ox, f2 oy, f2 oz, f2 dx,
+                                      f2 dy, f2 dz, f2 negk) {
+    const f2 ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;
+    const f2 hb = pk_fma(ocz, dz, pk_fma(ocy, dy, ocx * dx));
+    const f2 q = pk_fma(ocz, ocz, pk_fma(ocy, ocy, ocx * ocx));
+    return pk_fma(negk, q, pk_fma(hb, hb, r2));
 }
 
-// Closest hit over the whole list (intersect.wgsl:133-143). `sph` is padded
-// to a multiple of 4 records plus one extra group of 4, the pad records having
-// r^2 = -inf (G = -inf: never candidates). Returns best index (-1 = miss), t.
-__device__ __forceinline__ int intersect_world(const float4* __restrict__ sph, uint32_t ngroups,
-                                               v3 o, v3 d, float& t_out) {
+// Run the exact test for every queued candidate of this lane, in list order.
+// Queue entries are (group << 4 | 4-bit candidate mask), one column per lane.
+__device__ __forceinline__ void drain_candidates(const uint32_t* cq, uint32_t cnt,
+                                                 const float4* __restrict__ sph, v3 o, v3 d,
+                                                 float a, float& best_t, int& best_i) {
+    const uint32_t lane = __lane_id();
+    for (uint32_t k = 0; k < cnt; ++k) {
+        const uint32_t e = cq[k * 64 + lane];
+        uint32_t m = e & 15u;
+        const uint32_t base = (e >> 4) * 4;
+        while (m) {
+            const uint32_t j = __builtin_ctz(m);
+            m &= m - 1;
+            exact_test(sph[base + j], (int)(base + j), o, d, a, best_t, best_i);
+        }
+    }
+}
+
+// Closest hit over the whole list (intersect.wgsl:133-143).
+// grp: the sphere list as groups of 4 in SoA (cx[4], cy[4], cz[4], r2[4]),
+// padded with pad records of r^2 = -inf (G = -inf: never candidates) to a
+// whole number of groups plus one extra group (prefetch reach). Wave-uniform:
+// read with s_load_dwordx16 and fed to the packed ops as SGPR pairs.
+// sph: the same records AoS (cx, cy, cz, r2), gathered per lane by the exact tests.
+// Pass 1 filters every sphere and queues candidates per lane (LDS, cq);
+// pass 2 (drain) runs the exact reference test on them in list order, so the
+// wave pays for max-over-lanes candidates, not for their union.
+// Returns the best index (-1 = miss) and t.
+__device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
+                                               const float4* __restrict__ sph, uint32_t ngroups,
+                                               v3 o, v3 d, float& t_out, uint32_t* cq
+#ifdef RT_PROFILE
+                                               , Prof& prof_
+#endif
+                                               ) {
     const float dd = dot(d, d);
     const float l = sqrtf(dd);
     const float a = l * l;                        // sqr(length(r.dir)), intersect.wgsl:98
     const float rs = __builtin_amdgcn_rsqf(dd);  // filter only: approximate 1/|d|
-    const v3 dn = mk(d.x * rs, d.y * rs, d.z * rs);
-    const float negk = -(1.0f - 0x1p-16f);
+    const f2 ox = bc(o.x), oy = bc(o.y), oz = bc(o.z);
+    const f2 dx = bc(d.x * rs), dy = bc(d.y * rs), dz = bc(d.z * rs);
+    const f2 negk = bc(-(1.0f - 0x1p-16f));
+    const uint32_t lane = __lane_id();
     float best_t = VERY_FAR;
     int best_i = -1;
-    float4 n0 = sph[0], n1 = sph[1], n2 = sph[2], n3 = sph[3];
+    uint32_t cnt = 0;
+    float4 p0 = grp[0], p1 = grp[1], p2 = grp[2], p3 = grp[3];
     for (uint32_t g = 0; g < ngroups; ++g) {
-        const float4 s0 = n0, s1 = n1, s2 = n2, s3 = n3;
-        const uint32_t i = g * 4;
-        n0 = sph[i + 4]; n1 = sph[i + 5]; n2 = sph[i + 6]; n3 = sph[i + 7];  // prefetch
-        const uint64_t m0 = __ballot(!(filter_g(s0, o, dn, negk) < 0.0f));
-        const uint64_t m1 = __ballot(!(filter_g(s1, o, dn, negk) < 0.0f));
-        const uint64_t m2 = __ballot(!(filter_g(s2, o, dn, negk) < 0.0f));
-        const uint64_t m3 = __ballot(!(filter_g(s3, o, dn, negk) < 0.0f));
-        if ((m0 | m1 | m2 | m3) != 0) {
-            const uint64_t me = 1ull << __lane_id();
-            if (m0 & me) exact_test(s0, (int)i, o, d, a, best_t, best_i);
-            if (m1 & me) exact_test(s1, (int)i + 1, o, d, a, best_t, best_i);
-            if (m2 & me) exact_test(s2, (int)i + 2, o, d, a, best_t, best_i);
-            if (m3 & me) exact_test(s3, (int)i + 3, o, d, a, best_t, best_i);
+        const float4 cx = p0, cy = p1, cz = p2, rr = p3;
+        const uint32_t nx = 4 * g + 4;  // prefetch the next group
+        p0 = grp[nx]; p1 = grp[nx + 1]; p2 = grp[nx + 2]; p3 = grp[nx + 3];
+        const f2 g01 = filter2(f2{cx.x, cx.y}, f2{cy.x, cy.y}, f2{cz.x, cz.y}, f2{rr.x, rr.y},
+                               ox, oy, oz, dx, dy, dz, negk);
+        const f2 g23 = filter2(f2{cx.z, cx.w}, f2{cy.z, cy.w}, f2{cz.z, cz.w}, f2{rr.z, rr.w},
+                               ox, oy, oz, dx, dy, dz, negk);
+        // group skip: all four G < 0 (a NaN G is dropped by max: NaN G never hits)
+        const float gm = fmaxf(fmaxf(g01.x, g01.y), fmaxf(g23.x, g23.y));
+        if (__ballot(!(gm < 0.0f)) != 0) {
+            PROF_ADD(5, 1);
+            if (__ballot(cnt >= RT_CQ_CAP) != 0) {  // a lane's queue is full: drain all
+                PROF_ADD(11, 1);
+                drain_candidates(cq, cnt, sph, o, d, a, best_t, best_i);
+                cnt = 0;
+            }
+            const uint32_t m = (uint32_t)!(g01.x < 0.0f) | ((uint32_t)!(g01.y < 0.0f) << 1) |
+                               ((uint32_t)!(g23.x < 0.0f) << 2) | ((uint32_t)!(g23.y < 0.0f) << 3);
+            if (m) {
+                cq[cnt * 64 + lane] = (g << 4) | m;
+                ++cnt;
+            }
         }
     }
+    PROF_MARK(1);
+#ifdef RT_PROFILE
+    PROF_ADD(6, wave_max_u32(cnt));
+#endif
+    drain_candidates(cq, cnt, sph, o, d, a, best_t, best_i);
+    PROF_MARK(2);
     t_out = best_t;
     return best_i;
 }
@@ -292,10 +376,18 @@ __device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, f
 }
 
 __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_render_kernel(
-    KParams P, const float4* __restrict__ sph, const float2* __restrict__ sph_rm,
-    const rt_material* __restrict__ mats, float4* __restrict__ block_sums,
-    uint32_t* __restrict__ work_counter, unsigned long long* __restrict__ seg_counter) {
+    KParams P, const float4* __restrict__ grp, const float4* __restrict__ sph,
+    const float2* __restrict__ sph_rm, const rt_material* __restrict__ mats,
+    float4* __restrict__ block_sums, uint32_t* __restrict__ work_counter,
+    unsigned long long* __restrict__ seg_counter, unsigned long long* __restrict__ dbg) {
     const uint32_t lane = threadIdx.x & 63u;
+    PROF_DECL
+    PROF_START();
+#ifdef RT_PROFILE
+    const unsigned long long t_begin = prof_.last;
+#endif
+    __shared__ uint32_t s_cq[RT_BLOCK_THREADS * RT_CQ_CAP];  // per-lane candidate queues
+    uint32_t* cq = s_cq + (threadIdx.x / 64u) * (64u * RT_CQ_CAP);
     const uint32_t total = P.npix * P.nblocks;
     const bool use_cache = (P.flags & RT_FLAG_NO_PRIMARY_CACHE) == 0;
 
@@ -333,13 +425,20 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
             need = __ballot(!has_item);
         }
         if (__ballot(has_item) == 0) break;
+        PROF_MARK(0);
+        PROF_ADD(4, 1);
+        PROF_ADD(9, (unsigned long long)__popcll(__ballot(has_item)));
 
         // ---- intersect (intersect.wgsl:145-163): every lane with an item holds
         // a ray that needs tracing here.
         int hi = -1;
         float t = VERY_FAR;
         if (has_item) {
-            hi = intersect_world(sph, P.ngroups, st.o, st.d, t);
+            hi = intersect_world(grp, sph, P.ngroups, st.o, st.d, t, cq
+#ifdef RT_PROFILE
+                                 , prof_
+#endif
+                                 );
             ++traced;
             if (st.bounce == 0) {  // first sample of the block: remember the primary hit
                 cache_hi = hi;
@@ -349,6 +448,7 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
         // ---- shade; a finished path starts the next sample, whose primary hit
         // is reused (result-identical) so the lane goes on to its bounce-1 ray.
         bool shading = has_item;
+        PROF_MARK(12);  // bookkeeping between the drain and the shading loop
         while (shading) {
             ++segs;
             const bool done = shade(P, st, hi, t, sph, sph_rm, mats);
@@ -370,8 +470,15 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
                 }
             }
         }
+        PROF_MARK(3);
     }
 
+#ifdef RT_PROFILE
+    PROF_MARK(7);
+    prof_.c[8] = __builtin_amdgcn_s_memtime() - t_begin;
+    if (lane == 0)
+        for (int i = 0; i < 16; ++i) atomicAdd(dbg + i, prof_.c[i]);
+#endif
     // ---- segment counts: wave reduce, one atomic per wave
     unsigned long long v = segs, w = traced;
     for (int off = 32; off > 0; off >>= 1) {
@@ -427,11 +534,12 @@ __global__ void rt_assemble_kernel(const float4* __restrict__ gathered, uint32_t
 
 extern "C" {
 
-hipError_t rt_launch_render(const KParams* P, const float4* sph, const float2* sph_rm,
-                            const rt_material* mats, float4* block_sums, uint32_t* work_counter,
-                            unsigned long long* seg_counter, uint32_t grid, hipStream_t stream) {
-    hipLaunchKernelGGL(rt_render_kernel, dim3(grid), dim3(RT_BLOCK_THREADS), 0, stream, *P, sph,
-                       sph_rm, mats, block_sums, work_counter, seg_counter);
+hipError_t rt_launch_render(const KParams* P, const float4* grp, const float4* sph,
+                            const float2* sph_rm, const rt_material* mats, float4* block_sums,
+                            uint32_t* work_counter, unsigned long long* seg_counter, uint32_t grid,
+                            hipStream_t stream) {
+    hipLaunchKernelGGL(rt_render_kernel, dim3(grid), dim3(RT_BLOCK_THREADS), 0, stream, *P, grp,
+                       sph, sph_rm, mats, block_sums, work_counter, seg_counter, seg_counter + 2);
     return hipGetLastError();
 }
 

@@ -16,8 +16,8 @@ from .abi import RtStats, check, make_params
 
 
 class Renderer:
-    def __init__(self, device: int = 0):
-        self.lib = abi.load()
+    def __init__(self, device: int = 0, lib_path=None):
+        self.lib = abi.load(lib_path)
         ctx = ctypes.c_void_p()
         rc = self.lib.rt_create(int(device), ctypes.byref(ctx))
         check(self.lib, None, rc)
@@ -89,6 +89,12 @@ class Renderer:
         rc = self.lib.rt_wait(self.ctx, ctypes.byref(st))
         check(self.lib, self.ctx, rc)
         return st.as_dict()
+
+    def debug_counters(self):
+        """Diagnostic counters of the last call (non-zero only for -DRT_PROFILE builds)."""
+        out = (ctypes.c_uint64 * 16)()
+        self.lib.rt_debug_counters(self.ctx, out)
+        return list(out)
 
     def assemble_shards(self, gathered_ptr: int, max_rows, image_ptr: int, width, height,
                         row_block, shard_count, stream=None):
