@@ -112,6 +112,7 @@ _PROTOS = {
     "rt_render_async": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(RtParams), _VP]),
     "rt_wait": (ctypes.c_int, [_VP, ctypes.POINTER(RtStats)]),
     "rt_assemble_shards": (ctypes.c_int, [_VP, _VP, _U32, _VP, _U32, _U32, _U32, _U32, _VP]),
+    "rt_intersect": (ctypes.c_int, [_VP, _VP, _U32, _VP, _VP]),
     "rt_last_error": (ctypes.c_char_p, [_VP]),
 }
 

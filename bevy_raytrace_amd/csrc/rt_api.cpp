@@ -204,31 +204,44 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n, const rt_mat
         if (r < RT_LAMBERTIAN || r > RT_DIELECTRIC)
             return fail(ctx, RT_ERR_BAD_SCENE, "material %u: reflectance %d not in {0,1,2}", j, r);
     }
-    // Sphere stream for the kernel's scalar-load loop: (cx, cy, cz, r*r) records
-    // padded to a whole number of groups of 4 plus one extra group (prefetch
-    // reach); pad records have r^2 = -inf, which the filter never passes.
-    const uint32_t ngroups = (n + 3) / 4;
-    const size_t nrec = (size_t)(ngroups + 1) * 4;
+    // Sphere records for the kernel. AoS (cx, cy, cz, r*r) for the exact tests
+    // and shading; SoA groups of RT_GROUP (cx[8], cy[8], cz[8], S[8]) for the
+    // wave-uniform filter loop, S = r^2 - (1 - m - mu) |c|^2 rounded once from
+    // double (DESIGN.md "Exact filter"). Padded to whole groups; pad records
+    // have r^2 = S = -inf, which the filter never passes.
+    const uint32_t ngroups = (n + RT_GROUP - 1) / RT_GROUP;
+    const size_t nrec = (size_t)(ngroups + 1) * RT_GROUP;
     std::vector<float4> sph(nrec, make_float4(0.0f, 0.0f, 0.0f, -INFINITY));
+    std::vector<float> S(nrec, -INFINITY);
     std::vector<float2> rm(n ? n : 1, make_float2(0.0f, 0.0f));
+    const double kS = 1.0 - 0x1p-16 - 0x1p-17;
     for (uint32_t i = 0; i < n; ++i) {
         const rt_sphere& s = spheres[i];
         if (s.material >= m)
             return fail(ctx, RT_ERR_BAD_SCENE, "sphere %u: material %u >= material count %u", i,
                         s.material, m);
         const float r = s.radius;
-        sph[i] = make_float4(s.center[0], s.center[1], s.center[2], r * r);  // sqr(s.radius)
+        const float r2 = r * r;  // sqr(s.radius): the f32 value the exact test uses
+        sph[i] = make_float4(s.center[0], s.center[1], s.center[2], r2);
+        const double cx = s.center[0], cy = s.center[1], cz = s.center[2];
+        S[i] = (float)((double)r2 - kS * (cx * cx + cy * cy + cz * cz));
         float mbits;
         std::memcpy(&mbits, &s.material, 4);
         rm[i] = make_float2(r, mbits);
     }
     std::vector<float4> grp(nrec);  // SoA regroup of the padded records
-    for (size_t g = 0; g < nrec / 4; ++g) {
-        const float4* q = &sph[4 * g];
-        grp[4 * g + 0] = make_float4(q[0].x, q[1].x, q[2].x, q[3].x);
-        grp[4 * g + 1] = make_float4(q[0].y, q[1].y, q[2].y, q[3].y);
-        grp[4 * g + 2] = make_float4(q[0].z, q[1].z, q[2].z, q[3].z);
-        grp[4 * g + 3] = make_float4(q[0].w, q[1].w, q[2].w, q[3].w);
+    for (size_t g = 0; g < nrec / RT_GROUP; ++g) {
+        const float4* q = &sph[RT_GROUP * g];
+        const float* sg = &S[RT_GROUP * g];
+        float4* o = &grp[RT_GROUP * g];
+        o[0] = make_float4(q[0].x, q[1].x, q[2].x, q[3].x);
+        o[1] = make_float4(q[4].x, q[5].x, q[6].x, q[7].x);
+        o[2] = make_float4(q[0].y, q[1].y, q[2].y, q[3].y);
+        o[3] = make_float4(q[4].y, q[5].y, q[6].y, q[7].y);
+        o[4] = make_float4(q[0].z, q[1].z, q[2].z, q[3].z);
+        o[5] = make_float4(q[4].z, q[5].z, q[6].z, q[7].z);
+        o[6] = make_float4(sg[0], sg[1], sg[2], sg[3]);
+        o[7] = make_float4(sg[4], sg[5], sg[6], sg[7]);
     }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -452,6 +465,33 @@ int rt_assemble_shards(rt_ctx* ctx, const float* gathered_device, uint32_t max_r
                                     reinterpret_cast<float4*>(image_device), width, height, B,
                                     shard_count, s));
     if (!stream) HIP_TRY(ctx, hipStreamSynchronize(s));
+    return RT_OK;
+}
+
+int rt_intersect(rt_ctx* ctx, const float* rays, uint32_t n, int32_t* hit_index, float* hit_t) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_intersect: ctx is NULL");
+    if (!ctx->has_scene) return fail(ctx, RT_ERR_NO_SCENE, "rt_intersect before rt_set_scene");
+    if (n == 0) return RT_OK;
+    if (!rays || !hit_index || !hit_t)
+        return fail(ctx, RT_ERR_INVALID_ARG, "rt_intersect: NULL array");
+    if (ctx->pending) return fail(ctx, RT_ERR_INVALID_ARG, "a previous async call was not waited for");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    void* buf = nullptr;
+    const size_t rb = sizeof(float) * 6 * (size_t)n, ob = sizeof(int32_t) * (size_t)n;
+    HIP_TRY(ctx, hipMalloc(&buf, rb + 2 * ob));
+    char* b = (char*)buf;
+    hipError_t e = hipMemcpyAsync(b, rays, rb, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess)
+        e = rt_launch_intersect(ctx->d_grp, ctx->d_sph, ctx->ngroups, (const float*)b, n,
+                                (int*)(b + rb), (float*)(b + rb + ob), ctx->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(hit_index, b + rb, ob, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(hit_t, b + rb + ob, ob, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    hipFree(buf);
+    if (e != hipSuccess)
+        return fail(ctx, RT_ERR_DEVICE, "rt_intersect: %s", hipGetErrorString(e));
     return RT_OK;
 }
 

@@ -12,6 +12,7 @@
 // [0,4) two u64 segment counters, [4,36) 16 u64 diagnostic counters
 // (RT_PROFILE builds), [36, ...) one u32 work counter per pass.
 #define RT_CNT_WORK_OFFSET 36
+#define RT_GROUP 8            // spheres per filter group (SoA, 128 B)
 #ifndef RT_CQ_CAP
 #define RT_CQ_CAP 8           // candidate-queue entries per lane (LDS)
 #endif
@@ -28,7 +29,7 @@ struct KParams {
     uint32_t block_begin;  // first sample block of this pass
     uint32_t nblocks;      // sample blocks in this pass
     uint32_t nspheres;
-    uint32_t ngroups;      // padded sphere groups of 4 (see rt_set_scene)
+    uint32_t ngroups;      // padded sphere groups of RT_GROUP (see rt_set_scene)
     uint32_t flags;
     float T[16];           // camera transform, column-major
     float tan_half, focus_plane, aspect, half_w, half_h;
@@ -45,5 +46,8 @@ hipError_t rt_launch_collect(const float4* block_sums, uint32_t npix, uint32_t n
 hipError_t rt_launch_assemble(const float4* gathered, uint32_t max_rows, float4* image,
                               uint32_t width, uint32_t height, uint32_t row_block,
                               uint32_t shard_count, hipStream_t stream);
+hipError_t rt_launch_intersect(const float4* grp, const float4* sph, uint32_t ngroups,
+                               const float* rays, uint32_t n, int* out_i, float* out_t,
+                               hipStream_t stream);
 hipError_t rt_render_occupancy(int* blocks_per_cu);
 }

@@ -167,27 +167,56 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f2 bc(float x) { return f2{x, x}; }
 
-// Conservative filter for two spheres at once (packed fp32: v_pk_add/mul/fma_f32,
-// the only way to the 157.3 TF fp32 peak on gfx950 -- tools/ubench/fma_rate.hip).
-// G < 0 => certain miss (file header); 11 packed ops per sphere pair.
-__device__ __forceinline__ f2 filter2(f2 cx, f2 cy, f2 cz, f2 r2, f2 ox, f2 oy, f2 oz, f2 dx,
-                                      f2 dy, f2 dz, f2 negk) {
-    const f2 ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;
-    const f2 hb = pk_fma(ocz, dz, pk_fma(ocy, dy, ocx * dx));
-    const f2 q = pk_fma(ocz, ocz, pk_fma(ocy, ocy, ocx * ocx));
-    return pk_fma(negk, q, pk_fma(hb, hb, r2));
+// Per-ray constants of the expanded-form filter (see file header / DESIGN.md):
+//   G' = (k1 - dn.c)^2 + S + K + o2.c
+//      = hb^2 + r^2 - (1 - m) |o - c|^2 + mu (|o|^2 + |c|^2)
+// with hb = dn.(o - c), dn ~ d/|d|, S = r^2 - (1 - m - mu)|c|^2 (per sphere,
+// host), k1 = dn.o, K = -(1 - m - mu)|o|^2, o2 = 2(1 - m) o (per ray).
+// m = 2^-16 bounds the exact path's rounding relative to |o - c|^2 + r^2,
+// mu = 2^-17 the expanded form's cancellation relative to |o|^2 + |c|^2.
+struct RayF {
+    f2 dx, dy, dz, o2x, o2y, o2z, k1, K;
+};
+
+__device__ __forceinline__ RayF ray_filter_consts(v3 o, v3 d) {
+    const float rs = __builtin_amdgcn_rsqf(dot(d, d));  // approximate 1/|d| (covered by m)
+    const float dnx = d.x * rs, dny = d.y * rs, dnz = d.z * rs;
+    const float m = 0x1p-16f, mu = 0x1p-17f;
+    const float oo = __builtin_fmaf(o.z, o.z, __builtin_fmaf(o.y, o.y, o.x * o.x));
+    const float k1 = __builtin_fmaf(dnz, o.z, __builtin_fmaf(dny, o.y, dnx * o.x));
+    const float two = 2.0f * (1.0f - m);
+    RayF r;
+    r.dx = bc(dnx); r.dy = bc(dny); r.dz = bc(dnz);
+    r.o2x = bc(two * o.x); r.o2y = bc(two * o.y); r.o2z = bc(two * o.z);
+    r.k1 = bc(k1);
+    r.K = bc(-(1.0f - m - mu) * oo);
+    return r;
+}
+
+// Filter two spheres at once: 9 packed fp32 ops (v_pk_fma/mul/add_f32 -- the
+// only way to the 157.3 TF fp32 peak on gfx950, tools/ubench/fma_rate.hip).
+// G' < 0 => certain miss.
+__device__ __forceinline__ f2 filter2(f2 cx, f2 cy, f2 cz, f2 S, const RayF& r) {
+    const f2 dc = pk_fma(r.dz, cz, pk_fma(r.dy, cy, r.dx * cx));
+    const f2 hb = r.k1 - dc;
+    const f2 u = pk_fma(r.o2x, cx, pk_fma(r.o2y, cy, pk_fma(r.o2z, cz, S + r.K)));
+    return pk_fma(hb, hb, u);
+}
+
+__device__ __forceinline__ uint32_t sgn_clear(float g) {  // 1 if the sign bit of g is clear
+    return (~__float_as_uint(g)) >> 31;
 }
 
 // Run the exact test for every queued candidate of this lane, in list order.
-// Queue entries are (group << 4 | 4-bit candidate mask), one column per lane.
+// Queue entries are (group << 8 | 8-bit candidate mask), one column per lane.
 __device__ __forceinline__ void drain_candidates(const uint32_t* cq, uint32_t cnt,
                                                  const float4* __restrict__ sph, v3 o, v3 d,
                                                  float a, float& best_t, int& best_i) {
     const uint32_t lane = __lane_id();
     for (uint32_t k = 0; k < cnt; ++k) {
         const uint32_t e = cq[k * 64 + lane];
-        uint32_t m = e & 15u;
-        const uint32_t base = (e >> 4) * 4;
+        uint32_t m = e & 0xFFu;
+        const uint32_t base = (e >> 8) * RT_GROUP;
         while (m) {
             const uint32_t j = __builtin_ctz(m);
             m &= m - 1;
@@ -197,13 +226,14 @@ __device__ __forceinline__ void drain_candidates(const uint32_t* cq, uint32_t cn
 }
 
 // Closest hit over the whole list (intersect.wgsl:133-143).
-// grp: the sphere list as groups of 4 in SoA (cx[4], cy[4], cz[4], r2[4]),
-// padded with pad records of r^2 = -inf (G = -inf: never candidates) to a
-// whole number of groups plus one extra group (prefetch reach). Wave-uniform:
-// read with s_load_dwordx16 and fed to the packed ops as SGPR pairs.
-// sph: the same records AoS (cx, cy, cz, r2), gathered per lane by the exact tests.
-// Pass 1 filters every sphere and queues candidates per lane (LDS, cq);
-// pass 2 (drain) runs the exact reference test on them in list order, so the
+// grp: the sphere list as groups of RT_GROUP=8, SoA (cx[8], cy[8], cz[8], S[8]),
+// padded to whole groups with pad records of S = -inf (never candidates).
+// Wave-uniform: read with s_load_dwordx16 and fed to the packed ops as SGPR
+// pairs. sph: the padded records AoS (cx, cy, cz, r2), gathered per lane by
+// the exact tests. Pass 1 filters every sphere and queues candidates per lane
+// (LDS, cq); the group test is one AND of the 8 sign bits (a G' of -0 or a NaN
+// with the sign set is dropped: neither can hit). Pass 2 (drain)
+// runs the exact reference test on the queued candidates in list order, so the
 // wave pays for max-over-lanes candidates, not for their union.
 // Returns the best index (-1 = miss) and t.
 __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
@@ -213,39 +243,38 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
                                                , Prof& prof_
 #endif
                                                ) {
-    const float dd = dot(d, d);
-    const float l = sqrtf(dd);
-    const float a = l * l;                        // sqr(length(r.dir)), intersect.wgsl:98
-    const float rs = __builtin_amdgcn_rsqf(dd);  // filter only: approximate 1/|d|
-    const f2 ox = bc(o.x), oy = bc(o.y), oz = bc(o.z);
-    const f2 dx = bc(d.x * rs), dy = bc(d.y * rs), dz = bc(d.z * rs);
-    const f2 negk = bc(-(1.0f - 0x1p-16f));
+    const float l = sqrtf(dot(d, d));
+    const float a = l * l;  // sqr(length(r.dir)), intersect.wgsl:98
+    const RayF R = ray_filter_consts(o, d);
     const uint32_t lane = __lane_id();
     float best_t = VERY_FAR;
     int best_i = -1;
     uint32_t cnt = 0;
-    float4 p0 = grp[0], p1 = grp[1], p2 = grp[2], p3 = grp[3];
     for (uint32_t g = 0; g < ngroups; ++g) {
-        const float4 cx = p0, cy = p1, cz = p2, rr = p3;
-        const uint32_t nx = 4 * g + 4;  // prefetch the next group
-        p0 = grp[nx]; p1 = grp[nx + 1]; p2 = grp[nx + 2]; p3 = grp[nx + 3];
-        const f2 g01 = filter2(f2{cx.x, cx.y}, f2{cy.x, cy.y}, f2{cz.x, cz.y}, f2{rr.x, rr.y},
-                               ox, oy, oz, dx, dy, dz, negk);
-        const f2 g23 = filter2(f2{cx.z, cx.w}, f2{cy.z, cy.w}, f2{cz.z, cz.w}, f2{rr.z, rr.w},
-                               ox, oy, oz, dx, dy, dz, negk);
-        // group skip: all four G < 0 (a NaN G is dropped by max: NaN G never hits)
-        const float gm = fmaxf(fmaxf(g01.x, g01.y), fmaxf(g23.x, g23.y));
-        if (__ballot(!(gm < 0.0f)) != 0) {
+        const float4* p = grp + (size_t)g * 8;
+        const float4 X0 = p[0], X1 = p[1], Y0 = p[2], Y1 = p[3];
+        const float4 Z0 = p[4], Z1 = p[5], S0 = p[6], S1 = p[7];
+        const f2 g01 = filter2(f2{X0.x, X0.y}, f2{Y0.x, Y0.y}, f2{Z0.x, Z0.y}, f2{S0.x, S0.y}, R);
+        const f2 g23 = filter2(f2{X0.z, X0.w}, f2{Y0.z, Y0.w}, f2{Z0.z, Z0.w}, f2{S0.z, S0.w}, R);
+        const f2 g45 = filter2(f2{X1.x, X1.y}, f2{Y1.x, Y1.y}, f2{Z1.x, Z1.y}, f2{S1.x, S1.y}, R);
+        const f2 g67 = filter2(f2{X1.z, X1.w}, f2{Y1.z, Y1.w}, f2{Z1.z, Z1.w}, f2{S1.z, S1.w}, R);
+        const uint32_t all_neg = __float_as_uint(g01.x) & __float_as_uint(g01.y) &
+                                 __float_as_uint(g23.x) & __float_as_uint(g23.y) &
+                                 __float_as_uint(g45.x) & __float_as_uint(g45.y) &
+                                 __float_as_uint(g67.x) & __float_as_uint(g67.y);
+        if (__ballot((int)all_neg >= 0) != 0) {
             PROF_ADD(5, 1);
             if (__ballot(cnt >= RT_CQ_CAP) != 0) {  // a lane's queue is full: drain all
                 PROF_ADD(11, 1);
                 drain_candidates(cq, cnt, sph, o, d, a, best_t, best_i);
                 cnt = 0;
             }
-            const uint32_t m = (uint32_t)!(g01.x < 0.0f) | ((uint32_t)!(g01.y < 0.0f) << 1) |
-                               ((uint32_t)!(g23.x < 0.0f) << 2) | ((uint32_t)!(g23.y < 0.0f) << 3);
+            const uint32_t m = sgn_clear(g01.x) | (sgn_clear(g01.y) << 1) |
+                               (sgn_clear(g23.x) << 2) | (sgn_clear(g23.y) << 3) |
+                               (sgn_clear(g45.x) << 4) | (sgn_clear(g45.y) << 5) |
+                               (sgn_clear(g67.x) << 6) | (sgn_clear(g67.y) << 7);
             if (m) {
-                cq[cnt * 64 + lane] = (g << 4) | m;
+                cq[cnt * 64 + lane] = (g << 8) | m;
                 ++cnt;
             }
         }
@@ -491,6 +520,30 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
     }
 }
 
+// Batch closest-hit query (rt_intersect): one ray per lane, same intersect_world.
+__global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_kernel(
+    const float4* __restrict__ grp, const float4* __restrict__ sph, uint32_t ngroups,
+    const float* __restrict__ rays, uint32_t n, int* __restrict__ out_i, float* __restrict__ out_t) {
+    __shared__ uint32_t s_cq[RT_BLOCK_THREADS * RT_CQ_CAP];
+    uint32_t* cq = s_cq + (threadIdx.x / 64u) * (64u * RT_CQ_CAP);
+#ifdef RT_PROFILE
+    PROF_DECL
+    PROF_START();
+#endif
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float* r = rays + (size_t)i * 6;
+    float t;
+    const int hi = intersect_world(grp, sph, ngroups, mk(r[0], r[1], r[2]), mk(r[3], r[4], r[5]),
+                                   t, cq
+#ifdef RT_PROFILE
+                                   , prof_
+#endif
+                                   );
+    out_i[i] = hi;
+    out_t[i] = t;
+}
+
 // Fold this pass's block sums into acc (block order) and, on the last pass,
 // write out = acc / spp with alpha 1 (collect.wgsl:115-125).
 __global__ void rt_collect_kernel(const float4* __restrict__ block_sums, uint32_t npix,
@@ -559,6 +612,15 @@ hipError_t rt_launch_assemble(const float4* gathered, uint32_t max_rows, float4*
     const size_t n = (size_t)width * height;
     hipLaunchKernelGGL(rt_assemble_kernel, dim3((uint32_t)((n + T - 1) / T)), dim3(T), 0, stream,
                        gathered, max_rows, image, width, height, row_block, shard_count);
+    return hipGetLastError();
+}
+
+hipError_t rt_launch_intersect(const float4* grp, const float4* sph, uint32_t ngroups,
+                               const float* rays, uint32_t n, int* out_i, float* out_t,
+                               hipStream_t stream) {
+    const uint32_t T = RT_BLOCK_THREADS;
+    hipLaunchKernelGGL(rt_intersect_kernel, dim3((n + T - 1) / T), dim3(T), 0, stream, grp, sph,
+                       ngroups, rays, n, out_i, out_t);
     return hipGetLastError();
 }
 

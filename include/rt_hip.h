@@ -178,6 +178,13 @@ int rt_render_async(rt_ctx* ctx, const rt_camera* camera, const rt_params* param
                     float* out_rgba);
 int rt_wait(rt_ctx* ctx, rt_stats* stats);
 
+/* Closest-hit query for a batch of rays against the current scene: the same
+ * intersect_world code path the renderer traces with (intersect.wgsl:133-143).
+ * rays: n x 6 floats (origin xyz, direction xyz), HOST memory. Outputs (host):
+ * hit_index[i] = sphere index or -1 (miss), hit_t[i] = t (1e20 on a miss).
+ * Synchronous. Used for picking and for the intersection parity tests. */
+int rt_intersect(rt_ctx* ctx, const float* rays, uint32_t n, int32_t* hit_index, float* hit_t);
+
 /* Re-assemble gathered shard outputs into the full image on the device:
  * gathered = shard_count consecutive slabs of max_rows*width*4 floats (slab k =
  * shard k's output, padded to max_rows rows); image = height*width*4 floats. */

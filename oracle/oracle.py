@@ -43,6 +43,7 @@ def load():
         lib.rto_sky.argtypes = [fp, fp]
         lib.rto_intersect.argtypes = [vp, u32, fp, fp, fp, fp, fp, ctypes.POINTER(u32)]
         lib.rto_intersect.restype = ctypes.c_int
+        lib.rto_intersect_batch.argtypes = [vp, u32, vp, u32, vp, vp, ctypes.c_int]
         lib.rto_trace_path.argtypes = [vp, vp, u32, vp, u32, u32, u32, u32, u32, u32, u32, fp,
                                        ctypes.POINTER(u32)]
         lib.rto_render.argtypes = [vp, vp, u32, vp, u32, ctypes.POINTER(_Params), vp,
@@ -84,6 +85,17 @@ def sky(d):
     out = _f3()
     load().rto_sky(_f3(d), out)
     return np.array(out[:], np.float32)
+
+
+def intersect_batch(spheres, rays, nthreads=None):
+    """rays (n, 6) float32 -> (index int32, t float32), intersect.wgsl:133-143."""
+    r = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 6)
+    idx = np.empty(r.shape[0], np.int32)
+    t = np.empty(r.shape[0], np.float32)
+    load().rto_intersect_batch(_ptr(spheres), len(spheres), r.ctypes.data_as(ctypes.c_void_p),
+                               r.shape[0], idx.ctypes.data_as(ctypes.c_void_p),
+                               t.ctypes.data_as(ctypes.c_void_p), nthreads or os.cpu_count() or 1)
+    return idx, t
 
 
 def trace_path(cam, spheres, materials, width, height, x, y, frame, max_depth):

@@ -194,6 +194,42 @@ int rto_intersect(const rt_sphere* spheres, uint32_t n, const float origin[3],
     return i;
 }
 
+typedef struct {
+    const rt_sphere* s;
+    uint32_t n;
+    const float* rays;
+    uint32_t nrays;
+    int32_t* idx;
+    float* t;
+    int tid, nt;
+} ijob_t;
+
+static void* iworker(void* arg) {
+    ijob_t* j = (ijob_t*)arg;
+    for (uint32_t r = (uint32_t)j->tid; r < j->nrays; r += (uint32_t)j->nt) {
+        const float* q = j->rays + (size_t)r * 6;
+        hit_t h;
+        int i = intersect_world(j->s, j->n, mk(q[0], q[1], q[2]), mk(q[3], q[4], q[5]), &h);
+        j->idx[r] = i;
+        j->t[r] = i >= 0 ? h.t : VERY_FAR;
+    }
+    return NULL;
+}
+
+void rto_intersect_batch(const rt_sphere* spheres, uint32_t n, const float* rays,
+                         uint32_t nrays, int32_t* idx, float* t, int nthreads) {
+    if (nthreads <= 0) nthreads = 1;
+    ijob_t* jobs = (ijob_t*)calloc((size_t)nthreads, sizeof(ijob_t));
+    pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+    for (int k = 0; k < nthreads; ++k) {
+        jobs[k] = (ijob_t){spheres, n, rays, nrays, idx, t, k, nthreads};
+        pthread_create(&th[k], NULL, iworker, &jobs[k]);
+    }
+    for (int k = 0; k < nthreads; ++k) pthread_join(th[k], NULL);
+    free(jobs);
+    free(th);
+}
+
 static inline v3 reflect(v3 v, v3 n) {                   /* shade.wgsl:132-134 */
     float k = 2.0f * dot(v, n);
     return sub(v, scale(n, k));

@@ -44,6 +44,10 @@ int rto_intersect(const rt_sphere* spheres, uint32_t n, const float origin[3],
                   const float dir[3], float* t, float pos[3], float normal[3],
                   uint32_t* front_face);
 
+/* Batch of rays (n x 6 floats: origin, direction) -> index (-1 miss) and t. */
+void rto_intersect_batch(const rt_sphere* spheres, uint32_t n, const float* rays,
+                         uint32_t nrays, int32_t* idx, float* t, int nthreads);
+
 /* One path: colour of sample `frame` of pixel (x, y), and its segment count. */
 void rto_trace_path(const rt_camera* cam, const rt_sphere* spheres, uint32_t n,
                     const rt_material* materials, uint32_t m, uint32_t width,
