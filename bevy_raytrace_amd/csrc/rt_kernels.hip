@@ -175,7 +175,7 @@ __device__ __forceinline__ f2 bc(float x) { return f2{x, x}; }
 // m = 2^-16 bounds the exact path's rounding relative to |o - c|^2 + r^2,
 // mu = 2^-17 the expanded form's cancellation relative to |o|^2 + |c|^2.
 struct RayF {
-    f2 dx, dy, dz, o2x, o2y, o2z, k1, K;
+    f2 dx, dy, dz, o2x, o2y, o2z, k1, K;  // dx,dy,dz hold -dn
 };
 
 __device__ __forceinline__ RayF ray_filter_consts(v3 o, v3 d) {
@@ -186,7 +186,7 @@ __device__ __forceinline__ RayF ray_filter_consts(v3 o, v3 d) {
     const float k1 = __builtin_fmaf(dnz, o.z, __builtin_fmaf(dny, o.y, dnx * o.x));
     const float two = 2.0f * (1.0f - m);
     RayF r;
-    r.dx = bc(dnx); r.dy = bc(dny); r.dz = bc(dnz);
+    r.dx = bc(-dnx); r.dy = bc(-dny); r.dz = bc(-dnz);  // negated: hb = k1 + (-dn).c
     r.o2x = bc(two * o.x); r.o2y = bc(two * o.y); r.o2z = bc(two * o.z);
     r.k1 = bc(k1);
     r.K = bc(-(1.0f - m - mu) * oo);
@@ -195,10 +195,9 @@ __device__ __forceinline__ RayF ray_filter_consts(v3 o, v3 d) {
 
 // Filter two spheres at once: 9 packed fp32 ops (v_pk_fma/mul/add_f32 -- the
 // only way to the 157.3 TF fp32 peak on gfx950, tools/ubench/fma_rate.hip).
-// G' < 0 => certain miss.
+// G' < 0 => certain miss. 8 packed ops per sphere pair.
 __device__ __forceinline__ f2 filter2(f2 cx, f2 cy, f2 cz, f2 S, const RayF& r) {
-    const f2 dc = pk_fma(r.dz, cz, pk_fma(r.dy, cy, r.dx * cx));
-    const f2 hb = r.k1 - dc;
+    const f2 hb = pk_fma(r.dz, cz, pk_fma(r.dy, cy, pk_fma(r.dx, cx, r.k1)));  // k1 - dn.c
     const f2 u = pk_fma(r.o2x, cx, pk_fma(r.o2y, cy, pk_fma(r.o2z, cz, S + r.K)));
     return pk_fma(hb, hb, u);
 }
@@ -298,6 +297,7 @@ __device__ __forceinline__ uint32_t lanemask_lt_count(uint64_t m) {
 // Lane state of one in-flight path.
 struct PathState {
     v3 o, d;            // current ray
+    v3 pd;              // primary direction of this pixel (generate.wgsl: pixel-only)
     v3 color;           // throughput (intersection.color, clear.wgsl:86)
     v3 bsum;            // sum of finished samples of the current block
     v3 nseed;           // normalize(seed)
@@ -308,12 +308,16 @@ struct PathState {
     uint32_t bounce;
 };
 
+// New sample s of the lane's pixel: seed (shade.wgsl:216-218), primary ray
+// (generate.wgsl:109-129; origin = camera translation, direction cached per
+// item since it depends on the pixel only), throughput 1 (clear.wgsl:86).
 __device__ __forceinline__ void start_sample(const KParams& P, PathState& st) {
     const uint32_t frame = P.frame0 + st.s;
     const v3 seed = hash3(st.x + P.width * st.y + (P.width * P.height) * frame);
     st.seedx = seed.x;
     st.nseed = normalize(seed);
-    primary_ray(P, st.x, st.y, st.o, st.d);
+    st.o = mk(0.0f + P.T[12], 0.0f + P.T[13], 0.0f + P.T[14]);
+    st.d = st.pd;
     st.color = mk(1.0f, 1.0f, 1.0f);
     st.bounce = 0;
 }
@@ -330,56 +334,71 @@ __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint
     st.s = b * RT_SAMPLE_BLOCK;
     st.s_end = min(P.spp, st.s + RT_SAMPLE_BLOCK);
     st.bsum = mk(0.0f, 0.0f, 0.0f);
+    v3 po;
+    primary_ray(P, st.x, st.y, po, st.pd);
     start_sample(P, st);
 }
 
 // One path step after an intersection: shade.wgsl:199-258 for hit `hi` at t.
 // Returns true when the path has finished (miss, or hit at bounce D-1).
+// Written as converged stages so that each normalize (correctly rounded sqrt
+// + 3 divides) is issued once per wave, not once per material branch:
+//   record  : hit point + normal (intersect.wgsl:117-127)
+//   pre     : normalize(reflect(d,n)) for metal, normalize(d) for dielectric
+//   select  : per-material arithmetic producing the vector to normalize
+//   post    : normalize(d) for the sky, the new direction otherwise
+// Every lane performs exactly the reference's op sequence for its case.
 __device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, float t,
                                       const float4* __restrict__ sph,
                                       const float2* __restrict__ sph_rm,
                                       const rt_material* __restrict__ mats) {
-    if (hi < 0) {  // miss, shade.wgsl:229-233
-        st.color = mul(st.color, sky(st.d));
-        return true;
-    }
-    if (st.bounce == P.max_depth - 1) {  // shade.wgsl:236-238
+    const bool miss = hi < 0;
+    if (!miss && st.bounce == P.max_depth - 1) {  // shade.wgsl:236-238
         st.color = mk(0.0f, 0.0f, 0.0f);
         return true;
     }
-    const float4 s = sph[hi];
-    const float2 rm = sph_rm[hi];
-    const float radius = rm.x;
-    const uint32_t mi = __float_as_uint(rm.y);
-    // hit record, intersect.wgsl:117-127
-    const v3 pos = add(st.o, scale(st.d, t));
-    const v3 q = sub(pos, mk(s.x, s.y, s.z));
-    v3 nrm = normalize(mk(q.x / radius, q.y / radius, q.z / radius));
+    // ---- record (hit lanes)
+    v3 pos = mk(0.0f, 0.0f, 0.0f), nrm = mk(0.0f, 0.0f, 0.0f);
     bool front = true;
-    if (dot(st.d, nrm) > 0.0f) {
-        nrm = neg(nrm);
-        front = false;
+    int refl = -1;
+    float4 mc = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+    float fuzz = 0.0f, ior = 1.0f;
+    if (!miss) {
+        const float4 s = sph[hi];
+        const float2 rm = sph_rm[hi];
+        const float radius = rm.x;
+        const uint32_t mi = __float_as_uint(rm.y);
+        pos = add(st.o, scale(st.d, t));
+        const v3 q = sub(pos, mk(s.x, s.y, s.z));
+        nrm = normalize(mk(q.x / radius, q.y / radius, q.z / radius));
+        if (dot(st.d, nrm) > 0.0f) {
+            nrm = neg(nrm);
+            front = false;
+        }
+        const rt_material& m = mats[mi];
+        refl = m.reflectance;
+        mc = *reinterpret_cast<const float4*>(m.color);
+        fuzz = m.fuzziness;
+        ior = m.index_of_refraction;
     }
-    const rt_material& m = mats[mi];
-    const int refl = m.reflectance;
-    if (refl == RT_LAMBERTIAN) {  // shade.wgsl:118-130
+    // ---- pre-normalize: metal normalize(reflect(d, n)) (shade.wgsl:140),
+    //      dielectric unit_dir = normalize(d) (shade.wgsl:169)
+    v3 un = mk(0.0f, 0.0f, 0.0f);
+    if (refl == RT_METALLIC || refl == RT_DIELECTRIC)
+        un = normalize(refl == RT_METALLIC ? reflect(st.d, nrm) : st.d);
+    // ---- select
+    v3 v = st.d;           // vector to normalize (sky: d, shade.wgsl:190)
+    bool post = true;      // false: dielectric reflection keeps reflect(d, n) unnormalized
+    v3 e_dir_raw = mk(0.0f, 0.0f, 0.0f);
+    if (refl == RT_LAMBERTIAN) {  // shade.wgsl:121-124
         const v3 dest = add(add(pos, nrm), st.nseed);
-        st.d = normalize(sub(dest, pos));
-        st.o = pos;
-        st.color = mul(st.color, mk(m.color[0], m.color[1], m.color[2]));
-    } else if (refl == RT_METALLIC) {  // shade.wgsl:136-146
-        const v3 e_origin = add(pos, scale(nrm, EPSILON));
-        const v3 reflected = normalize(reflect(st.d, nrm));
-        const v3 noise = scale(st.nseed, m.fuzziness);
-        st.d = normalize(add(reflected, noise));
-        st.o = e_origin;
-        st.color = mul(st.color, mk(m.color[0], m.color[1], m.color[2]));
-    } else {  // dielectric, shade.wgsl:163-187 (attenuation 1)
-        const float ior = m.index_of_refraction;
+        v = sub(dest, pos);
+    } else if (refl == RT_METALLIC) {  // shade.wgsl:141-142
+        v = add(un, scale(st.nseed, fuzz));
+    } else if (refl == RT_DIELECTRIC) {  // shade.wgsl:164-180
         float ratio = ior;
         if (front) ratio = 1.0f / ior;
-        const v3 unit_dir = normalize(st.d);
-        const float cos_theta = fminf(dot(neg(unit_dir), nrm), 1.0f);
+        const float cos_theta = fminf(dot(neg(un), nrm), 1.0f);
         const float sin_theta = sqrtf(1.0f - cos_theta * cos_theta);
         const bool cannot_refract = ratio * sin_theta > 1.0f;
         float r0 = (1.0f - ratio) / (1.0f + ratio);  // reflectance(), shade.wgsl:156-161
@@ -387,18 +406,33 @@ __device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, f
         const float xr = 1.0f - cos_theta;
         const float x2 = xr * xr;
         const float refl_p = r0 + (1.0f - r0) * ((x2 * x2) * xr);
-        v3 e_dir;
         if (cannot_refract || refl_p > st.seedx) {
-            e_dir = reflect(st.d, nrm);
-        } else {  // refract, shade.wgsl:148-154
-            const float ct = fminf(dot(neg(unit_dir), nrm), 1.0f);
-            const v3 perp = scale(add(unit_dir, scale(nrm, ct)), ratio);
+            e_dir_raw = reflect(st.d, nrm);
+            post = false;
+        } else {  // refract(unit_dir, n, ratio), shade.wgsl:148-153
+            const v3 perp = scale(add(un, scale(nrm, cos_theta)), ratio);
             const float lp = length(perp);
             const float par = -sqrtf(fabsf(1.0f - (lp * lp)));
-            e_dir = normalize(add(perp, scale(nrm, par)));
+            v = add(perp, scale(nrm, par));
         }
-        st.o = add(pos, scale(nrm, EPSILON));
-        st.d = e_dir;
+    }
+    // ---- post-normalize
+    v3 vn = mk(0.0f, 0.0f, 0.0f);
+    if (post) vn = normalize(v);
+    if (miss) {  // miss(), shade.wgsl:189-197, color *= sky
+        const float tt = 0.5f * vn.y + 1.0f;
+        const float omt = (1.0f - tt) * 1.0f;
+        st.color = mul(st.color, mk(omt + tt * 0.5f, omt + tt * 0.7f, omt + tt * 1.0f));
+        return true;
+    }
+    if (refl == RT_LAMBERTIAN) {
+        st.o = pos;  // no offset (shade.wgsl:123)
+        st.d = vn;
+        st.color = mul(st.color, mk(mc.x, mc.y, mc.z));
+    } else {
+        st.o = add(pos, scale(nrm, EPSILON));  // shade.wgsl:139, 182
+        st.d = post ? vn : e_dir_raw;
+        if (refl == RT_METALLIC) st.color = mul(st.color, mk(mc.x, mc.y, mc.z));
     }
     ++st.bounce;
     return false;
