@@ -202,3 +202,23 @@ def test_native_library_is_in_tree():
     """The product path runs librt_hip.so from the package directory."""
     lib = abi.load()
     assert os.path.dirname(lib._name) == abi.PKG_DIR
+
+
+def test_plugin_frames_match_oracle():
+    """RayTracePlugin/RayTraceNode mirror: the reference's own schedule
+    (spp 1, depth 3, frame counter advancing) on a small target."""
+    from bevy_raytrace_amd.camera import RayTraceCamera
+    from bevy_raytrace_amd.plugin import (FrameCounter, RayTraceOutputImage, RayTracePlugin,
+                                          RayTraceSettings, World)
+    world = World()
+    world.insert_resource(RayTraceCamera(160, 90))
+    sc = scene.reference_scene()
+    node = RayTracePlugin(RayTraceSettings(), sc).build(world)
+    sp, mt = arrays(sc)
+    for f in range(3):
+        RayTracePlugin.frame(world, node)
+        img = world.resource(RayTraceOutputImage).data
+        ref, segs = O.render(RayTraceCamera(160, 90).to_gpu(), sp, mt, 160, 90, 1, 3, frame0=f)
+        check_exact(img, ref)
+        assert node.last_stats["segments"] == segs
+    assert world.resource(FrameCounter).frame == 3
