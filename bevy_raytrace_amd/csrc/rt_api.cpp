@@ -56,6 +56,8 @@ struct rt_ctx {
     size_t bs_cap = 0;
     float4* d_acc = nullptr;
     size_t acc_cap = 0;
+    float4* d_pd = nullptr;         // per-pixel primary directions (rt_primary_kernel)
+    size_t pd_cap = 0;
     float4* d_out = nullptr;        // host-output path staging
     size_t out_cap = 0;
     uint32_t* d_counters = nullptr; // [0..3] 2 x u64 segment counters, [4..] per-pass work counters
@@ -107,6 +109,18 @@ static int ensure(rt_ctx* ctx, T** p, size_t* cap, size_t bytes) {
     HIP_TRY(ctx, hipMalloc((void**)p, bytes));
     *cap = bytes;
     return RT_OK;
+}
+
+// Granlund-Montgomery constants for FastDiv (rt_internal.h).
+static FastDiv make_fastdiv(uint32_t d) {
+    FastDiv f{};
+    f.d = d;
+    uint32_t l = 0;
+    while (l < 32 && (1ull << l) < d) ++l;  // l = ceil(log2 d)
+    f.m = (uint32_t)((((1ull << l) - d) << 32) / d + 1);
+    f.sh1 = l < 1 ? l : 1;
+    f.sh2 = l > 1 ? l - 1 : 0;
+    return f;
 }
 
 static size_t scratch_limit() {
@@ -184,6 +198,7 @@ void rt_destroy(rt_ctx* ctx) {
     hipFree(ctx->d_block_sums);
     hipFree(ctx->d_acc);
     hipFree(ctx->d_out);
+    hipFree(ctx->d_pd);
     hipFree(ctx->d_counters);
     if (ctx->h_segs) hipHostFree(ctx->h_segs);
     for (hipEvent_t e : ctx->ev) hipEventDestroy(e);
@@ -302,6 +317,8 @@ static int enqueue(rt_ctx* ctx, const rt_camera* cam, const rt_params* prm, floa
         }
         int rc = ensure(ctx, &ctx->d_block_sums, &ctx->bs_cap, per_block * (size_t)pb);
         if (rc) return rc;
+        rc = ensure(ctx, &ctx->d_pd, &ctx->pd_cap, per_block);
+        if (rc) return rc;
         if (passes.size() > 1) {
             rc = ensure(ctx, &ctx->d_acc, &ctx->acc_cap, per_block);
             if (rc) return rc;
@@ -339,10 +356,14 @@ static int enqueue(rt_ctx* ctx, const rt_camera* cam, const rt_params* prm, floa
     K_.aspect = (float)p.width;
     K_.half_w = (float)p.width / 2.0f;
     K_.half_h = (float)p.height / 2.0f;
+    K_.div_npix = make_fastdiv(npix ? npix : 1);
+    K_.div_width = make_fastdiv(p.width);
+    K_.div_row_block = make_fastdiv(B);
 
     HIP_TRY(ctx, hipEventRecord(ctx->ev_t0, stream));
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, words_pad * sizeof(uint32_t), stream));
     const uint32_t grid_full = (uint32_t)(ctx->cu_count * ctx->blocks_per_cu);
+    if (npix) HIP_TRY(ctx, rt_launch_primary(&K_, ctx->d_pd, stream));
     for (size_t i = 0; i < passes.size(); ++i) {
         K_.block_begin = passes[i].block_begin;
         K_.nblocks = passes[i].nblocks;
@@ -351,7 +372,8 @@ static int enqueue(rt_ctx* ctx, const rt_camera* cam, const rt_params* prm, floa
         const uint64_t need_blocks = (chunks + (RT_BLOCK_THREADS / 64) - 1) / (RT_BLOCK_THREADS / 64);
         const uint32_t grid = (uint32_t)(need_blocks < grid_full ? need_blocks : grid_full);
         HIP_TRY(ctx, hipEventRecord(ctx->ev[2 * i], stream));
-        HIP_TRY(ctx, rt_launch_render(&K_, ctx->d_grp, ctx->d_sph, ctx->d_sph_rm, ctx->d_mats, ctx->d_block_sums,
+        HIP_TRY(ctx, rt_launch_render(&K_, ctx->d_grp, ctx->d_sph, ctx->d_sph_rm, ctx->d_mats, ctx->d_pd,
+                                      ctx->d_block_sums,
                                       ctx->d_counters + RT_CNT_WORK_OFFSET + i,
                                       reinterpret_cast<unsigned long long*>(ctx->d_counters),
                                       grid, stream));

@@ -17,8 +17,14 @@
 #define RT_CQ_CAP 8           // candidate-queue entries per lane (LDS)
 #endif
 #ifndef RT_MIN_WAVES_PER_SIMD
-#define RT_MIN_WAVES_PER_SIMD 4
+#define RT_MIN_WAVES_PER_SIMD 6
 #endif
+
+// Unsigned 32-bit division by a run-time invariant d >= 1 as a multiply-high
+// (Granlund & Montgomery 1994, Fig. 4.1): exact for every 32-bit n.
+struct FastDiv {
+    uint32_t m, sh1, sh2, d;
+};
 
 // Kernel parameters (by value; lands in SGPRs). Camera constants are
 // precomputed on the host exactly as generate.wgsl:67-95 computes them.
@@ -33,11 +39,13 @@ struct KParams {
     uint32_t flags;
     float T[16];           // camera transform, column-major
     float tan_half, focus_plane, aspect, half_w, half_h;
+    FastDiv div_npix, div_width, div_row_block;
 };
 
 extern "C" {
 hipError_t rt_launch_render(const KParams* P, const float4* grp, const float4* sph,
-                            const float2* sph_rm, const rt_material* mats, float4* block_sums,
+                            const float2* sph_rm, const rt_material* mats, const float4* pd,
+                            float4* block_sums,
                             uint32_t* work_counter, unsigned long long* seg_counter, uint32_t grid,
                             hipStream_t stream);
 hipError_t rt_launch_collect(const float4* block_sums, uint32_t npix, uint32_t nblocks,
@@ -50,4 +58,5 @@ hipError_t rt_launch_intersect(const float4* grp, const float4* sph, uint32_t ng
                                const float* rays, uint32_t n, int* out_i, float* out_t,
                                hipStream_t stream);
 hipError_t rt_render_occupancy(int* blocks_per_cu);
+hipError_t rt_launch_primary(const KParams* P, float4* pd, hipStream_t stream);
 }

@@ -136,8 +136,19 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 
 // Exact reference test of one sphere (intersect.wgsl:97-115 + :137).
 // s.w = RN(radius*radius) = sqr(s.radius); r2p = s.w * (1 + 2^-20).
+#ifdef RT_PROFILE
+__device__ uint32_t g_prof_dummy;
+#define EXACT_COUNT(k) (ecnt[k]++)
+#define EXACT_ARGS , uint32_t* ecnt
+#define EXACT_PASS , ecnt
+#else
+#define EXACT_COUNT(k)
+#define EXACT_ARGS
+#define EXACT_PASS
+#endif
 __device__ __forceinline__ void exact_test(float4 s, int idx, v3 o, v3 d, float a,
-                                           float& best_t, int& best_i) {
+                                           float& best_t, int& best_i EXACT_ARGS) {
+    EXACT_COUNT(0);
     const v3 oc = mk(o.x - s.x, o.y - s.y, o.z - s.z);
     const float half_b = dot(oc, d);
     const float qq = dot(oc, oc);
@@ -146,6 +157,7 @@ __device__ __forceinline__ void exact_test(float4 s, int idx, v3 o, v3 d, float 
     // trip). Then dis <= half_b^2, sqrt(dis) <= half_b, and both roots are
     // <= 0 < EPSILON, exactly as the full evaluation below would find.
     if (half_b >= 0.0f && qq >= s.w * (1.0f + 0x1p-20f)) return;
+    EXACT_COUNT(1);
     const float lo = sqrtf(qq);
     const float c = lo * lo - s.w;
     const float dis = half_b * half_b - a * c;
@@ -175,7 +187,8 @@ __device__ __forceinline__ f2 bc(float x) { return f2{x, x}; }
 // m = 2^-16 bounds the exact path's rounding relative to |o - c|^2 + r^2,
 // mu = 2^-17 the expanded form's cancellation relative to |o|^2 + |c|^2.
 struct RayF {
-    f2 dx, dy, dz, o2x, o2y, o2z, k1, K;  // dx,dy,dz hold -dn
+    f2 dx, dy, dz, o2x, o2y, o2z, k1;  // dx,dy,dz hold -dn
+    float T;                           // candidate threshold -K
 };
 
 __device__ __forceinline__ RayF ray_filter_consts(v3 o, v3 d) {
@@ -189,28 +202,27 @@ __device__ __forceinline__ RayF ray_filter_consts(v3 o, v3 d) {
     r.dx = bc(-dnx); r.dy = bc(-dny); r.dz = bc(-dnz);  // negated: hb = k1 + (-dn).c
     r.o2x = bc(two * o.x); r.o2y = bc(two * o.y); r.o2z = bc(two * o.z);
     r.k1 = bc(k1);
-    r.K = bc(-(1.0f - m - mu) * oo);
+    r.T = (1.0f - m - mu) * oo;
     return r;
 }
 
 // Filter two spheres at once: 9 packed fp32 ops (v_pk_fma/mul/add_f32 -- the
 // only way to the 157.3 TF fp32 peak on gfx950, tools/ubench/fma_rate.hip).
-// G' < 0 => certain miss. 8 packed ops per sphere pair.
+// Returns H = hb^2 + S + o2.c; G' = H + K, so "G' >= 0" is "H >= T" with the
+// per-ray threshold T = -K (an exact comparison). 7 packed ops per sphere pair.
 __device__ __forceinline__ f2 filter2(f2 cx, f2 cy, f2 cz, f2 S, const RayF& r) {
+    // every op has ONE SGPR-pair operand (sphere data) -- the constant-bus limit
     const f2 hb = pk_fma(r.dz, cz, pk_fma(r.dy, cy, pk_fma(r.dx, cx, r.k1)));  // k1 - dn.c
-    const f2 u = pk_fma(r.o2x, cx, pk_fma(r.o2y, cy, pk_fma(r.o2z, cz, S + r.K)));
-    return pk_fma(hb, hb, u);
+    return pk_fma(r.o2x, cx, pk_fma(r.o2y, cy, pk_fma(r.o2z, cz, pk_fma(hb, hb, S))));
 }
 
-__device__ __forceinline__ uint32_t sgn_clear(float g) {  // 1 if the sign bit of g is clear
-    return (~__float_as_uint(g)) >> 31;
-}
+__device__ __forceinline__ uint32_t ge(float h, float t) { return h >= t ? 1u : 0u; }
 
 // Run the exact test for every queued candidate of this lane, in list order.
 // Queue entries are (group << 8 | 8-bit candidate mask), one column per lane.
 __device__ __forceinline__ void drain_candidates(const uint32_t* cq, uint32_t cnt,
                                                  const float4* __restrict__ sph, v3 o, v3 d,
-                                                 float a, float& best_t, int& best_i) {
+                                                 float a, float& best_t, int& best_i EXACT_ARGS) {
     const uint32_t lane = __lane_id();
     for (uint32_t k = 0; k < cnt; ++k) {
         const uint32_t e = cq[k * 64 + lane];
@@ -219,7 +231,7 @@ __device__ __forceinline__ void drain_candidates(const uint32_t* cq, uint32_t cn
         while (m) {
             const uint32_t j = __builtin_ctz(m);
             m &= m - 1;
-            exact_test(sph[base + j], (int)(base + j), o, d, a, best_t, best_i);
+            exact_test(sph[base + j], (int)(base + j), o, d, a, best_t, best_i EXACT_PASS);
         }
     }
 }
@@ -230,8 +242,7 @@ __device__ __forceinline__ void drain_candidates(const uint32_t* cq, uint32_t cn
 // Wave-uniform: read with s_load_dwordx16 and fed to the packed ops as SGPR
 // pairs. sph: the padded records AoS (cx, cy, cz, r2), gathered per lane by
 // the exact tests. Pass 1 filters every sphere and queues candidates per lane
-// (LDS, cq); the group test is one AND of the 8 sign bits (a G' of -0 or a NaN
-// with the sign set is dropped: neither can hit). Pass 2 (drain)
+// (LDS, cq); the group test is max(H) >= T over the 8 spheres. Pass 2 (drain)
 // runs the exact reference test on the queued candidates in list order, so the
 // wave pays for max-over-lanes candidates, not for their union.
 // Returns the best index (-1 = miss) and t.
@@ -249,6 +260,9 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
     float best_t = VERY_FAR;
     int best_i = -1;
     uint32_t cnt = 0;
+#ifdef RT_PROFILE
+    uint32_t ecnt[2] = {0, 0};
+#endif
     for (uint32_t g = 0; g < ngroups; ++g) {
         const float4* p = grp + (size_t)g * 8;
         const float4 X0 = p[0], X1 = p[1], Y0 = p[2], Y1 = p[3];
@@ -257,21 +271,21 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
         const f2 g23 = filter2(f2{X0.z, X0.w}, f2{Y0.z, Y0.w}, f2{Z0.z, Z0.w}, f2{S0.z, S0.w}, R);
         const f2 g45 = filter2(f2{X1.x, X1.y}, f2{Y1.x, Y1.y}, f2{Z1.x, Z1.y}, f2{S1.x, S1.y}, R);
         const f2 g67 = filter2(f2{X1.z, X1.w}, f2{Y1.z, Y1.w}, f2{Z1.z, Z1.w}, f2{S1.z, S1.w}, R);
-        const uint32_t all_neg = __float_as_uint(g01.x) & __float_as_uint(g01.y) &
-                                 __float_as_uint(g23.x) & __float_as_uint(g23.y) &
-                                 __float_as_uint(g45.x) & __float_as_uint(g45.y) &
-                                 __float_as_uint(g67.x) & __float_as_uint(g67.y);
-        if (__ballot((int)all_neg >= 0) != 0) {
+        // group test: max of the 8 H (v_max3 tree; a NaN H is dropped by
+        // max -- a NaN H never hits) against the ray's threshold
+        const float hmax = fmaxf(fmaxf(fmaxf(g01.x, g01.y), fmaxf(g23.x, g23.y)),
+                                 fmaxf(fmaxf(g45.x, g45.y), fmaxf(g67.x, g67.y)));
+        if (__ballot(hmax >= R.T) != 0) {
             PROF_ADD(5, 1);
             if (__ballot(cnt >= RT_CQ_CAP) != 0) {  // a lane's queue is full: drain all
                 PROF_ADD(11, 1);
-                drain_candidates(cq, cnt, sph, o, d, a, best_t, best_i);
+                drain_candidates(cq, cnt, sph, o, d, a, best_t, best_i EXACT_PASS);
                 cnt = 0;
             }
-            const uint32_t m = sgn_clear(g01.x) | (sgn_clear(g01.y) << 1) |
-                               (sgn_clear(g23.x) << 2) | (sgn_clear(g23.y) << 3) |
-                               (sgn_clear(g45.x) << 4) | (sgn_clear(g45.y) << 5) |
-                               (sgn_clear(g67.x) << 6) | (sgn_clear(g67.y) << 7);
+            const float T = R.T;
+            const uint32_t m = ge(g01.x, T) | (ge(g01.y, T) << 1) | (ge(g23.x, T) << 2) |
+                               (ge(g23.y, T) << 3) | (ge(g45.x, T) << 4) | (ge(g45.y, T) << 5) |
+                               (ge(g67.x, T) << 6) | (ge(g67.y, T) << 7);
             if (m) {
                 cq[cnt * 64 + lane] = (g << 8) | m;
                 ++cnt;
@@ -282,8 +296,17 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
 #ifdef RT_PROFILE
     PROF_ADD(6, wave_max_u32(cnt));
 #endif
-    drain_candidates(cq, cnt, sph, o, d, a, best_t, best_i);
+    drain_candidates(cq, cnt, sph, o, d, a, best_t, best_i EXACT_PASS);
     PROF_MARK(2);
+#ifdef RT_PROFILE
+    PROF_ADD(13, wave_max_u32(ecnt[0]));
+    PROF_ADD(14, wave_max_u32(ecnt[1]));
+    {
+        uint32_t sum0 = ecnt[0];
+        for (int off = 32; off > 0; off >>= 1) sum0 += __shfl_xor(sum0, off);
+        PROF_ADD(15, sum0);
+    }
+#endif
     t_out = best_t;
     return best_i;
 }
@@ -322,20 +345,31 @@ __device__ __forceinline__ void start_sample(const KParams& P, PathState& st) {
     st.bounce = 0;
 }
 
-__device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint32_t item) {
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+    const uint32_t t = __umulhi(f.m, n);
+    return (t + ((n - t) >> f.sh1)) >> f.sh2;
+}
+
+// Shard pixel p -> global (x, y): rows are interleaved blocks of row_block.
+__device__ __forceinline__ void pixel_xy(const KParams& P, uint32_t p, uint32_t& x, uint32_t& y) {
+    const uint32_t r = fdiv(p, P.div_width);
+    x = p - r * P.width;
+    const uint32_t rb = fdiv(r, P.div_row_block);
+    y = (rb * P.shard_count + P.shard_index) * P.row_block + (r - rb * P.row_block);
+}
+
+__device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint32_t item,
+                                           const float4* __restrict__ pd) {
     st.item = item;
-    const uint32_t bl = item / P.npix;
+    const uint32_t bl = fdiv(item, P.div_npix);
     const uint32_t p = item - bl * P.npix;
-    const uint32_t r = p / P.width;
-    st.x = p - r * P.width;
-    const uint32_t B = P.row_block;
-    st.y = ((r / B) * P.shard_count + P.shard_index) * B + (r % B);
+    pixel_xy(P, p, st.x, st.y);
     const uint32_t b = P.block_begin + bl;
     st.s = b * RT_SAMPLE_BLOCK;
     st.s_end = min(P.spp, st.s + RT_SAMPLE_BLOCK);
     st.bsum = mk(0.0f, 0.0f, 0.0f);
-    v3 po;
-    primary_ray(P, st.x, st.y, po, st.pd);
+    const float4 q = pd[p];  // primary direction, rt_primary_kernel
+    st.pd = mk(q.x, q.y, q.z);
     start_sample(P, st);
 }
 
@@ -441,7 +475,8 @@ __device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, f
 __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_render_kernel(
     KParams P, const float4* __restrict__ grp, const float4* __restrict__ sph,
     const float2* __restrict__ sph_rm, const rt_material* __restrict__ mats,
-    float4* __restrict__ block_sums, uint32_t* __restrict__ work_counter,
+    const float4* __restrict__ pd, float4* __restrict__ block_sums,
+    uint32_t* __restrict__ work_counter,
     unsigned long long* __restrict__ seg_counter, unsigned long long* __restrict__ dbg) {
     const uint32_t lane = threadIdx.x & 63u;
     PROF_DECL
@@ -481,7 +516,7 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
             const uint32_t rank = lanemask_lt_count(need);
             const uint32_t cnt = (uint32_t)__popcll(need);
             if (!has_item && rank < avail) {
-                start_item(P, st, q_next + rank);
+                start_item(P, st, q_next + rank, pd);
                 has_item = true;
             }
             q_next += min(avail, cnt);
@@ -554,6 +589,18 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
     }
 }
 
+// Primary ray direction of every shard pixel (generate.wgsl:66-126), once per
+// frame: the direction depends on the pixel only (lens offset 0, no jitter).
+__global__ void rt_primary_kernel(KParams P, float4* __restrict__ pd) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P.npix) return;
+    uint32_t x, y;
+    pixel_xy(P, p, x, y);
+    v3 o, d;
+    primary_ray(P, x, y, o, d);
+    pd[p] = make_float4(d.x, d.y, d.z, 0.0f);
+}
+
 // Batch closest-hit query (rt_intersect): one ray per lane, same intersect_world.
 __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_kernel(
     const float4* __restrict__ grp, const float4* __restrict__ sph, uint32_t ngroups,
@@ -622,11 +669,18 @@ __global__ void rt_assemble_kernel(const float4* __restrict__ gathered, uint32_t
 extern "C" {
 
 hipError_t rt_launch_render(const KParams* P, const float4* grp, const float4* sph,
-                            const float2* sph_rm, const rt_material* mats, float4* block_sums,
-                            uint32_t* work_counter, unsigned long long* seg_counter, uint32_t grid,
-                            hipStream_t stream) {
+                            const float2* sph_rm, const rt_material* mats, const float4* pd,
+                            float4* block_sums, uint32_t* work_counter,
+                            unsigned long long* seg_counter, uint32_t grid, hipStream_t stream) {
     hipLaunchKernelGGL(rt_render_kernel, dim3(grid), dim3(RT_BLOCK_THREADS), 0, stream, *P, grp,
-                       sph, sph_rm, mats, block_sums, work_counter, seg_counter, seg_counter + 2);
+                       sph, sph_rm, mats, pd, block_sums, work_counter, seg_counter,
+                       seg_counter + 2);
+    return hipGetLastError();
+}
+
+hipError_t rt_launch_primary(const KParams* P, float4* pd, hipStream_t stream) {
+    const uint32_t T = 256;
+    hipLaunchKernelGGL(rt_primary_kernel, dim3((P->npix + T - 1) / T), dim3(T), 0, stream, *P, pd);
     return hipGetLastError();
 }
 

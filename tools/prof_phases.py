@@ -22,6 +22,8 @@ for key, sc, W, H, S, D in [("rtiow1080", scene.rtiow_final_scene(), 1920, 1080,
         print("  phase shares: " + ", ".join(f"{NAMES[i]}={c[i]/tot:.3f}" for i in NAMES))
         it = max(c[4], 1)
         print(f"  wave iterations={c[4]} lanes/iter={c[9]/it:.1f} cand-groups/iter={c[5]/it:.1f} "
-              f"of {(len(sp)+3)//4} drain-max/iter={c[6]/it:.2f} flushes/iter={c[11]/it:.3f} "
+              f"of {(len(sp)+7)//8} drain-max/iter={c[6]/it:.2f} flushes/iter={c[11]/it:.3f} "
               f"wave-cycles total={c[8]} per-iter={c[8]/it:.0f}")
+        print(f"  exact tests per iter: wave-max {c[13]/it:.2f}  wave-max full-path {c[14]/it:.2f}  "
+              f"lane-sum {c[15]/it:.1f} (per lane {c[15]/max(c[9],1):.2f})")
     r.close()
