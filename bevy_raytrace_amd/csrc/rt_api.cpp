@@ -359,6 +359,11 @@ static int enqueue(rt_ctx* ctx, const rt_camera* cam, const rt_params* prm, floa
     K_.div_npix = make_fastdiv(npix ? npix : 1);
     K_.div_width = make_fastdiv(p.width);
     K_.div_row_block = make_fastdiv(B);
+    K_.tile_full_rows = rows / 8;
+    K_.tile_full_cols = p.width / 8;
+    K_.tile_wrem = p.width % 8;
+    K_.div_8w = make_fastdiv(8 * p.width);
+    K_.div_wrem = make_fastdiv(K_.tile_wrem ? K_.tile_wrem : 1);
 
     HIP_TRY(ctx, hipEventRecord(ctx->ev_t0, stream));
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, words_pad * sizeof(uint32_t), stream));
@@ -371,6 +376,8 @@ static int enqueue(rt_ctx* ctx, const rt_camera* cam, const rt_params* prm, floa
         const uint64_t chunks = (items + RT_WAVE_CHUNK - 1) / RT_WAVE_CHUNK;
         const uint64_t need_blocks = (chunks + (RT_BLOCK_THREADS / 64) - 1) / (RT_BLOCK_THREADS / 64);
         const uint32_t grid = (uint32_t)(need_blocks < grid_full ? need_blocks : grid_full);
+        const uint64_t tail_items = 2ull * RT_WAVE_CHUNK * grid * (RT_BLOCK_THREADS / 64);
+        K_.tail_start = (uint32_t)(items > tail_items ? items - tail_items : 0);
         HIP_TRY(ctx, hipEventRecord(ctx->ev[2 * i], stream));
         HIP_TRY(ctx, rt_launch_render(&K_, ctx->d_grp, ctx->d_sph, ctx->d_sph_rm, ctx->d_mats, ctx->d_pd,
                                       ctx->d_block_sums,

@@ -8,6 +8,7 @@
 
 #define RT_BLOCK_THREADS 256  // 4 waves per workgroup
 #define RT_WAVE_CHUNK 64      // work items a wave takes per atomic
+#define RT_WAVE_CHUNK_TAIL 16 // ... in the last 2 x 64 x waves items of the queue
 // Counter block at the start of the ctx's counter buffer (u32 words):
 // [0,4) two u64 segment counters, [4,36) 16 u64 diagnostic counters
 // (RT_PROFILE builds), [36, ...) one u32 work counter per pass.
@@ -40,6 +41,13 @@ struct KParams {
     float T[16];           // camera transform, column-major
     float tan_half, focus_plane, aspect, half_w, half_h;
     FastDiv div_npix, div_width, div_row_block;
+    uint32_t tail_start;   // queue position from which waves take RT_WAVE_CHUNK_TAIL items
+    // processing order of a block's pixels: 8x8 tiles (rows of tiles), then the
+    // rows % 8 leftover rows row-major
+    uint32_t tile_full_rows;  // rows / 8
+    uint32_t tile_full_cols;  // width / 8
+    uint32_t tile_wrem;       // width % 8
+    FastDiv div_8w, div_wrem;
 };
 
 extern "C" {

@@ -358,11 +358,44 @@ __device__ __forceinline__ void pixel_xy(const KParams& P, uint32_t p, uint32_t&
     y = (rb * P.shard_count + P.shard_index) * P.row_block + (r - rb * P.row_block);
 }
 
+// k-th pixel of a block in processing order -> shard-local pixel index
+// (row-major). Order: 8x8 tiles, so the 64 lanes of a wave trace a compact
+// patch of the image (coherent rays: fewer sphere groups with a candidate in
+// the wave); tile rows run bottom-up so the queue ends on the cheap sky rows.
+__device__ __forceinline__ uint32_t order_to_pixel(const KParams& P, uint32_t k) {
+    k = P.npix - 1 - k;
+    const uint32_t W = P.width;
+    const uint32_t tiled = P.tile_full_rows * 8 * W;
+    uint32_t x, r;
+    if (k < tiled) {
+        const uint32_t tr = fdiv(k, P.div_8w);
+        const uint32_t rem = k - tr * 8 * W;
+        const uint32_t tx = rem >> 6;
+        if (tx < P.tile_full_cols) {
+            x = tx * 8 + (rem & 7);
+            r = tr * 8 + ((rem >> 3) & 7);
+        } else {  // the narrow last tile of the tile row
+            const uint32_t j = rem - P.tile_full_cols * 64;
+            const uint32_t jr = fdiv(j, P.div_wrem);
+            x = P.tile_full_cols * 8 + (j - jr * P.tile_wrem);
+            r = tr * 8 + jr;
+        }
+    } else {
+        const uint32_t j = k - tiled;
+        const uint32_t jr = fdiv(j, P.div_width);
+        x = j - jr * W;
+        r = P.tile_full_rows * 8 + jr;
+    }
+    return r * W + x;
+}
+
+// Work item -> (sample block, pixel). block_sums is indexed by (block, pixel)
+// for the collect pass.
 __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint32_t item,
                                            const float4* __restrict__ pd) {
-    st.item = item;
     const uint32_t bl = fdiv(item, P.div_npix);
-    const uint32_t p = item - bl * P.npix;
+    const uint32_t p = order_to_pixel(P, item - bl * P.npix);
+    st.item = bl * P.npix + p;
     pixel_xy(P, p, st.x, st.y);
     const uint32_t b = P.block_begin + bl;
     st.s = b * RT_SAMPLE_BLOCK;
@@ -502,15 +535,18 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
         uint64_t need = __ballot(!has_item);
         while (need != 0 && !exhausted) {
             if (q_next >= q_end) {
+                // big chunks keep the counter cold; small ones near the end of
+                // the queue keep the waves' finishing times together
+                const uint32_t chunk = q_end >= P.tail_start ? RT_WAVE_CHUNK_TAIL : RT_WAVE_CHUNK;
                 uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(work_counter, (uint32_t)RT_WAVE_CHUNK);
+                if (lane == 0) base = atomicAdd(work_counter, chunk);
                 base = __shfl(base, 0);
                 if (base >= total) {
                     exhausted = true;
                     break;
                 }
                 q_next = base;
-                q_end = min(base + (uint32_t)RT_WAVE_CHUNK, total);
+                q_end = min(base + chunk, total);
             }
             const uint32_t avail = q_end - q_next;
             const uint32_t rank = lanemask_lt_count(need);
