@@ -56,7 +56,7 @@ struct rt_ctx {
     size_t bs_cap = 0;
     float4* d_acc = nullptr;
     size_t acc_cap = 0;
-    float4* d_pd = nullptr;         // per-pixel primary directions (rt_primary_kernel)
+    float4* d_pd = nullptr;         // pixel table (rt_primary_kernel), 32 B per pixel
     size_t pd_cap = 0;
     float4* d_out = nullptr;        // host-output path staging
     size_t out_cap = 0;
@@ -295,6 +295,8 @@ static int enqueue(rt_ctx* ctx, const rt_camera* cam, const rt_params* prm, floa
     const uint32_t B = p.row_block ? p.row_block : 1;
     if (p.shard_index >= K)
         return fail(ctx, RT_ERR_INVALID_ARG, "shard_index %u >= shard_count %u", p.shard_index, K);
+    if (p.width > 65535 || p.height > 65535)
+        return fail(ctx, RT_ERR_INVALID_ARG, "width/height %u x %u above 65535", p.width, p.height);
     if ((uint64_t)p.width * p.height > 0xFFFFFFFFull)
         return fail(ctx, RT_ERR_INVALID_ARG, "image of %u x %u pixels exceeds 2^32", p.width, p.height);
     const uint32_t rows = rt_shard_rows(p.height, B, K, p.shard_index);
@@ -317,7 +319,7 @@ static int enqueue(rt_ctx* ctx, const rt_camera* cam, const rt_params* prm, floa
         }
         int rc = ensure(ctx, &ctx->d_block_sums, &ctx->bs_cap, per_block * (size_t)pb);
         if (rc) return rc;
-        rc = ensure(ctx, &ctx->d_pd, &ctx->pd_cap, per_block);
+        rc = ensure(ctx, &ctx->d_pd, &ctx->pd_cap, 2 * per_block);  // 32-B pixel table entries
         if (rc) return rc;
         if (passes.size() > 1) {
             rc = ensure(ctx, &ctx->d_acc, &ctx->acc_cap, per_block);

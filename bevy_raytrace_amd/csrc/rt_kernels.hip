@@ -391,17 +391,27 @@ __device__ __forceinline__ uint32_t order_to_pixel(const KParams& P, uint32_t k)
 
 // Work item -> (sample block, pixel). block_sums is indexed by (block, pixel)
 // for the collect pass.
+// pixel table entry (rt_primary_kernel): k-th pixel of the processing order
+// -> its primary direction and (shard pixel index, x | y << 16).
+struct PixelEntry {
+    float4 d;       // xyz: primary direction, w: unused
+    uint32_t p, xy;
+    uint32_t pad0, pad1;
+};
+
 __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint32_t item,
-                                           const float4* __restrict__ pd) {
+                                           const PixelEntry* __restrict__ tab) {
     const uint32_t bl = fdiv(item, P.div_npix);
-    const uint32_t p = order_to_pixel(P, item - bl * P.npix);
-    st.item = bl * P.npix + p;
-    pixel_xy(P, p, st.x, st.y);
+    const PixelEntry& e = tab[item - bl * P.npix];
+    const uint4 pxy = *reinterpret_cast<const uint4*>(&e.p);
+    const float4 q = e.d;
+    st.item = bl * P.npix + pxy.x;
+    st.x = pxy.y & 0xFFFFu;
+    st.y = pxy.y >> 16;
     const uint32_t b = P.block_begin + bl;
     st.s = b * RT_SAMPLE_BLOCK;
     st.s_end = min(P.spp, st.s + RT_SAMPLE_BLOCK);
     st.bsum = mk(0.0f, 0.0f, 0.0f);
-    const float4 q = pd[p];  // primary direction, rt_primary_kernel
     st.pd = mk(q.x, q.y, q.z);
     start_sample(P, st);
 }
@@ -508,7 +518,7 @@ __device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, f
 __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_render_kernel(
     KParams P, const float4* __restrict__ grp, const float4* __restrict__ sph,
     const float2* __restrict__ sph_rm, const rt_material* __restrict__ mats,
-    const float4* __restrict__ pd, float4* __restrict__ block_sums,
+    const PixelEntry* __restrict__ tab, float4* __restrict__ block_sums,
     uint32_t* __restrict__ work_counter,
     unsigned long long* __restrict__ seg_counter, unsigned long long* __restrict__ dbg) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -552,7 +562,7 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
             const uint32_t rank = lanemask_lt_count(need);
             const uint32_t cnt = (uint32_t)__popcll(need);
             if (!has_item && rank < avail) {
-                start_item(P, st, q_next + rank, pd);
+                start_item(P, st, q_next + rank, tab);
                 has_item = true;
             }
             q_next += min(avail, cnt);
@@ -625,16 +635,24 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
     }
 }
 
-// Primary ray direction of every shard pixel (generate.wgsl:66-126), once per
-// frame: the direction depends on the pixel only (lens offset 0, no jitter).
-__global__ void rt_primary_kernel(KParams P, float4* __restrict__ pd) {
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= P.npix) return;
+// Pixel table, once per frame: for the k-th pixel of the processing order
+// its shard pixel index, global (x, y) and primary ray direction
+// (generate.wgsl:66-126; the direction depends on the pixel only: lens
+// offset 0, no jitter).
+__global__ void rt_primary_kernel(KParams P, PixelEntry* __restrict__ tab) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= P.npix) return;
+    const uint32_t p = order_to_pixel(P, k);
     uint32_t x, y;
     pixel_xy(P, p, x, y);
     v3 o, d;
     primary_ray(P, x, y, o, d);
-    pd[p] = make_float4(d.x, d.y, d.z, 0.0f);
+    PixelEntry e;
+    e.d = make_float4(d.x, d.y, d.z, 0.0f);
+    e.p = p;
+    e.xy = x | (y << 16);
+    e.pad0 = e.pad1 = 0;
+    tab[k] = e;
 }
 
 // Batch closest-hit query (rt_intersect): one ray per lane, same intersect_world.
@@ -709,14 +727,15 @@ hipError_t rt_launch_render(const KParams* P, const float4* grp, const float4* s
                             float4* block_sums, uint32_t* work_counter,
                             unsigned long long* seg_counter, uint32_t grid, hipStream_t stream) {
     hipLaunchKernelGGL(rt_render_kernel, dim3(grid), dim3(RT_BLOCK_THREADS), 0, stream, *P, grp,
-                       sph, sph_rm, mats, pd, block_sums, work_counter, seg_counter,
-                       seg_counter + 2);
+                       sph, sph_rm, mats, reinterpret_cast<const PixelEntry*>(pd), block_sums,
+                       work_counter, seg_counter, seg_counter + 2);
     return hipGetLastError();
 }
 
 hipError_t rt_launch_primary(const KParams* P, float4* pd, hipStream_t stream) {
     const uint32_t T = 256;
-    hipLaunchKernelGGL(rt_primary_kernel, dim3((P->npix + T - 1) / T), dim3(T), 0, stream, *P, pd);
+    hipLaunchKernelGGL(rt_primary_kernel, dim3((P->npix + T - 1) / T), dim3(T), 0, stream, *P,
+                       reinterpret_cast<PixelEntry*>(pd));
     return hipGetLastError();
 }
 

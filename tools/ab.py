@@ -34,9 +34,12 @@ for rep in range(a.reps + 1):
             print(f"{os.path.basename(p)}: identical_to_first={ok}", flush=True)
             continue
         times[p].append(st["kernel_ms"])
+base = np.array(times[a.libs[0]])
 for p in a.libs:
     t = np.array(times[p])
     segs = st["traced_segments"]
     tf = segs * 18 * len(sp) / (np.median(t) * 1e-3) / 1e12
+    ratio = t / base  # same-round ratio vs the first library (round-to-round drift cancels)
     print(f"{os.path.basename(p):40s} median {np.median(t):8.3f} ms  min {t.min():8.3f}  "
-          f"frac {tf/157.3:.3f}", flush=True)
+          f"frac {tf/157.3:.3f}  ratio-vs-first median {np.median(ratio):.4f} "
+          f"[{ratio.min():.4f}, {ratio.max():.4f}]", flush=True)
