@@ -516,7 +516,7 @@ __device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, f
 }
 
 __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_render_kernel(
-    KParams P, const float4* __restrict__ grp, const float4* __restrict__ sph,
+    KParams P, const float4* grp, const float4* __restrict__ sph,
     const float2* __restrict__ sph_rm, const rt_material* __restrict__ mats,
     const PixelEntry* __restrict__ tab, float4* __restrict__ block_sums,
     uint32_t* __restrict__ work_counter,
@@ -529,6 +529,14 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
 #endif
     __shared__ uint32_t s_cq[RT_BLOCK_THREADS * RT_CQ_CAP];  // per-lane candidate queues
     uint32_t* cq = s_cq + (threadIdx.x / 64u) * (64u * RT_CQ_CAP);
+#ifdef RT_SPHERES_LDS
+    // Experiment variant: the filter reads the sphere groups from LDS (staged
+    // once per workgroup) instead of the scalar cache.
+    extern __shared__ float4 s_grp[];
+    for (uint32_t i = threadIdx.x; i < (P.ngroups + 1) * 8; i += RT_BLOCK_THREADS) s_grp[i] = grp[i];
+    __syncthreads();
+    grp = s_grp;
+#endif
     const uint32_t total = P.npix * P.nblocks;
     const bool use_cache = (P.flags & RT_FLAG_NO_PRIMARY_CACHE) == 0;
 
@@ -726,7 +734,12 @@ hipError_t rt_launch_render(const KParams* P, const float4* grp, const float4* s
                             const float2* sph_rm, const rt_material* mats, const float4* pd,
                             float4* block_sums, uint32_t* work_counter,
                             unsigned long long* seg_counter, uint32_t grid, hipStream_t stream) {
-    hipLaunchKernelGGL(rt_render_kernel, dim3(grid), dim3(RT_BLOCK_THREADS), 0, stream, *P, grp,
+#ifdef RT_SPHERES_LDS
+    const size_t dyn = (size_t)(P->ngroups + 1) * 8 * sizeof(float4);
+#else
+    const size_t dyn = 0;
+#endif
+    hipLaunchKernelGGL(rt_render_kernel, dim3(grid), dim3(RT_BLOCK_THREADS), dyn, stream, *P, grp,
                        sph, sph_rm, mats, reinterpret_cast<const PixelEntry*>(pd), block_sums,
                        work_counter, seg_counter, seg_counter + 2);
     return hipGetLastError();
