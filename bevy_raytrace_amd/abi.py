@@ -113,6 +113,8 @@ _PROTOS = {
     "rt_wait": (ctypes.c_int, [_VP, ctypes.POINTER(RtStats)]),
     "rt_assemble_shards": (ctypes.c_int, [_VP, _VP, _U32, _VP, _U32, _U32, _U32, _U32, _VP]),
     "rt_intersect": (ctypes.c_int, [_VP, _VP, _U32, _VP, _VP]),
+    "rt_update_spheres": (ctypes.c_int, [_VP, _U32, _VP, _U32]),
+    "rt_update_materials": (ctypes.c_int, [_VP, _U32, _VP, _U32]),
     "rt_last_error": (ctypes.c_char_p, [_VP]),
 }
 

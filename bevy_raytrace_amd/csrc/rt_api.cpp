@@ -19,6 +19,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -50,6 +51,10 @@ struct rt_ctx {
     float2* d_sph_rm = nullptr;     // (radius, material bits)
     rt_material* d_mats = nullptr;
     size_t grp_cap = 0, sph_cap = 0, sph_rm_cap = 0, mat_cap = 0;
+    std::vector<float4> h_sph, h_grp;  // host mirrors of the packed scene
+    std::vector<float> h_S;
+    std::vector<float2> h_rm;
+    std::vector<rt_material> h_mats;
 
     // work buffers
     float4* d_block_sums = nullptr;
@@ -208,76 +213,147 @@ void rt_destroy(rt_ctx* ctx) {
     delete ctx;
 }
 
+// ---- scene packing --------------------------------------------------------
+// Sphere records for the kernel. AoS (cx, cy, cz, r*r) for the exact tests and
+// shading; SoA groups of RT_GROUP (cx[8], cy[8], cz[8], S[8]) for the
+// wave-uniform filter loop, S = r^2 - (1 - m - mu) |c|^2 rounded once from
+// double (DESIGN.md "Exact filter"). Padded to whole groups plus one; pad
+// records have r^2 = S = -inf, which the filter never passes. Host mirrors
+// are kept so rt_update_* re-packs and uploads only the touched groups.
+static void pack_record(rt_ctx* ctx, uint32_t i, const rt_sphere& s) {
+    const float r = s.radius;
+    const float r2 = r * r;  // sqr(s.radius): the f32 value the exact test uses
+    ctx->h_sph[i] = make_float4(s.center[0], s.center[1], s.center[2], r2);
+    const double kS = 1.0 - 0x1p-16 - 0x1p-17;
+    const double cx = s.center[0], cy = s.center[1], cz = s.center[2];
+    ctx->h_S[i] = (float)((double)r2 - kS * (cx * cx + cy * cy + cz * cz));
+    float mbits;
+    std::memcpy(&mbits, &s.material, 4);
+    ctx->h_rm[i] = make_float2(r, mbits);
+}
+
+static void pack_group(rt_ctx* ctx, size_t g) {
+    const float4* q = &ctx->h_sph[RT_GROUP * g];
+    const float* sg = &ctx->h_S[RT_GROUP * g];
+    float4* o = &ctx->h_grp[RT_GROUP * g];
+    o[0] = make_float4(q[0].x, q[1].x, q[2].x, q[3].x);
+    o[1] = make_float4(q[4].x, q[5].x, q[6].x, q[7].x);
+    o[2] = make_float4(q[0].y, q[1].y, q[2].y, q[3].y);
+    o[3] = make_float4(q[4].y, q[5].y, q[6].y, q[7].y);
+    o[4] = make_float4(q[0].z, q[1].z, q[2].z, q[3].z);
+    o[5] = make_float4(q[4].z, q[5].z, q[6].z, q[7].z);
+    o[6] = make_float4(sg[0], sg[1], sg[2], sg[3]);
+    o[7] = make_float4(sg[4], sg[5], sg[6], sg[7]);
+}
+
+static int check_materials(rt_ctx* ctx, const rt_material* mats, uint32_t first, uint32_t count) {
+    for (uint32_t j = 0; j < count; ++j) {
+        const int r = mats[j].reflectance;
+        if (r < RT_LAMBERTIAN || r > RT_DIELECTRIC)
+            return fail(ctx, RT_ERR_BAD_SCENE, "material %u: reflectance %d not in {0,1,2}",
+                        first + j, r);
+    }
+    return RT_OK;
+}
+
+static int check_spheres(rt_ctx* ctx, const rt_sphere* sp, uint32_t first, uint32_t count,
+                         uint32_t m) {
+    for (uint32_t i = 0; i < count; ++i)
+        if (sp[i].material >= m)
+            return fail(ctx, RT_ERR_BAD_SCENE, "sphere %u: material %u >= material count %u",
+                        first + i, sp[i].material, m);
+    return RT_OK;
+}
+
+static int quiesce(rt_ctx* ctx) {  // no kernel may be reading the scene while it changes
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->pending && ctx->pending_stream) HIP_TRY(ctx, hipStreamSynchronize(ctx->pending_stream));
+    return RT_OK;
+}
+
 int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n, const rt_material* materials,
                  uint32_t m) {
     if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_set_scene: ctx is NULL");
     if (n && !spheres) return fail(ctx, RT_ERR_INVALID_ARG, "rt_set_scene: spheres is NULL, n=%u", n);
     if (m && !materials)
         return fail(ctx, RT_ERR_INVALID_ARG, "rt_set_scene: materials is NULL, m=%u", m);
-    for (uint32_t j = 0; j < m; ++j) {
-        const int r = materials[j].reflectance;
-        if (r < RT_LAMBERTIAN || r > RT_DIELECTRIC)
-            return fail(ctx, RT_ERR_BAD_SCENE, "material %u: reflectance %d not in {0,1,2}", j, r);
-    }
-    // Sphere records for the kernel. AoS (cx, cy, cz, r*r) for the exact tests
-    // and shading; SoA groups of RT_GROUP (cx[8], cy[8], cz[8], S[8]) for the
-    // wave-uniform filter loop, S = r^2 - (1 - m - mu) |c|^2 rounded once from
-    // double (DESIGN.md "Exact filter"). Padded to whole groups; pad records
-    // have r^2 = S = -inf, which the filter never passes.
+    int rc = check_materials(ctx, materials, 0, m);
+    if (rc) return rc;
+    rc = check_spheres(ctx, spheres, 0, n, m);
+    if (rc) return rc;
     const uint32_t ngroups = (n + RT_GROUP - 1) / RT_GROUP;
     const size_t nrec = (size_t)(ngroups + 1) * RT_GROUP;
-    std::vector<float4> sph(nrec, make_float4(0.0f, 0.0f, 0.0f, -INFINITY));
-    std::vector<float> S(nrec, -INFINITY);
-    std::vector<float2> rm(n ? n : 1, make_float2(0.0f, 0.0f));
-    const double kS = 1.0 - 0x1p-16 - 0x1p-17;
-    for (uint32_t i = 0; i < n; ++i) {
-        const rt_sphere& s = spheres[i];
-        if (s.material >= m)
-            return fail(ctx, RT_ERR_BAD_SCENE, "sphere %u: material %u >= material count %u", i,
-                        s.material, m);
-        const float r = s.radius;
-        const float r2 = r * r;  // sqr(s.radius): the f32 value the exact test uses
-        sph[i] = make_float4(s.center[0], s.center[1], s.center[2], r2);
-        const double cx = s.center[0], cy = s.center[1], cz = s.center[2];
-        S[i] = (float)((double)r2 - kS * (cx * cx + cy * cy + cz * cz));
-        float mbits;
-        std::memcpy(&mbits, &s.material, 4);
-        rm[i] = make_float2(r, mbits);
-    }
-    std::vector<float4> grp(nrec);  // SoA regroup of the padded records
-    for (size_t g = 0; g < nrec / RT_GROUP; ++g) {
-        const float4* q = &sph[RT_GROUP * g];
-        const float* sg = &S[RT_GROUP * g];
-        float4* o = &grp[RT_GROUP * g];
-        o[0] = make_float4(q[0].x, q[1].x, q[2].x, q[3].x);
-        o[1] = make_float4(q[4].x, q[5].x, q[6].x, q[7].x);
-        o[2] = make_float4(q[0].y, q[1].y, q[2].y, q[3].y);
-        o[3] = make_float4(q[4].y, q[5].y, q[6].y, q[7].y);
-        o[4] = make_float4(q[0].z, q[1].z, q[2].z, q[3].z);
-        o[5] = make_float4(q[4].z, q[5].z, q[6].z, q[7].z);
-        o[6] = make_float4(sg[0], sg[1], sg[2], sg[3]);
-        o[7] = make_float4(sg[4], sg[5], sg[6], sg[7]);
-    }
-    HIP_TRY(ctx, hipSetDevice(ctx->device));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    if (ctx->pending && ctx->pending_stream) HIP_TRY(ctx, hipStreamSynchronize(ctx->pending_stream));
-    int rc = ensure(ctx, &ctx->d_sph, &ctx->sph_cap, sizeof(float4) * nrec);
+    ctx->h_sph.assign(nrec, make_float4(0.0f, 0.0f, 0.0f, -INFINITY));
+    ctx->h_S.assign(nrec, -INFINITY);
+    ctx->h_rm.assign(n ? n : 1, make_float2(0.0f, 0.0f));
+    ctx->h_grp.assign(nrec, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    for (uint32_t i = 0; i < n; ++i) pack_record(ctx, i, spheres[i]);
+    for (size_t g = 0; g < nrec / RT_GROUP; ++g) pack_group(ctx, g);
+    ctx->h_mats.assign(materials, materials + m);
+    rc = quiesce(ctx);
+    if (rc) return rc;
+    rc = ensure(ctx, &ctx->d_sph, &ctx->sph_cap, sizeof(float4) * nrec);
     if (rc) return rc;
     rc = ensure(ctx, &ctx->d_grp, &ctx->grp_cap, sizeof(float4) * nrec);
     if (rc) return rc;
-    rc = ensure(ctx, &ctx->d_sph_rm, &ctx->sph_rm_cap, sizeof(float2) * rm.size());
+    rc = ensure(ctx, &ctx->d_sph_rm, &ctx->sph_rm_cap, sizeof(float2) * ctx->h_rm.size());
     if (rc) return rc;
     rc = ensure(ctx, &ctx->d_mats, &ctx->mat_cap, sizeof(rt_material) * (size_t)m);
     if (rc) return rc;
-    HIP_TRY(ctx, hipMemcpy(ctx->d_sph, sph.data(), sizeof(float4) * nrec, hipMemcpyHostToDevice));
-    HIP_TRY(ctx, hipMemcpy(ctx->d_grp, grp.data(), sizeof(float4) * nrec, hipMemcpyHostToDevice));
-    HIP_TRY(ctx, hipMemcpy(ctx->d_sph_rm, rm.data(), sizeof(float2) * rm.size(), hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(ctx->d_sph, ctx->h_sph.data(), sizeof(float4) * nrec, hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(ctx->d_grp, ctx->h_grp.data(), sizeof(float4) * nrec, hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(ctx->d_sph_rm, ctx->h_rm.data(), sizeof(float2) * ctx->h_rm.size(),
+                           hipMemcpyHostToDevice));
     if (m)
         HIP_TRY(ctx, hipMemcpy(ctx->d_mats, materials, sizeof(rt_material) * m, hipMemcpyHostToDevice));
     ctx->n = n;
     ctx->ngroups = ngroups;
     ctx->m = m;
     ctx->has_scene = true;
+    return RT_OK;
+}
+
+int rt_update_spheres(rt_ctx* ctx, uint32_t first, const rt_sphere* spheres, uint32_t count) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_update_spheres: ctx is NULL");
+    if (!ctx->has_scene) return fail(ctx, RT_ERR_NO_SCENE, "rt_update_spheres before rt_set_scene");
+    if (count == 0) return RT_OK;
+    if (!spheres) return fail(ctx, RT_ERR_INVALID_ARG, "rt_update_spheres: spheres is NULL");
+    if ((uint64_t)first + count > ctx->n)
+        return fail(ctx, RT_ERR_INVALID_ARG, "rt_update_spheres: [%u, %u) outside the %u spheres",
+                    first, first + count, ctx->n);
+    int rc = check_spheres(ctx, spheres, first, count, ctx->m);
+    if (rc) return rc;
+    for (uint32_t i = 0; i < count; ++i) pack_record(ctx, first + i, spheres[i]);
+    const size_t g0 = first / RT_GROUP, g1 = (first + count - 1) / RT_GROUP + 1;
+    for (size_t g = g0; g < g1; ++g) pack_group(ctx, g);
+    rc = quiesce(ctx);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpy(ctx->d_sph + first, &ctx->h_sph[first], sizeof(float4) * count,
+                           hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(ctx->d_sph_rm + first, &ctx->h_rm[first], sizeof(float2) * count,
+                           hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(ctx->d_grp + RT_GROUP * g0, &ctx->h_grp[RT_GROUP * g0],
+                           sizeof(float4) * RT_GROUP * (g1 - g0), hipMemcpyHostToDevice));
+    return RT_OK;
+}
+
+int rt_update_materials(rt_ctx* ctx, uint32_t first, const rt_material* materials,
+                        uint32_t count) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_update_materials: ctx is NULL");
+    if (!ctx->has_scene) return fail(ctx, RT_ERR_NO_SCENE, "rt_update_materials before rt_set_scene");
+    if (count == 0) return RT_OK;
+    if (!materials) return fail(ctx, RT_ERR_INVALID_ARG, "rt_update_materials: materials is NULL");
+    if ((uint64_t)first + count > ctx->m)
+        return fail(ctx, RT_ERR_INVALID_ARG, "rt_update_materials: [%u, %u) outside the %u materials",
+                    first, first + count, ctx->m);
+    int rc = check_materials(ctx, materials, first, count);
+    if (rc) return rc;
+    std::copy(materials, materials + count, ctx->h_mats.begin() + first);
+    rc = quiesce(ctx);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpy(ctx->d_mats + first, materials, sizeof(rt_material) * count,
+                           hipMemcpyHostToDevice));
     return RT_OK;
 }
 

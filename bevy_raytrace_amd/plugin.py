@@ -73,19 +73,31 @@ class RayTraceNode:
 
     def __init__(self):
         self.renderer = None
-        self._scene_key = None
+        self._sp = None
+        self._mt = None
         self.last_stats = None
+        self.uploads = {"full": 0, "spheres": 0, "materials": 0}
 
     def update(self, world: World):
+        """Extract + prepare (sphere.rs:166-197): upload only what changed."""
         settings = world.resource(RayTraceSettings)
         if self.renderer is None:
             self.renderer = Renderer(settings.device)
         sc = world.resource(Scene)
         sp, mt = sc.objects_gpu(), sc.materials_gpu()
-        key = (sp.tobytes(), mt.tobytes())
-        if key != self._scene_key:
+        if self._sp is None or len(sp) != len(self._sp) or len(mt) != len(self._mt):
             self.renderer.set_scene(sp, mt)
-            self._scene_key = key
+            self.uploads["full"] += 1
+        else:
+            for new, old, up, key in ((mt, self._mt, self.renderer.update_materials, "materials"),
+                                      (sp, self._sp, self.renderer.update_spheres, "spheres")):
+                dirty = np.nonzero(new.view(np.uint8).reshape(len(new), -1)
+                                   != old.view(np.uint8).reshape(len(old), -1))[0]
+                if dirty.size:
+                    i0, i1 = int(dirty.min()), int(dirty.max()) + 1
+                    up(i0, new[i0:i1])
+                    self.uploads[key] += 1
+        self._sp, self._mt = sp, mt
 
     def run(self, world: World):
         settings = world.resource(RayTraceSettings)

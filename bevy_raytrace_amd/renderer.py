@@ -53,6 +53,18 @@ class Renderer:
         check(self.lib, self.ctx, rc)
         self.n_spheres = int(sp.size)
 
+    def update_spheres(self, first: int, spheres: np.ndarray):
+        sp = np.ascontiguousarray(spheres, dtype=abi.SPHERE_DTYPE)
+        rc = self.lib.rt_update_spheres(self.ctx, int(first), sp.ctypes.data_as(ctypes.c_void_p),
+                                        sp.size)
+        check(self.lib, self.ctx, rc)
+
+    def update_materials(self, first: int, materials: np.ndarray):
+        mt = np.ascontiguousarray(materials, dtype=abi.MATERIAL_DTYPE)
+        rc = self.lib.rt_update_materials(self.ctx, int(first), mt.ctypes.data_as(ctypes.c_void_p),
+                                          mt.size)
+        check(self.lib, self.ctx, rc)
+
     # --------------------------------------------------------------- render
     def render(self, camera: np.ndarray, width, height, spp, max_depth, frame0=0, row_block=8,
                shard_count=1, shard_index=0, flags=0):

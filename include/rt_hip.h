@@ -159,6 +159,15 @@ void rt_destroy(rt_ctx* ctx);
 int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n,
                  const rt_material* materials, uint32_t m);
 
+/* Incremental scene edits (SURVEY §8f "persistent scene + dirty tracking";
+ * the reference re-uploads the whole list every frame, sphere.rs:180-197, and
+ * the materials when their count changes, ray_trace_materials.rs:129-164).
+ * Replace records [first, first+count) of the current scene; counts N and M
+ * are unchanged. Only the touched sphere groups are re-packed and uploaded. */
+int rt_update_spheres(rt_ctx* ctx, uint32_t first, const rt_sphere* spheres, uint32_t count);
+int rt_update_materials(rt_ctx* ctx, uint32_t first, const rt_material* materials,
+                        uint32_t count);
+
 /* Render one frame (replaces RayTraceNode::run, src/ray_trace_node.rs:195-224).
  * Synchronous. out_rgba: caller-owned HOST buffer of
  * rt_shard_rows(...) * width * 4 floats (Rgba32Float, row-major, alpha 1,

@@ -222,3 +222,66 @@ def test_plugin_frames_match_oracle():
         check_exact(img, ref)
         assert node.last_stats["segments"] == segs
     assert world.resource(FrameCounter).frame == 3
+
+
+def test_update_spheres_and_materials(renderer):
+    """rt_update_spheres / rt_update_materials == a full rt_set_scene of the edited scene."""
+    sc = scene.rtiow_final_scene()
+    sp, mt = arrays(sc)
+    renderer.set_scene(sp, mt)
+    sp2, mt2 = sp.copy(), mt.copy()
+    sp2["center"][10:27] += np.float32(0.3)          # spans three 8-sphere groups
+    sp2["radius"][12] = np.float32(0.35)
+    sp2["material"][20] = 2                           # now the glass centre sphere's material
+    sp2["center"][-1] = (3.5, 1.2, -0.4)              # last group (padding neighbours)
+    mt2[5]["color"] = (0.9, 0.1, 0.1, 1.0)
+    mt2[7]["reflectance"] = 1
+    mt2[7]["fuzziness"] = np.float32(0.25)
+    renderer.update_spheres(10, sp2[10:27])
+    renderer.update_spheres(len(sp) - 1, sp2[-1:])
+    renderer.update_materials(5, mt2[5:8])
+    cam = default_camera_block()
+    img, st = renderer.render(cam, 128, 72, 4, 8)
+    ref, segs = O.render(cam, sp2, mt2, 128, 72, 4, 8)
+    check_exact(img, ref)
+    assert st["segments"] == segs
+    rays = np.array([[13, 2, 3, -1, -0.15, -0.2]], np.float32)
+    gi, gt = renderer.intersect(rays)
+    ci, ct = O.intersect_batch(sp2, rays)
+    assert gi[0] == ci[0] and gt[0] == ct[0]
+
+
+def test_update_errors(renderer):
+    sp, mt = arrays(scene.config1_scene())
+    renderer.set_scene(sp, mt)
+    with pytest.raises(abi.RayTraceError) as e:
+        renderer.update_spheres(3, sp[:2])            # runs past the 4 spheres
+    assert e.value.status == abi.RT_ERR_INVALID_ARG
+    bad = sp[:1].copy()
+    bad["material"] = 9
+    with pytest.raises(abi.RayTraceError) as e:
+        renderer.update_spheres(0, bad)
+    assert e.value.status == abi.RT_ERR_BAD_SCENE
+    badm = mt[:1].copy()
+    badm["reflectance"] = 3
+    with pytest.raises(abi.RayTraceError) as e:
+        renderer.update_materials(0, badm)
+    assert e.value.status == abi.RT_ERR_BAD_SCENE
+
+
+def test_plugin_dirty_tracking_animates():
+    """Moving one sphere per frame re-uploads that sphere only; frames stay exact."""
+    from bevy_raytrace_amd.camera import RayTraceCamera
+    from bevy_raytrace_amd.plugin import RayTraceOutputImage, RayTracePlugin, RayTraceSettings, World
+    world = World()
+    world.insert_resource(RayTraceCamera(96, 54))
+    sc = scene.reference_scene()
+    world.insert_resource(sc)
+    node = RayTracePlugin(RayTraceSettings(samples_per_ray=2, max_depth=4)).build(world)
+    for f in range(3):
+        sc.spheres[-2].center = (-4.0, 1.0 + 0.25 * f, 0.0)
+        RayTracePlugin.frame(world, node)
+        sp, mt = arrays(sc)
+        ref, segs = O.render(RayTraceCamera(96, 54).to_gpu(), sp, mt, 96, 54, 2, 4, frame0=2 * f)
+        check_exact(world.resource(RayTraceOutputImage).data, ref)
+    assert node.uploads == {"full": 1, "spheres": 2, "materials": 0}
