@@ -114,6 +114,9 @@ _PROTOS = {
     "rt_assemble_shards": (ctypes.c_int, [_VP, _VP, _U32, _VP, _U32, _U32, _U32, _U32, _VP]),
     "rt_intersect": (ctypes.c_int, [_VP, _VP, _U32, _VP, _VP]),
     "rt_update_spheres": (ctypes.c_int, [_VP, _U32, _VP, _U32]),
+    "rt_render_progressive": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(RtParams), ctypes.c_int, _VP,
+                                             ctypes.POINTER(ctypes.c_uint64)]),
+    "rt_encode_srgb8": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint64, _VP]),
     "rt_update_materials": (ctypes.c_int, [_VP, _U32, _VP, _U32]),
     "rt_last_error": (ctypes.c_char_p, [_VP]),
 }

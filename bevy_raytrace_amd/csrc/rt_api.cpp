@@ -63,6 +63,10 @@ struct rt_ctx {
     size_t acc_cap = 0;
     float4* d_pd = nullptr;         // pixel table (rt_primary_kernel), 32 B per pixel
     size_t pd_cap = 0;
+    float4* d_prog = nullptr;       // progressive running sum (rt_render_progressive)
+    size_t prog_cap = 0;
+    uint64_t prog_total = 0;        // samples accumulated so far
+    uint64_t prog_key = 0;          // geometry the running sum belongs to
     float4* d_out = nullptr;        // host-output path staging
     size_t out_cap = 0;
     uint32_t* d_counters = nullptr; // [0..3] 2 x u64 segment counters, [4..] per-pass work counters
@@ -204,6 +208,7 @@ void rt_destroy(rt_ctx* ctx) {
     hipFree(ctx->d_acc);
     hipFree(ctx->d_out);
     hipFree(ctx->d_pd);
+    hipFree(ctx->d_prog);
     hipFree(ctx->d_counters);
     if (ctx->h_segs) hipHostFree(ctx->h_segs);
     for (hipEvent_t e : ctx->ev) hipEventDestroy(e);
@@ -359,7 +364,8 @@ int rt_update_materials(rt_ctx* ctx, uint32_t first, const rt_material* material
 
 // Validate and enqueue a whole frame on `stream`, writing float4 pixels to d_out.
 static int enqueue(rt_ctx* ctx, const rt_camera* cam, const rt_params* prm, float4* d_out,
-                   hipStream_t stream, uint32_t* out_passes, uint64_t* out_paths) {
+                   hipStream_t stream, uint32_t* out_passes, uint64_t* out_paths,
+                   int prog_mode = 0, float prog_total = 0.0f) {
     if (!cam || !prm) return fail(ctx, RT_ERR_INVALID_ARG, "camera or params is NULL");
     if (!ctx->has_scene) return fail(ctx, RT_ERR_NO_SCENE, "rt_render before rt_set_scene");
     if (ctx->pending) return fail(ctx, RT_ERR_INVALID_ARG, "a previous async call was not waited for");
@@ -464,7 +470,8 @@ static int enqueue(rt_ctx* ctx, const rt_camera* cam, const rt_params* prm, floa
                                       grid, stream));
         HIP_TRY(ctx, hipEventRecord(ctx->ev[2 * i + 1], stream));
         HIP_TRY(ctx, rt_launch_collect(ctx->d_block_sums, npix, K_.nblocks, ctx->d_acc, i == 0,
-                                       i + 1 == passes.size(), (float)p.spp, d_out, stream));
+                                       i + 1 == passes.size(), (float)p.spp, d_out, ctx->d_prog,
+                                       prog_mode, prog_total, stream));
     }
     HIP_TRY(ctx, hipMemcpyAsync(ctx->h_segs, ctx->d_counters, 18 * sizeof(unsigned long long),
                                 hipMemcpyDeviceToHost, stream));
@@ -553,6 +560,55 @@ int rt_render(rt_ctx* ctx, const rt_camera* camera, const rt_params* params, flo
     int rc = rt_render_async(ctx, camera, params, out_rgba);
     if (rc) return rc;
     return rt_wait(ctx, stats);
+}
+
+int rt_render_progressive(rt_ctx* ctx, const rt_camera* camera, const rt_params* params,
+                          int reset, float* out_rgba, uint64_t* total_spp) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_render_progressive: ctx is NULL");
+    if (!out_rgba || !params)
+        return fail(ctx, RT_ERR_INVALID_ARG, "rt_render_progressive: NULL argument");
+    if (ctx->pending) return fail(ctx, RT_ERR_INVALID_ARG, "a previous async call was not waited for");
+    const uint32_t K = params->shard_count ? params->shard_count : 1;
+    const uint32_t B = params->row_block ? params->row_block : 1;
+    const uint32_t rows = rt_shard_rows(params->height, B, K, params->shard_index);
+    const size_t npix = (size_t)rows * params->width;
+    const size_t bytes = npix * sizeof(float4);
+    // the running sum belongs to one image geometry; another one restarts it
+    const uint64_t key = ((uint64_t)params->width << 40) ^ ((uint64_t)params->height << 20) ^
+                         ((uint64_t)B << 10) ^ ((uint64_t)K << 5) ^ params->shard_index;
+    if (key != ctx->prog_key || !ctx->d_prog) reset = 1;
+    int rc = ensure(ctx, &ctx->d_prog, &ctx->prog_cap, bytes ? bytes : 16);
+    if (rc) return rc;
+    rc = ensure(ctx, &ctx->d_out, &ctx->out_cap, bytes ? bytes : 16);
+    if (rc) return rc;
+    const uint64_t total = (reset ? 0 : ctx->prog_total) + params->spp;
+    uint32_t passes = 0;
+    uint64_t paths = 0;
+    rc = enqueue(ctx, camera, params, ctx->d_out, ctx->stream, &passes, &paths, reset ? 1 : 2,
+                 (float)total);
+    if (rc) return rc;
+    if (bytes)
+        HIP_TRY(ctx, hipMemcpyAsync(out_rgba, ctx->d_out, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipEventRecord(ctx->ev_t1, ctx->stream));
+    HIP_TRY(ctx, hipEventSynchronize(ctx->ev_t1));
+    ctx->prog_total = total;
+    ctx->prog_key = key;
+    if (total_spp) *total_spp = total;
+    return RT_OK;
+}
+
+int rt_encode_srgb8(rt_ctx* ctx, const float* rgba_device, uint8_t* rgba8_device, uint64_t npix,
+                    void* stream) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_encode_srgb8: ctx is NULL");
+    if (npix == 0) return RT_OK;
+    if (!rgba_device || !rgba8_device)
+        return fail(ctx, RT_ERR_INVALID_ARG, "rt_encode_srgb8: NULL buffer");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    HIP_TRY(ctx, rt_launch_srgb8(reinterpret_cast<const float4*>(rgba_device),
+                                 reinterpret_cast<uchar4*>(rgba8_device), npix, s));
+    if (!stream) HIP_TRY(ctx, hipStreamSynchronize(s));
+    return RT_OK;
 }
 
 int rt_assemble_shards(rt_ctx* ctx, const float* gathered_device, uint32_t max_rows,

@@ -58,7 +58,8 @@ hipError_t rt_launch_render(const KParams* P, const float4* grp, const float4* s
                             hipStream_t stream);
 hipError_t rt_launch_collect(const float4* block_sums, uint32_t npix, uint32_t nblocks,
                              float4* acc, int first_pass, int last_pass, float spp, float4* out,
-                             hipStream_t stream);
+                             float4* prog, int prog_mode, float prog_total, hipStream_t stream);
+hipError_t rt_launch_srgb8(const float4* in, uchar4* out, uint64_t npix, hipStream_t stream);
 hipError_t rt_launch_assemble(const float4* gathered, uint32_t max_rows, float4* image,
                               uint32_t width, uint32_t height, uint32_t row_block,
                               uint32_t shard_count, hipStream_t stream);

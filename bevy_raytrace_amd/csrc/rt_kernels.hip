@@ -689,9 +689,13 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_kernel(
 
 // Fold this pass's block sums into acc (block order) and, on the last pass,
 // write out = acc / spp with alpha 1 (collect.wgsl:115-125).
+// Progressive mode (rt_render_progressive): on the last pass the frame's sum
+// is folded into the running sum, prog = prog + sum (prog_mode 2) or
+// prog = sum (1, reset), and out = prog / total_spp.
 __global__ void rt_collect_kernel(const float4* __restrict__ block_sums, uint32_t npix,
                                   uint32_t nblocks, float4* __restrict__ acc, int first_pass,
-                                  int last_pass, float spp, float4* __restrict__ out) {
+                                  int last_pass, float spp, float4* __restrict__ out,
+                                  float4* __restrict__ prog, int prog_mode, float prog_total) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npix) return;
     float ax, ay, az;
@@ -708,10 +712,36 @@ __global__ void rt_collect_kernel(const float4* __restrict__ block_sums, uint32_
         const float4 v = block_sums[(size_t)b * npix + p];
         ax = ax + v.x; ay = ay + v.y; az = az + v.z;
     }
-    if (last_pass)
-        out[p] = make_float4(ax / spp, ay / spp, az / spp, 1.0f);
-    else
+    if (!last_pass) {
         acc[p] = make_float4(ax, ay, az, 0.0f);
+    } else if (prog_mode == 0) {
+        out[p] = make_float4(ax / spp, ay / spp, az / spp, 1.0f);
+    } else {
+        if (prog_mode == 2) {
+            const float4 v = prog[p];
+            ax = v.x + ax; ay = v.y + ay; az = v.z + az;
+        }
+        prog[p] = make_float4(ax, ay, az, 0.0f);
+        out[p] = make_float4(ax / prog_total, ay / prog_total, az / prog_total, 1.0f);
+    }
+}
+
+// Display encode: linear RGBA32F -> sRGB RGBA8 (IEC 61966-2-1 transfer curve),
+// channels clamped to [0, 1] (NaN -> 0), alpha 255. The reference shows the
+// linear texture through Bevy's sprite pass (ray_trace_output.rs:62-77).
+__global__ void rt_srgb8_kernel(const float4* __restrict__ in, uchar4* __restrict__ out,
+                                uint64_t npix) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npix) return;
+    const float4 v = in[i];
+    const float c[3] = {v.x, v.y, v.z};
+    unsigned char q[3];
+    for (int k = 0; k < 3; ++k) {
+        float x = c[k] > 0.0f ? fminf(c[k], 1.0f) : 0.0f;  // NaN -> 0
+        x = x <= 0.0031308f ? 12.92f * x : 1.055f * powf(x, 1.0f / 2.4f) - 0.055f;
+        q[k] = (unsigned char)fminf(fmaxf(rintf(x * 255.0f), 0.0f), 255.0f);
+    }
+    out[i] = make_uchar4(q[0], q[1], q[2], 255);
 }
 
 // gathered: shard_count slabs of max_rows*W float4; image: H*W float4.
@@ -754,10 +784,18 @@ hipError_t rt_launch_primary(const KParams* P, float4* pd, hipStream_t stream) {
 
 hipError_t rt_launch_collect(const float4* block_sums, uint32_t npix, uint32_t nblocks,
                              float4* acc, int first_pass, int last_pass, float spp, float4* out,
-                             hipStream_t stream) {
+                             float4* prog, int prog_mode, float prog_total, hipStream_t stream) {
     const uint32_t T = 256;
     hipLaunchKernelGGL(rt_collect_kernel, dim3((npix + T - 1) / T), dim3(T), 0, stream,
-                       block_sums, npix, nblocks, acc, first_pass, last_pass, spp, out);
+                       block_sums, npix, nblocks, acc, first_pass, last_pass, spp, out, prog,
+                       prog_mode, prog_total);
+    return hipGetLastError();
+}
+
+hipError_t rt_launch_srgb8(const float4* in, uchar4* out, uint64_t npix, hipStream_t stream) {
+    const uint32_t T = 256;
+    hipLaunchKernelGGL(rt_srgb8_kernel, dim3((uint32_t)((npix + T - 1) / T)), dim3(T), 0, stream,
+                       in, out, npix);
     return hipGetLastError();
 }
 

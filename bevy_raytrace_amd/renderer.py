@@ -80,6 +80,29 @@ class Renderer:
         check(self.lib, self.ctx, rc)
         return out, st.as_dict()
 
+    def render_progressive(self, camera: np.ndarray, width, height, spp, max_depth, frame0=0,
+                           reset=False, row_block=8, shard_count=1, shard_index=0, flags=0):
+        """Render spp more samples into the device running sum; returns the
+        running mean image (rows, W, 4) and the total samples so far."""
+        cam = np.ascontiguousarray(camera, dtype=abi.CAMERA_DTYPE)
+        p = make_params(width, height, spp, max_depth, frame0, row_block, shard_count, shard_index,
+                        flags)
+        rows = self.lib.rt_shard_rows(p.height, p.row_block, max(1, p.shard_count), p.shard_index)
+        out = np.empty((rows, int(width), 4), dtype=np.float32)
+        total = ctypes.c_uint64(0)
+        rc = self.lib.rt_render_progressive(self.ctx, cam.ctypes.data_as(ctypes.c_void_p),
+                                            ctypes.byref(p), 1 if reset else 0,
+                                            out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(total))
+        check(self.lib, self.ctx, rc)
+        return out, int(total.value)
+
+    def encode_srgb8(self, rgba_ptr: int, out_ptr: int, npix: int, stream=None):
+        """Device Rgba32Float -> device sRGB RGBA8."""
+        rc = self.lib.rt_encode_srgb8(self.ctx, ctypes.c_void_p(int(rgba_ptr)),
+                                      ctypes.c_void_p(int(out_ptr)), int(npix),
+                                      ctypes.c_void_p(int(stream)) if stream else None)
+        check(self.lib, self.ctx, rc)
+
     def render_device(self, camera: np.ndarray, out_ptr: int, width, height, spp, max_depth,
                       frame0=0, row_block=8, shard_count=1, shard_index=0, flags=0, stream=None):
         """Enqueue a render into a device buffer (e.g. a torch tensor's data_ptr()).

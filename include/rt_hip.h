@@ -194,6 +194,23 @@ int rt_wait(rt_ctx* ctx, rt_stats* stats);
  * Synchronous. Used for picking and for the intersection parity tests. */
 int rt_intersect(rt_ctx* ctx, const float* rays, uint32_t n, int32_t* hit_index, float* hit_t);
 
+/* Progressive accumulation: the reference shows independent
+ * 1-spp frames (collect.wgsl:115-125, no history). Here a running per-pixel sum
+ * stays on the device across calls: each call renders params->spp new samples
+ * (frames frame0 .. frame0+spp-1; callers advance frame0 by spp per call),
+ * folds the call's sum into the running sum (sum_new = sum_old + call_sum, f32)
+ * and writes out_rgba (HOST) = running sum / total samples. reset != 0 (or a
+ * different image geometry) restarts the sum. Synchronous. *total_spp (may be
+ * NULL) receives the samples accumulated so far. */
+int rt_render_progressive(rt_ctx* ctx, const rt_camera* camera, const rt_params* params,
+                          int reset, float* out_rgba, uint64_t* total_spp);
+
+/* Display encode of an Rgba32Float image: sRGB transfer curve (IEC 61966-2-1),
+ * channels clamped to [0,1], NaN -> 0, alpha 255, RGBA8. DEVICE buffers,
+ * enqueued on `stream` (NULL = ctx stream, synchronous). */
+int rt_encode_srgb8(rt_ctx* ctx, const float* rgba_device, uint8_t* rgba8_device, uint64_t npix,
+                    void* stream);
+
 /* Re-assemble gathered shard outputs into the full image on the device:
  * gathered = shard_count consecutive slabs of max_rows*width*4 floats (slab k =
  * shard k's output, padded to max_rows rows); image = height*width*4 floats. */

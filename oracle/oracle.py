@@ -107,23 +107,29 @@ def trace_path(cam, spheres, materials, width, height, x, y, frame, max_depth):
     return np.array(out[:], np.float32), segs.value
 
 
-def _params(width, height, spp, max_depth, frame0, row_block, shard_count, shard_index):
+RAW_SUMS = 0x80000000
+
+
+def _params(width, height, spp, max_depth, frame0, row_block, shard_count, shard_index, flags=0):
     p = _Params()
     p.width, p.height, p.spp, p.max_depth = width, height, spp, max_depth
     p.frame0, p.row_block, p.shard_count, p.shard_index = frame0, row_block, shard_count, shard_index
+    p.flags = flags
     return p
 
 
 def render(cam, spheres, materials, width, height, spp, max_depth, frame0=0, row_block=8,
-           shard_count=1, shard_index=0, nthreads=None):
-    """Render the shard's rows -> (rows, W, 4) float32, segments."""
+           shard_count=1, shard_index=0, nthreads=None, raw_sums=False):
+    """Render the shard's rows -> (rows, W, 4) float32, segments.
+    raw_sums: the block-folded sample sums instead of sum / spp (alpha 0)."""
     cam = np.ascontiguousarray(cam)
     nthreads = nthreads or os.cpu_count() or 1
     B = max(1, row_block)
     nrows = sum(1 for y in range(height) if (y // B) % shard_count == shard_index)
     out = np.zeros((nrows, width, 4), dtype=np.float32)
     segs = ctypes.c_uint64(0)
-    p = _params(width, height, spp, max_depth, frame0, row_block, shard_count, shard_index)
+    p = _params(width, height, spp, max_depth, frame0, row_block, shard_count, shard_index,
+                RAW_SUMS if raw_sums else 0)
     rc = load().rto_render(cam.ctypes.data_as(ctypes.c_void_p), _ptr(spheres), len(spheres),
                            _ptr(materials), len(materials), ctypes.byref(p),
                            out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(segs), nthreads)

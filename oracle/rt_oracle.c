@@ -355,6 +355,10 @@ static void render_pixel(const job_t* j, uint32_t x, uint32_t y, float* px, uint
         }
         acc[0] = acc[0] + bs[0]; acc[1] = acc[1] + bs[1]; acc[2] = acc[2] + bs[2];
     }
+    if (p->flags & RTO_FLAG_RAW_SUMS) {
+        px[0] = acc[0]; px[1] = acc[1]; px[2] = acc[2]; px[3] = 0.0f;
+        return;
+    }
     const float fs = (float)p->spp;                     /* collect.wgsl:122 */
     px[0] = acc[0] / fs;
     px[1] = acc[1] / fs;

@@ -54,6 +54,10 @@ void rto_trace_path(const rt_camera* cam, const rt_sphere* spheres, uint32_t n,
                     uint32_t height, uint32_t x, uint32_t y, uint32_t frame,
                     uint32_t max_depth, float color[3], uint32_t* segments);
 
+/* params->flags bit: write the block-folded sample SUMS (alpha 0) instead of
+ * sum / spp -- for checking progressive accumulation. */
+#define RTO_FLAG_RAW_SUMS 0x80000000u
+
 /* Full render of the rows owned by params' shard (layout as rt_render).
  * nthreads <= 0 -> 1. Returns 0, or -1 on invalid arguments. */
 int rto_render(const rt_camera* cam, const rt_sphere* spheres, uint32_t n,

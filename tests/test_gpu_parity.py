@@ -285,3 +285,47 @@ def test_plugin_dirty_tracking_animates():
         ref, segs = O.render(RayTraceCamera(96, 54).to_gpu(), sp, mt, 96, 54, 2, 4, frame0=2 * f)
         check_exact(world.resource(RayTraceOutputImage).data, ref)
     assert node.uploads == {"full": 1, "spheres": 2, "materials": 0}
+
+
+def test_progressive_accumulation(renderer):
+    """Running sum across calls: sum = (s1 + s2) + s3 of the calls' block sums,
+    image = sum / total (oracle raw sums folded the same way)."""
+    sp, mt = arrays(scene.rtiow_final_scene())
+    cam = default_camera_block()
+    renderer.set_scene(sp, mt)
+    W, H, D = 80, 45, 8
+    acc = None
+    f0 = 0
+    for k, spp in enumerate([8, 3, 16]):
+        img, total = renderer.render_progressive(cam, W, H, spp, D, frame0=f0, reset=(k == 0))
+        part, _ = O.render(cam, sp, mt, W, H, spp, D, frame0=f0, raw_sums=True)
+        acc = part[..., :3] if acc is None else acc + part[..., :3]
+        f0 += spp
+        assert total == f0
+        exp = np.ones_like(img)
+        exp[..., :3] = acc / np.float32(total)
+        check_exact(img, exp)
+    # reset restarts; a different geometry restarts too
+    img, total = renderer.render_progressive(cam, W, H, 4, D, frame0=0, reset=True)
+    assert total == 4
+    ref, _ = O.render(cam, sp, mt, W, H, 4, D)
+    check_exact(img, ref)
+    img, total = renderer.render_progressive(cam, W + 1, H, 2, D, frame0=0)
+    assert total == 2
+
+
+def test_srgb8_encode(renderer):
+    import torch
+    x = np.random.default_rng(3).uniform(-0.2, 1.3, (1000, 4)).astype(np.float32)
+    x[:5, 0] = [np.nan, np.inf, -np.inf, 0.0031308, 1.0]
+    d_in = torch.from_numpy(x).cuda()
+    d_out = torch.empty((1000, 4), dtype=torch.uint8, device="cuda")
+    renderer.encode_srgb8(d_in.data_ptr(), d_out.data_ptr(), 1000)
+    got = d_out.cpu().numpy().astype(np.int32)
+    c = np.nan_to_num(np.clip(x[:, :3].astype(np.float64), 0, 1), nan=0.0)
+    c[np.isnan(x[:, :3])] = 0
+    s = np.where(c <= 0.0031308, 12.92 * c, 1.055 * c ** (1 / 2.4) - 0.055)
+    exp = np.rint(s * 255).astype(np.int32)
+    assert np.abs(got[:, :3] - exp).max() <= 1
+    assert (got[:, 3] == 255).all()
+    assert got[0, 0] == 0 and got[1, 0] == 255 and got[2, 0] == 0
