@@ -34,6 +34,7 @@ RT_DIELECTRIC = 2
 
 RT_SAMPLE_BLOCK = 8
 RT_FLAG_NO_PRIMARY_CACHE = 0x1
+RT_MAX_PENDING = 2          # frames in flight per ctx (rt_render_device / rt_render_async)
 
 SPHERE_DTYPE = np.dtype(
     [("center", "<f4", (3,)), ("radius", "<f4"), ("material", "<u4"), ("_pad", "<u4", (3,))]

@@ -36,9 +36,30 @@ struct Pass {
 
 }  // namespace
 
+// Per-frame work buffers (one set per frame in flight).
+struct Frame {
+    hipStream_t stream = nullptr;   // the slot's own stream (used when the caller gives none)
+    float4* d_block_sums = nullptr;
+    size_t bs_cap = 0;
+    float4* d_acc = nullptr;
+    size_t acc_cap = 0;
+    float4* d_pd = nullptr;         // pixel table (rt_primary_kernel), 32 B per pixel
+    size_t pd_cap = 0;
+    float4* d_out = nullptr;        // host-output path staging
+    size_t out_cap = 0;
+    uint32_t* d_counters = nullptr; // [0..3] 2 x u64 segment counters, [4..] per-pass work counters
+    size_t counters_cap = 0;        // in u32 words
+    unsigned long long* h_segs = nullptr;  // pinned, 18 counters
+    std::vector<hipEvent_t> ev;     // 2 per pass
+    hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;
+    // the pending call in this slot
+    hipStream_t pending_stream = nullptr;
+    uint32_t passes = 0;
+    uint64_t paths = 0;
+};
+
 struct rt_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;
     std::string err;
     int cu_count = 0;
     int blocks_per_cu = 0;
@@ -56,32 +77,18 @@ struct rt_ctx {
     std::vector<float2> h_rm;
     std::vector<rt_material> h_mats;
 
-    // work buffers
-    float4* d_block_sums = nullptr;
-    size_t bs_cap = 0;
-    float4* d_acc = nullptr;
-    size_t acc_cap = 0;
-    float4* d_pd = nullptr;         // pixel table (rt_primary_kernel), 32 B per pixel
-    size_t pd_cap = 0;
+    // frames in flight: RT_MAX_PENDING slots of per-frame work buffers, each
+    // with its own stream, so frame i+1 can start while frame i drains
+    Frame fr[RT_MAX_PENDING];
+    uint32_t head = 0;      // oldest pending slot
+    uint32_t npending = 0;  // frames enqueued and not yet waited for
+    hipStream_t stream = nullptr;  // = fr[0].stream: scene uploads, intersect, progressive
+    unsigned long long dbg[16] = {};  // diagnostic counters of the last waited frame
+
     float4* d_prog = nullptr;       // progressive running sum (rt_render_progressive)
     size_t prog_cap = 0;
     uint64_t prog_total = 0;        // samples accumulated so far
     uint64_t prog_key = 0;          // geometry the running sum belongs to
-    float4* d_out = nullptr;        // host-output path staging
-    size_t out_cap = 0;
-    uint32_t* d_counters = nullptr; // [0..3] 2 x u64 segment counters, [4..] per-pass work counters
-    size_t counters_cap = 0;        // in u32 words
-    unsigned long long* h_segs = nullptr;  // pinned, 2 counters
-    std::vector<hipEvent_t> ev;     // 2 per pass
-    hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;
-
-    // pending call (async)
-    bool pending = false;
-    hipStream_t pending_stream = nullptr;
-    uint32_t pending_passes = 0;
-    float* pending_host_out = nullptr;
-    size_t pending_out_bytes = 0;
-    uint64_t pending_paths = 0;
 };
 
 static int fail(rt_ctx* ctx, int code, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
@@ -138,7 +145,13 @@ static size_t scratch_limit() {
         unsigned long long v = strtoull(s, nullptr, 10);
         if (v >= 16) return (size_t)v;
     }
-    return (size_t)4 << 30;  // 4 GiB of block sums per pass
+    return (size_t)8 << 30;  // 8 GiB of block sums per pass (of 288 GB HBM)
+}
+
+// RT_TAIL_SPLIT=0 turns the single-sample tail items off (A/B measurements).
+static bool tail_split_enabled() {
+    const char* s = getenv("RT_TAIL_SPLIT");
+    return !(s && s[0] == '0');
 }
 
 extern "C" {
@@ -176,14 +189,18 @@ int rt_create(int device, rt_ctx** out_ctx) {
     int rc = RT_OK;
     do {
         if ((e = hipSetDevice(device)) != hipSuccess) break;
-        if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) break;
         if ((e = hipDeviceGetAttribute(&ctx->cu_count, hipDeviceAttributeMultiprocessorCount,
                                        device)) != hipSuccess)
             break;
         if ((e = rt_render_occupancy(&ctx->blocks_per_cu)) != hipSuccess) break;
-        if ((e = hipHostMalloc((void**)&ctx->h_segs, 18 * sizeof(unsigned long long))) != hipSuccess) break;
-        if ((e = hipEventCreate(&ctx->ev_t0)) != hipSuccess) break;
-        if ((e = hipEventCreate(&ctx->ev_t1)) != hipSuccess) break;
+        for (Frame& f : ctx->fr) {
+            if ((e = hipStreamCreateWithFlags(&f.stream, hipStreamNonBlocking)) != hipSuccess) break;
+            if ((e = hipHostMalloc((void**)&f.h_segs, 18 * sizeof(unsigned long long))) != hipSuccess)
+                break;
+            if ((e = hipEventCreate(&f.ev_t0)) != hipSuccess) break;
+            if ((e = hipEventCreate(&f.ev_t1)) != hipSuccess) break;
+        }
+        ctx->stream = ctx->fr[0].stream;
     } while (0);
     if (e != hipSuccess) {
         rc = fail(nullptr, RT_ERR_DEVICE, "rt_create: %s", hipGetErrorString(e));
@@ -198,23 +215,27 @@ int rt_create(int device, rt_ctx** out_ctx) {
 void rt_destroy(rt_ctx* ctx) {
     if (!ctx) return;
     hipSetDevice(ctx->device);
-    if (ctx->stream) hipStreamSynchronize(ctx->stream);
-    if (ctx->pending && ctx->pending_stream) hipStreamSynchronize(ctx->pending_stream);
+    for (Frame& f : ctx->fr) {
+        if (f.stream) hipStreamSynchronize(f.stream);
+        if (f.pending_stream) hipStreamSynchronize(f.pending_stream);
+    }
     hipFree(ctx->d_grp);
     hipFree(ctx->d_sph);
     hipFree(ctx->d_sph_rm);
     hipFree(ctx->d_mats);
-    hipFree(ctx->d_block_sums);
-    hipFree(ctx->d_acc);
-    hipFree(ctx->d_out);
-    hipFree(ctx->d_pd);
     hipFree(ctx->d_prog);
-    hipFree(ctx->d_counters);
-    if (ctx->h_segs) hipHostFree(ctx->h_segs);
-    for (hipEvent_t e : ctx->ev) hipEventDestroy(e);
-    if (ctx->ev_t0) hipEventDestroy(ctx->ev_t0);
-    if (ctx->ev_t1) hipEventDestroy(ctx->ev_t1);
-    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    for (Frame& f : ctx->fr) {
+        hipFree(f.d_block_sums);
+        hipFree(f.d_acc);
+        hipFree(f.d_out);
+        hipFree(f.d_pd);
+        hipFree(f.d_counters);
+        if (f.h_segs) hipHostFree(f.h_segs);
+        for (hipEvent_t e : f.ev) hipEventDestroy(e);
+        if (f.ev_t0) hipEventDestroy(f.ev_t0);
+        if (f.ev_t1) hipEventDestroy(f.ev_t1);
+        if (f.stream) hipStreamDestroy(f.stream);
+    }
     delete ctx;
 }
 
@@ -272,8 +293,10 @@ static int check_spheres(rt_ctx* ctx, const rt_sphere* sp, uint32_t first, uint3
 
 static int quiesce(rt_ctx* ctx) {  // no kernel may be reading the scene while it changes
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    if (ctx->pending && ctx->pending_stream) HIP_TRY(ctx, hipStreamSynchronize(ctx->pending_stream));
+    for (Frame& f : ctx->fr) {
+        HIP_TRY(ctx, hipStreamSynchronize(f.stream));
+        if (f.pending_stream) HIP_TRY(ctx, hipStreamSynchronize(f.pending_stream));
+    }
     return RT_OK;
 }
 
@@ -363,12 +386,12 @@ int rt_update_materials(rt_ctx* ctx, uint32_t first, const rt_material* material
 }
 
 // Validate and enqueue a whole frame on `stream`, writing float4 pixels to d_out.
-static int enqueue(rt_ctx* ctx, const rt_camera* cam, const rt_params* prm, float4* d_out,
-                   hipStream_t stream, uint32_t* out_passes, uint64_t* out_paths,
-                   int prog_mode = 0, float prog_total = 0.0f) {
+// The caller has checked that slot f is free (ctx->npending < RT_MAX_PENDING).
+static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params* prm,
+                   float4* d_out, hipStream_t stream, int prog_mode = 0,
+                   float prog_total = 0.0f) {
     if (!cam || !prm) return fail(ctx, RT_ERR_INVALID_ARG, "camera or params is NULL");
     if (!ctx->has_scene) return fail(ctx, RT_ERR_NO_SCENE, "rt_render before rt_set_scene");
-    if (ctx->pending) return fail(ctx, RT_ERR_INVALID_ARG, "a previous async call was not waited for");
     const rt_params p = *prm;
     if (p.width == 0 || p.height == 0 || p.spp == 0 || p.max_depth == 0)
         return fail(ctx, RT_ERR_INVALID_ARG, "width/height/spp/max_depth must be > 0 (%u,%u,%u,%u)",
@@ -388,36 +411,58 @@ static int enqueue(rt_ctx* ctx, const rt_camera* cam, const rt_params* prm, floa
 
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     std::vector<Pass> passes;
+    // Tail split (KParams::main_blocks): the last `ksplit` blocks of a pass
+    // are traced as single-sample items. Sized so the single-sample phase
+    // (>= ~2 segments per sample) lasts at least one whole-block item of
+    // 8 * max_depth segments per resident lane: ksplit >= D * lanes / (2 npix).
+    const uint64_t lanes = (uint64_t)ctx->cu_count * ctx->blocks_per_cu * RT_BLOCK_THREADS;
+    const bool split = tail_split_enabled() &&
+                       (uint64_t)npix * (2 * RT_SAMPLE_BLOCK) <= 0x7FFFFFFFull;
+    uint32_t ksplit = 0;
+    if (split && npix) {
+        const uint64_t k = ((uint64_t)p.max_depth * lanes + 2ull * npix - 1) / (2ull * npix);
+        ksplit = (uint32_t)(k < 1 ? 1 : (k > blocks_total ? blocks_total : k));
+    }
     if (npix) {
         const size_t per_block = (size_t)npix * sizeof(float4);
-        uint64_t pb = scratch_limit() / per_block;
+        uint64_t slots = scratch_limit() / per_block;  // float4 per pixel per slot
         const uint64_t by_index = 0x7FFFFFFFull / npix;  // work items fit in u32
-        if (pb > by_index) pb = by_index;
+        if (slots > by_index) slots = by_index;
+        uint64_t pb;  // blocks per pass: (pb - ksplit) block sums + 8 ksplit samples
+        if (!ksplit) {
+            pb = slots;
+        } else if (slots > (uint64_t)ksplit * RT_SAMPLE_BLOCK) {
+            pb = slots - (uint64_t)ksplit * (RT_SAMPLE_BLOCK - 1);
+        } else {  // scratch too small for the full split: every block is split
+            pb = slots / RT_SAMPLE_BLOCK;
+            ksplit = (uint32_t)(pb < 1 ? 1 : (pb > blocks_total ? blocks_total : pb));
+        }
         if (pb < 1) pb = 1;
         if (pb > blocks_total) pb = blocks_total;
+        const uint64_t extra = (uint64_t)ksplit * (RT_SAMPLE_BLOCK - 1);
         for (uint32_t b = 0; b < blocks_total; b += (uint32_t)pb) {
             const uint32_t nb = (uint32_t)((blocks_total - b) < pb ? (blocks_total - b) : pb);
             passes.push_back(Pass{b, nb});
         }
-        int rc = ensure(ctx, &ctx->d_block_sums, &ctx->bs_cap, per_block * (size_t)pb);
+        int rc = ensure(ctx, &f.d_block_sums, &f.bs_cap, per_block * (size_t)(pb + extra));
         if (rc) return rc;
-        rc = ensure(ctx, &ctx->d_pd, &ctx->pd_cap, 2 * per_block);  // 32-B pixel table entries
+        rc = ensure(ctx, &f.d_pd, &f.pd_cap, 2 * per_block);  // 32-B pixel table entries
         if (rc) return rc;
         if (passes.size() > 1) {
-            rc = ensure(ctx, &ctx->d_acc, &ctx->acc_cap, per_block);
+            rc = ensure(ctx, &f.d_acc, &f.acc_cap, per_block);
             if (rc) return rc;
         }
     }
     const size_t words = RT_CNT_WORK_OFFSET + passes.size();
     const size_t words_pad = (words + 3) & ~(size_t)3;  // 16-B multiple
     {
-        int rc = ensure(ctx, &ctx->d_counters, &ctx->counters_cap, words_pad * sizeof(uint32_t));
+        int rc = ensure(ctx, &f.d_counters, &f.counters_cap, words_pad * sizeof(uint32_t));
         if (rc) return rc;
     }
-    while (ctx->ev.size() < 2 * passes.size()) {
+    while (f.ev.size() < 2 * passes.size()) {
         hipEvent_t e;
         HIP_TRY(ctx, hipEventCreate(&e));
-        ctx->ev.push_back(e);
+        f.ev.push_back(e);
     }
 
     KParams K_{};
@@ -449,75 +494,104 @@ static int enqueue(rt_ctx* ctx, const rt_camera* cam, const rt_params* prm, floa
     K_.div_8w = make_fastdiv(8 * p.width);
     K_.div_wrem = make_fastdiv(K_.tile_wrem ? K_.tile_wrem : 1);
 
-    HIP_TRY(ctx, hipEventRecord(ctx->ev_t0, stream));
-    HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, words_pad * sizeof(uint32_t), stream));
+    HIP_TRY(ctx, hipEventRecord(f.ev_t0, stream));
+    HIP_TRY(ctx, hipMemsetAsync(f.d_counters, 0, words_pad * sizeof(uint32_t), stream));
     const uint32_t grid_full = (uint32_t)(ctx->cu_count * ctx->blocks_per_cu);
-    if (npix) HIP_TRY(ctx, rt_launch_primary(&K_, ctx->d_pd, stream));
+    if (npix) HIP_TRY(ctx, rt_launch_primary(&K_, f.d_pd, stream));
     for (size_t i = 0; i < passes.size(); ++i) {
         K_.block_begin = passes[i].block_begin;
         K_.nblocks = passes[i].nblocks;
-        const uint64_t items = (uint64_t)npix * K_.nblocks;
+        if (ksplit) {
+            const uint32_t ks = ksplit < K_.nblocks ? ksplit : K_.nblocks;
+            K_.main_blocks = K_.nblocks - ks;
+            K_.split_s0 = (K_.block_begin + K_.main_blocks) * RT_SAMPLE_BLOCK;
+            const uint32_t s_end = (K_.block_begin + K_.nblocks) * RT_SAMPLE_BLOCK;
+            K_.nsplit = (s_end < p.spp ? s_end : p.spp) - K_.split_s0;
+        } else {
+            K_.main_blocks = K_.nblocks;
+            K_.split_s0 = 0;
+            K_.nsplit = 0;
+        }
+        K_.main_items = npix * K_.main_blocks;
+        const uint64_t items = (uint64_t)K_.main_items + (uint64_t)npix * K_.nsplit;
         const uint64_t chunks = (items + RT_WAVE_CHUNK - 1) / RT_WAVE_CHUNK;
         const uint64_t need_blocks = (chunks + (RT_BLOCK_THREADS / 64) - 1) / (RT_BLOCK_THREADS / 64);
         const uint32_t grid = (uint32_t)(need_blocks < grid_full ? need_blocks : grid_full);
         const uint64_t tail_items = 2ull * RT_WAVE_CHUNK * grid * (RT_BLOCK_THREADS / 64);
         K_.tail_start = (uint32_t)(items > tail_items ? items - tail_items : 0);
-        HIP_TRY(ctx, hipEventRecord(ctx->ev[2 * i], stream));
-        HIP_TRY(ctx, rt_launch_render(&K_, ctx->d_grp, ctx->d_sph, ctx->d_sph_rm, ctx->d_mats, ctx->d_pd,
-                                      ctx->d_block_sums,
-                                      ctx->d_counters + RT_CNT_WORK_OFFSET + i,
-                                      reinterpret_cast<unsigned long long*>(ctx->d_counters),
+        HIP_TRY(ctx, hipEventRecord(f.ev[2 * i], stream));
+        HIP_TRY(ctx, rt_launch_render(&K_, ctx->d_grp, ctx->d_sph, ctx->d_sph_rm, ctx->d_mats, f.d_pd,
+                                      f.d_block_sums,
+                                      f.d_counters + RT_CNT_WORK_OFFSET + i,
+                                      reinterpret_cast<unsigned long long*>(f.d_counters),
                                       grid, stream));
-        HIP_TRY(ctx, hipEventRecord(ctx->ev[2 * i + 1], stream));
-        HIP_TRY(ctx, rt_launch_collect(ctx->d_block_sums, npix, K_.nblocks, ctx->d_acc, i == 0,
+        HIP_TRY(ctx, hipEventRecord(f.ev[2 * i + 1], stream));
+        HIP_TRY(ctx, rt_launch_collect(f.d_block_sums, npix, K_.main_blocks, K_.nsplit,
+                                       f.d_acc, i == 0,
                                        i + 1 == passes.size(), (float)p.spp, d_out, ctx->d_prog,
                                        prog_mode, prog_total, stream));
     }
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_segs, ctx->d_counters, 18 * sizeof(unsigned long long),
+    HIP_TRY(ctx, hipMemcpyAsync(f.h_segs, f.d_counters, 18 * sizeof(unsigned long long),
                                 hipMemcpyDeviceToHost, stream));
-    *out_passes = (uint32_t)passes.size();
-    *out_paths = (uint64_t)npix * p.spp;
+    f.passes = (uint32_t)passes.size();
+    f.paths = (uint64_t)npix * p.spp;
     return RT_OK;
 }
 
-// ev_t1 has been recorded by the caller after its last operation.
-static int finish(rt_ctx* ctx, uint32_t passes, uint64_t paths, rt_stats* st) {
-    HIP_TRY(ctx, hipEventSynchronize(ctx->ev_t1));
+// f.ev_t1 has been recorded after the frame's last operation.
+static int finish(rt_ctx* ctx, Frame& f, rt_stats* st) {
+    HIP_TRY(ctx, hipEventSynchronize(f.ev_t1));
+    f.pending_stream = nullptr;
+    for (int i = 0; i < 16; ++i) ctx->dbg[i] = f.h_segs[2 + i];
     if (!st) return RT_OK;
     std::memset(st, 0, sizeof(*st));
     double kms = 0.0;
-    for (uint32_t i = 0; i < passes; ++i) {
+    for (uint32_t i = 0; i < f.passes; ++i) {
         float ms = 0.0f;
-        HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->ev[2 * i], ctx->ev[2 * i + 1]));
+        HIP_TRY(ctx, hipEventElapsedTime(&ms, f.ev[2 * i], f.ev[2 * i + 1]));
         kms += ms;
     }
     float tms = 0.0f;
-    HIP_TRY(ctx, hipEventElapsedTime(&tms, ctx->ev_t0, ctx->ev_t1));
-    st->segments = ctx->h_segs[0];
-    st->traced_segments = ctx->h_segs[1];
+    HIP_TRY(ctx, hipEventElapsedTime(&tms, f.ev_t0, f.ev_t1));
+    st->segments = f.h_segs[0];
+    st->traced_segments = f.h_segs[1];
     st->sphere_tests = st->traced_segments * (uint64_t)ctx->n;
-    st->paths = paths;
+    st->paths = f.paths;
     st->kernel_ms = kms;
     st->total_ms = tms;
-    st->kernel_launches = passes;
+    st->kernel_launches = f.passes;
+    return RT_OK;
+}
+
+// The slot for the next frame, or nullptr (error set) when RT_MAX_PENDING
+// frames are already in flight.
+static Frame* next_slot(rt_ctx* ctx, const char* who) {
+    if (ctx->npending >= RT_MAX_PENDING) {
+        fail(ctx, RT_ERR_INVALID_ARG, "%s: %d calls already pending (rt_wait first)", who,
+             RT_MAX_PENDING);
+        return nullptr;
+    }
+    return &ctx->fr[(ctx->head + ctx->npending) % RT_MAX_PENDING];
+}
+
+static int no_pending(rt_ctx* ctx, const char* who) {
+    if (ctx->npending)
+        return fail(ctx, RT_ERR_INVALID_ARG, "%s: %u async call(s) not waited for", who,
+                    ctx->npending);
     return RT_OK;
 }
 
 int rt_render_device(rt_ctx* ctx, const rt_camera* camera, const rt_params* params,
                      float* out_rgba_device, void* stream) {
     if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_render_device: ctx is NULL");
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
-    uint32_t passes = 0;
-    uint64_t paths = 0;
-    int rc = enqueue(ctx, camera, params, reinterpret_cast<float4*>(out_rgba_device), s, &passes,
-                     &paths);
+    Frame* f = next_slot(ctx, "rt_render_device");
+    if (!f) return RT_ERR_INVALID_ARG;
+    hipStream_t s = stream ? (hipStream_t)stream : f->stream;
+    int rc = enqueue(ctx, *f, camera, params, reinterpret_cast<float4*>(out_rgba_device), s);
     if (rc) return rc;
-    HIP_TRY(ctx, hipEventRecord(ctx->ev_t1, s));
-    ctx->pending = true;
-    ctx->pending_stream = s;
-    ctx->pending_passes = passes;
-    ctx->pending_host_out = nullptr;
-    ctx->pending_paths = paths;
+    HIP_TRY(ctx, hipEventRecord(f->ev_t1, s));
+    f->pending_stream = s;
+    ++ctx->npending;
     return RT_OK;
 }
 
@@ -525,39 +599,39 @@ int rt_render_async(rt_ctx* ctx, const rt_camera* camera, const rt_params* param
     if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_render_async: ctx is NULL");
     if (!out_rgba) return fail(ctx, RT_ERR_INVALID_ARG, "rt_render_async: out_rgba is NULL");
     if (!params) return fail(ctx, RT_ERR_INVALID_ARG, "rt_render_async: params is NULL");
+    Frame* f = next_slot(ctx, "rt_render_async");
+    if (!f) return RT_ERR_INVALID_ARG;
     const uint32_t K = params->shard_count ? params->shard_count : 1;
     const uint32_t rows = rt_shard_rows(params->height, params->row_block, K, params->shard_index);
     const size_t bytes = (size_t)rows * params->width * sizeof(float4);
-    if (ctx->pending) return fail(ctx, RT_ERR_INVALID_ARG, "a previous async call was not waited for");
-    int rc = ensure(ctx, &ctx->d_out, &ctx->out_cap, bytes ? bytes : 16);
+    int rc = ensure(ctx, &f->d_out, &f->out_cap, bytes ? bytes : 16);
     if (rc) return rc;
-    uint32_t passes = 0;
-    uint64_t paths = 0;
-    rc = enqueue(ctx, camera, params, ctx->d_out, ctx->stream, &passes, &paths);
+    rc = enqueue(ctx, *f, camera, params, f->d_out, f->stream);
     if (rc) return rc;
     if (bytes)
-        HIP_TRY(ctx, hipMemcpyAsync(out_rgba, ctx->d_out, bytes, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipEventRecord(ctx->ev_t1, ctx->stream));
-    ctx->pending = true;
-    ctx->pending_stream = ctx->stream;
-    ctx->pending_passes = passes;
-    ctx->pending_host_out = out_rgba;
-    ctx->pending_out_bytes = bytes;
-    ctx->pending_paths = paths;
+        HIP_TRY(ctx, hipMemcpyAsync(out_rgba, f->d_out, bytes, hipMemcpyDeviceToHost, f->stream));
+    HIP_TRY(ctx, hipEventRecord(f->ev_t1, f->stream));
+    f->pending_stream = f->stream;
+    ++ctx->npending;
     return RT_OK;
 }
 
 int rt_wait(rt_ctx* ctx, rt_stats* stats) {
     if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_wait: ctx is NULL");
-    if (!ctx->pending) return fail(ctx, RT_ERR_INVALID_ARG, "rt_wait: nothing pending");
-    ctx->pending = false;
+    if (!ctx->npending) return fail(ctx, RT_ERR_INVALID_ARG, "rt_wait: nothing pending");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    return finish(ctx, ctx->pending_passes, ctx->pending_paths, stats);
+    Frame& f = ctx->fr[ctx->head];
+    ctx->head = (ctx->head + 1) % RT_MAX_PENDING;
+    --ctx->npending;
+    return finish(ctx, f, stats);
 }
 
 int rt_render(rt_ctx* ctx, const rt_camera* camera, const rt_params* params, float* out_rgba,
               rt_stats* stats) {
-    int rc = rt_render_async(ctx, camera, params, out_rgba);
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_render: ctx is NULL");
+    int rc = no_pending(ctx, "rt_render");
+    if (rc) return rc;
+    rc = rt_render_async(ctx, camera, params, out_rgba);
     if (rc) return rc;
     return rt_wait(ctx, stats);
 }
@@ -567,7 +641,9 @@ int rt_render_progressive(rt_ctx* ctx, const rt_camera* camera, const rt_params*
     if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_render_progressive: ctx is NULL");
     if (!out_rgba || !params)
         return fail(ctx, RT_ERR_INVALID_ARG, "rt_render_progressive: NULL argument");
-    if (ctx->pending) return fail(ctx, RT_ERR_INVALID_ARG, "a previous async call was not waited for");
+    int rc = no_pending(ctx, "rt_render_progressive");
+    if (rc) return rc;
+    Frame& f = ctx->fr[ctx->head];
     const uint32_t K = params->shard_count ? params->shard_count : 1;
     const uint32_t B = params->row_block ? params->row_block : 1;
     const uint32_t rows = rt_shard_rows(params->height, B, K, params->shard_index);
@@ -577,20 +653,17 @@ int rt_render_progressive(rt_ctx* ctx, const rt_camera* camera, const rt_params*
     const uint64_t key = ((uint64_t)params->width << 40) ^ ((uint64_t)params->height << 20) ^
                          ((uint64_t)B << 10) ^ ((uint64_t)K << 5) ^ params->shard_index;
     if (key != ctx->prog_key || !ctx->d_prog) reset = 1;
-    int rc = ensure(ctx, &ctx->d_prog, &ctx->prog_cap, bytes ? bytes : 16);
+    rc = ensure(ctx, &ctx->d_prog, &ctx->prog_cap, bytes ? bytes : 16);
     if (rc) return rc;
-    rc = ensure(ctx, &ctx->d_out, &ctx->out_cap, bytes ? bytes : 16);
+    rc = ensure(ctx, &f.d_out, &f.out_cap, bytes ? bytes : 16);
     if (rc) return rc;
     const uint64_t total = (reset ? 0 : ctx->prog_total) + params->spp;
-    uint32_t passes = 0;
-    uint64_t paths = 0;
-    rc = enqueue(ctx, camera, params, ctx->d_out, ctx->stream, &passes, &paths, reset ? 1 : 2,
-                 (float)total);
+    rc = enqueue(ctx, f, camera, params, f.d_out, f.stream, reset ? 1 : 2, (float)total);
     if (rc) return rc;
     if (bytes)
-        HIP_TRY(ctx, hipMemcpyAsync(out_rgba, ctx->d_out, bytes, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipEventRecord(ctx->ev_t1, ctx->stream));
-    HIP_TRY(ctx, hipEventSynchronize(ctx->ev_t1));
+        HIP_TRY(ctx, hipMemcpyAsync(out_rgba, f.d_out, bytes, hipMemcpyDeviceToHost, f.stream));
+    HIP_TRY(ctx, hipEventRecord(f.ev_t1, f.stream));
+    HIP_TRY(ctx, hipEventSynchronize(f.ev_t1));
     ctx->prog_total = total;
     ctx->prog_key = key;
     if (total_spp) *total_spp = total;
@@ -637,7 +710,8 @@ int rt_intersect(rt_ctx* ctx, const float* rays, uint32_t n, int32_t* hit_index,
     if (n == 0) return RT_OK;
     if (!rays || !hit_index || !hit_t)
         return fail(ctx, RT_ERR_INVALID_ARG, "rt_intersect: NULL array");
-    if (ctx->pending) return fail(ctx, RT_ERR_INVALID_ARG, "a previous async call was not waited for");
+    int rc = no_pending(ctx, "rt_intersect");
+    if (rc) return rc;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     void* buf = nullptr;
     const size_t rb = sizeof(float) * 6 * (size_t)n, ob = sizeof(int32_t) * (size_t)n;
@@ -662,7 +736,7 @@ int rt_intersect(rt_ctx* ctx, const float* rays, uint32_t n, int32_t* hit_index,
 // waited call; all zero unless the library was built with -DRT_PROFILE.
 int rt_debug_counters(const rt_ctx* ctx, uint64_t* out16) {
     if (!ctx || !out16) return RT_ERR_INVALID_ARG;
-    for (int i = 0; i < 16; ++i) out16[i] = ctx->h_segs[2 + i];
+    for (int i = 0; i < 16; ++i) out16[i] = ctx->dbg[i];
     return RT_OK;
 }
 

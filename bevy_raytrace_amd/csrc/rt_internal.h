@@ -35,6 +35,16 @@ struct KParams {
     uint32_t npix;         // pixels of this shard (rows * width)
     uint32_t block_begin;  // first sample block of this pass
     uint32_t nblocks;      // sample blocks in this pass
+    // Tail split: the pass's last blocks are dealt as single-sample items (one
+    // path each) so the queue ends on short items -- an 8-sample item of long
+    // paths (up to 8*max_depth iterations) started shortly before the queue
+    // runs dry would otherwise hold its wave while the GPU drains. Enough
+    // blocks are split that the single-sample phase outlasts any whole-block
+    // item (rt_api.cpp: split_blocks).
+    // Items [0, main_items) = (pixel, block) for the first main_blocks blocks;
+    // items [main_items, main_items + nsplit*npix) = (pixel, sample
+    // split_s0 + j), sample-major. Their colours land after the block sums.
+    uint32_t main_blocks, nsplit, main_items, split_s0;
     uint32_t nspheres;
     uint32_t ngroups;      // padded sphere groups of RT_GROUP (see rt_set_scene)
     uint32_t flags;
@@ -56,8 +66,8 @@ hipError_t rt_launch_render(const KParams* P, const float4* grp, const float4* s
                             float4* block_sums,
                             uint32_t* work_counter, unsigned long long* seg_counter, uint32_t grid,
                             hipStream_t stream);
-hipError_t rt_launch_collect(const float4* block_sums, uint32_t npix, uint32_t nblocks,
-                             float4* acc, int first_pass, int last_pass, float spp, float4* out,
+hipError_t rt_launch_collect(const float4* block_sums, uint32_t npix, uint32_t main_blocks,
+                             uint32_t nsplit, float4* acc, int first_pass, int last_pass, float spp, float4* out,
                              float4* prog, int prog_mode, float prog_total, hipStream_t stream);
 hipError_t rt_launch_srgb8(const float4* in, uchar4* out, uint64_t npix, hipStream_t stream);
 hipError_t rt_launch_assemble(const float4* gathered, uint32_t max_rows, float4* image,

@@ -401,16 +401,18 @@ struct PixelEntry {
 
 __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint32_t item,
                                            const PixelEntry* __restrict__ tab) {
-    const uint32_t bl = fdiv(item, P.div_npix);
-    const PixelEntry& e = tab[item - bl * P.npix];
+    const bool split = item >= P.main_items;  // single-sample tail item
+    const uint32_t j = split ? item - P.main_items : item;
+    const uint32_t bl = fdiv(j, P.div_npix);  // block (main) or sample offset (split)
+    const PixelEntry& e = tab[j - bl * P.npix];
     const uint4 pxy = *reinterpret_cast<const uint4*>(&e.p);
     const float4 q = e.d;
-    st.item = bl * P.npix + pxy.x;
+    // output slot: block sums first, then the split samples (same row layout)
+    st.item = (split ? P.main_blocks + bl : bl) * P.npix + pxy.x;
     st.x = pxy.y & 0xFFFFu;
     st.y = pxy.y >> 16;
-    const uint32_t b = P.block_begin + bl;
-    st.s = b * RT_SAMPLE_BLOCK;
-    st.s_end = min(P.spp, st.s + RT_SAMPLE_BLOCK);
+    st.s = split ? P.split_s0 + bl : (P.block_begin + bl) * RT_SAMPLE_BLOCK;
+    st.s_end = split ? st.s + 1 : min(P.spp, st.s + RT_SAMPLE_BLOCK);
     st.bsum = mk(0.0f, 0.0f, 0.0f);
     st.pd = mk(q.x, q.y, q.z);
     start_sample(P, st);
@@ -515,6 +517,14 @@ __device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, f
     return false;
 }
 
+#ifdef RT_WAVE_TRACE
+// Diagnostic build only (-DRT_WAVE_TRACE): per wave (start, end, exhausted-at)
+// in s_memrealtime ticks (100 MHz) and (iterations, items) -- the schedule's
+// tail shape. Read back with rt_debug_wave_trace().
+#define RT_TRACE_MAX_WAVES 32768
+__device__ unsigned long long g_wave_trace[RT_TRACE_MAX_WAVES * 4];
+#endif
+
 __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_render_kernel(
     KParams P, const float4* grp, const float4* __restrict__ sph,
     const float2* __restrict__ sph_rm, const rt_material* __restrict__ mats,
@@ -537,7 +547,25 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
     __syncthreads();
     grp = s_grp;
 #endif
-    const uint32_t total = P.npix * P.nblocks;
+    const uint32_t total = P.main_items + P.nsplit * P.npix;
+#ifdef RT_WAVE_TRACE
+#ifdef RT_WAVE_TRACE_LITE
+    if (lane == 0) {  // stored at once: nothing stays live across the loop
+        const uint32_t wid0 = blockIdx.x * (RT_BLOCK_THREADS / 64) + threadIdx.x / 64;
+        if (wid0 < RT_TRACE_MAX_WAVES) g_wave_trace[wid0 * 4 + 0] = __builtin_amdgcn_s_memrealtime();
+    }
+    const unsigned long long tr_t0 = 0;
+#else
+    const unsigned long long tr_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    unsigned long long tr_ex = 0;
+    uint32_t tr_iters = 0, tr_items = 0, tr_after = 0;
+#ifdef RT_WAVE_TRACE_LITE  // start/end only: keeps the product's register budget
+#define TR_COUNT(x)
+#else
+#define TR_COUNT(x) x
+#endif
+#endif
     const bool use_cache = (P.flags & RT_FLAG_NO_PRIMARY_CACHE) == 0;
 
     PathState st;
@@ -560,6 +588,9 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
                 if (lane == 0) base = atomicAdd(work_counter, chunk);
                 base = __shfl(base, 0);
                 if (base >= total) {
+#ifdef RT_WAVE_TRACE
+                    TR_COUNT(tr_ex = __builtin_amdgcn_s_memrealtime());
+#endif
                     exhausted = true;
                     break;
                 }
@@ -573,10 +604,17 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
                 start_item(P, st, q_next + rank, tab);
                 has_item = true;
             }
+#ifdef RT_WAVE_TRACE
+            TR_COUNT(tr_items += min(avail, cnt));
+#endif
             q_next += min(avail, cnt);
             need = __ballot(!has_item);
         }
         if (__ballot(has_item) == 0) break;
+#ifdef RT_WAVE_TRACE
+        TR_COUNT(++tr_iters);
+        TR_COUNT(tr_after += exhausted ? 1u : 0u);
+#endif
         PROF_MARK(0);
         PROF_ADD(4, 1);
         PROF_ADD(9, (unsigned long long)__popcll(__ballot(has_item)));
@@ -630,6 +668,22 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
     prof_.c[8] = __builtin_amdgcn_s_memtime() - t_begin;
     if (lane == 0)
         for (int i = 0; i < 16; ++i) atomicAdd(dbg + i, prof_.c[i]);
+#endif
+#ifdef RT_WAVE_TRACE
+    {
+        const uint32_t wid = blockIdx.x * (RT_BLOCK_THREADS / 64) + threadIdx.x / 64;
+        if (lane == 0 && wid < RT_TRACE_MAX_WAVES) {
+#ifndef RT_WAVE_TRACE_LITE
+            g_wave_trace[wid * 4 + 0] = tr_t0;
+#else
+            (void)tr_t0;
+#endif
+            g_wave_trace[wid * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+            g_wave_trace[wid * 4 + 2] = tr_ex;
+            g_wave_trace[wid * 4 + 3] = ((unsigned long long)tr_items << 32) |
+                                        (min(tr_after, 65535u) << 16) | min(tr_iters, 65535u);
+        }
+    }
 #endif
     // ---- segment counts: wave reduce, one atomic per wave
     unsigned long long v = segs, w = traced;
@@ -688,29 +742,46 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_kernel(
 }
 
 // Fold this pass's block sums into acc (block order) and, on the last pass,
-// write out = acc / spp with alpha 1 (collect.wgsl:115-125).
+// write out = acc / spp with alpha 1 (collect.wgsl:115-125). The pass's last
+// blocks were traced as single samples (KParams tail split): each of their
+// block sums is formed here exactly as a lane forms it, ((0 + c0) + c1) + ...,
+// in sample order, then folded like any other block.
 // Progressive mode (rt_render_progressive): on the last pass the frame's sum
 // is folded into the running sum, prog = prog + sum (prog_mode 2) or
 // prog = sum (1, reset), and out = prog / total_spp.
 __global__ void rt_collect_kernel(const float4* __restrict__ block_sums, uint32_t npix,
-                                  uint32_t nblocks, float4* __restrict__ acc, int first_pass,
+                                  uint32_t main_blocks, uint32_t nsplit,
+                                  float4* __restrict__ acc, int first_pass,
                                   int last_pass, float spp, float4* __restrict__ out,
                                   float4* __restrict__ prog, int prog_mode, float prog_total) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npix) return;
-    float ax, ay, az;
-    uint32_t b0 = 0;
-    if (first_pass) {
-        const float4 v = block_sums[p];
-        ax = v.x; ay = v.y; az = v.z;
-        b0 = 1;
-    } else {
+    float ax = 0.0f, ay = 0.0f, az = 0.0f;
+    bool have = !first_pass;
+    if (have) {
         const float4 v = acc[p];
         ax = v.x; ay = v.y; az = v.z;
     }
-    for (uint32_t b = b0; b < nblocks; ++b) {
-        const float4 v = block_sums[(size_t)b * npix + p];
-        ax = ax + v.x; ay = ay + v.y; az = az + v.z;
+    const uint32_t nb = main_blocks + (nsplit + RT_SAMPLE_BLOCK - 1) / RT_SAMPLE_BLOCK;
+    for (uint32_t b = 0; b < nb; ++b) {
+        float4 v;
+        if (b < main_blocks) {
+            v = block_sums[(size_t)b * npix + p];
+        } else {  // a split block: its samples' colours, summed in sample order
+            const uint32_t j0 = (b - main_blocks) * RT_SAMPLE_BLOCK;
+            const uint32_t j1 = min(nsplit, j0 + RT_SAMPLE_BLOCK);
+            v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            for (uint32_t j = j0; j < j1; ++j) {
+                const float4 c = block_sums[(size_t)(main_blocks + j) * npix + p];
+                v.x = v.x + c.x; v.y = v.y + c.y; v.z = v.z + c.z;
+            }
+        }
+        if (have) {
+            ax = ax + v.x; ay = ay + v.y; az = az + v.z;
+        } else {
+            ax = v.x; ay = v.y; az = v.z;
+            have = true;
+        }
     }
     if (!last_pass) {
         acc[p] = make_float4(ax, ay, az, 0.0f);
@@ -782,12 +853,13 @@ hipError_t rt_launch_primary(const KParams* P, float4* pd, hipStream_t stream) {
     return hipGetLastError();
 }
 
-hipError_t rt_launch_collect(const float4* block_sums, uint32_t npix, uint32_t nblocks,
-                             float4* acc, int first_pass, int last_pass, float spp, float4* out,
-                             float4* prog, int prog_mode, float prog_total, hipStream_t stream) {
+hipError_t rt_launch_collect(const float4* block_sums, uint32_t npix, uint32_t main_blocks,
+                             uint32_t nsplit, float4* acc, int first_pass, int last_pass, float spp,
+                             float4* out, float4* prog, int prog_mode, float prog_total,
+                             hipStream_t stream) {
     const uint32_t T = 256;
     hipLaunchKernelGGL(rt_collect_kernel, dim3((npix + T - 1) / T), dim3(T), 0, stream,
-                       block_sums, npix, nblocks, acc, first_pass, last_pass, spp, out, prog,
+                       block_sums, npix, main_blocks, nsplit, acc, first_pass, last_pass, spp, out, prog,
                        prog_mode, prog_total);
     return hipGetLastError();
 }
@@ -817,6 +889,15 @@ hipError_t rt_launch_intersect(const float4* grp, const float4* sph, uint32_t ng
                        ngroups, rays, n, out_i, out_t);
     return hipGetLastError();
 }
+
+#ifdef RT_WAVE_TRACE
+int rt_debug_wave_trace(unsigned long long* out, uint32_t max_waves) {
+    if (max_waves > RT_TRACE_MAX_WAVES) max_waves = RT_TRACE_MAX_WAVES;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_trace),
+                               (size_t)max_waves * 4 * sizeof(unsigned long long)) == hipSuccess
+               ? (int)max_waves : -1;
+}
+#endif
 
 hipError_t rt_render_occupancy(int* blocks_per_cu) {
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_render_kernel,

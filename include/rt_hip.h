@@ -175,8 +175,16 @@ int rt_update_materials(rt_ctx* ctx, uint32_t first, const rt_material* material
 int rt_render(rt_ctx* ctx, const rt_camera* camera, const rt_params* params,
               float* out_rgba, rt_stats* stats);
 
+/* Frames in flight: up to RT_MAX_PENDING rt_render_device / rt_render_async
+ * calls may be pending on one ctx. Each pending frame owns a slot of work
+ * buffers and (when no stream is given) its own stream, so the next frame's
+ * waves start on CUs the previous frame's last waves have released.
+ * rt_wait() completes the OLDEST pending frame. rt_render,
+ * rt_render_progressive and rt_intersect require no pending frame. */
+#define RT_MAX_PENDING 2
+
 /* Same, but the output is a DEVICE pointer on this ctx's device and the work
- * is enqueued on `stream` (hipStream_t, NULL = the ctx's own stream).
+ * is enqueued on `stream` (hipStream_t, NULL = the frame slot's own stream).
  * Returns after enqueueing; call rt_wait() before reading stats. */
 int rt_render_device(rt_ctx* ctx, const rt_camera* camera, const rt_params* params,
                      float* out_rgba_device, void* stream);

@@ -101,12 +101,35 @@ def test_multi_pass_scratch_identical(renderer, monkeypatch):
     cam = default_camera_block()
     renderer.set_scene(sp, mt)
     one, st1 = renderer.render(cam, 80, 45, 40, 6)
-    monkeypatch.setenv("RT_SCRATCH_BYTES", str(80 * 45 * 16 * 2))  # 2 blocks per pass
+    # 16 slots: a small image splits every block into single samples (8 slots
+    # per block), so 2 blocks per pass
+    monkeypatch.setenv("RT_SCRATCH_BYTES", str(80 * 45 * 16 * 16))
     many, st2 = renderer.render(cam, 80, 45, 40, 6)
     assert st2["kernel_launches"] == 3 and st1["kernel_launches"] == 1
     check_exact(many, one)
     ref, segs = O.render(cam, sp, mt, 80, 45, 40, 6)
     check_exact(one, ref)
+
+
+@pytest.mark.parametrize("S", [1, 6, 8, 21, 64])
+def test_tail_split_identical(renderer, monkeypatch, S):
+    """The single-sample tail items (last block of a pass, summed in sample
+    order by the collect kernel) give the same image as whole-block items."""
+    sp, mt = arrays(scene.rtiow_final_scene())
+    cam = default_camera_block()
+    renderer.set_scene(sp, mt)
+    on, st_on = renderer.render(cam, 72, 40, S, 10, frame0=5, flags=NO_REUSE)
+    monkeypatch.setenv("RT_TAIL_SPLIT", "0")
+    off, st_off = renderer.render(cam, 72, 40, S, 10, frame0=5, flags=NO_REUSE)
+    check_exact(on, off)
+    assert st_on["segments"] == st_off["segments"]
+    monkeypatch.setenv("RT_SCRATCH_BYTES", str(72 * 40 * 16 * 8))  # 1 (split) block per pass
+    monkeypatch.delenv("RT_TAIL_SPLIT")
+    passes, _ = renderer.render(cam, 72, 40, S, 10, frame0=5)
+    check_exact(passes, on)
+    ref, segs = O.render(cam, sp, mt, 72, 40, S, 10, frame0=5)
+    check_exact(on, ref)
+    assert st_on["segments"] == segs
 
 
 @pytest.mark.parametrize("K,B", [(2, 8), (3, 5), (8, 1)])
@@ -188,6 +211,34 @@ def test_errors(renderer):
         assert e.value.status == abi.RT_ERR_INVALID_ARG
     with pytest.raises(abi.RayTraceError):
         renderer.render(cam, 8, 8, 1, 1, shard_count=2, shard_index=2)
+
+
+def test_frames_in_flight(renderer):
+    """RT_MAX_PENDING frames enqueued back to back (each slot on its own
+    stream) give the same images and stats as one-at-a-time renders; a third
+    enqueue and a synchronous call while frames are pending are refused."""
+    import torch
+    sp, mt = arrays(scene.rtiow_final_scene())
+    cam = default_camera_block()
+    renderer.set_scene(sp, mt)
+    W, H, S, D = 96, 54, 10, 9
+    refs = [renderer.render(cam, W, H, S, D, frame0=f0, flags=NO_REUSE) for f0 in (0, 10)]
+    bufs = [torch.empty((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(2)]
+    for rep in range(2):
+        for b, f0 in zip(bufs, (0, 10)):
+            renderer.render_device(cam, b.data_ptr(), W, H, S, D, frame0=f0, flags=NO_REUSE)
+        if rep == 0:
+            with pytest.raises(abi.RayTraceError) as e:
+                renderer.render_device(cam, bufs[0].data_ptr(), W, H, S, D)
+            assert e.value.status == abi.RT_ERR_INVALID_ARG
+            with pytest.raises(abi.RayTraceError):
+                renderer.render(cam, W, H, S, D)
+        stats = [renderer.wait(), renderer.wait()]
+        for b, st, (ref, rst) in zip(bufs, stats, refs):
+            check_exact(b.cpu().numpy(), ref)
+            assert st["segments"] == rst["segments"]
+    with pytest.raises(abi.RayTraceError):
+        renderer.wait()
 
 
 def test_render_before_scene():
