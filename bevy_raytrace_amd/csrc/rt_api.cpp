@@ -412,15 +412,22 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     std::vector<Pass> passes;
     // Tail split (KParams::main_blocks): the last `ksplit` blocks of a pass
-    // are traced as single-sample items. Sized so the single-sample phase
-    // (>= ~2 segments per sample) lasts at least one whole-block item of
-    // 8 * max_depth segments per resident lane: ksplit >= D * lanes / (2 npix).
+    // are traced as single-sample items, so no wave can be left holding an
+    // 8-sample item when the queue runs dry. Without primary-hit reuse every
+    // block is split (nothing is shared between the samples of a block).
+    // With reuse, whole-block items keep the cached primary hit and the
+    // single-sample phase is sized to outlast one whole-block item of
+    // 8 * max_depth segments on a wave running at a third of the mean
+    // iteration rate (waves of 8x8 tiles full of long paths are that slow):
+    // ksplit >= 3 * D * lanes / (2 * npix) at >= ~2 segments per sample.
     const uint64_t lanes = (uint64_t)ctx->cu_count * ctx->blocks_per_cu * RT_BLOCK_THREADS;
     const bool split = tail_split_enabled() &&
                        (uint64_t)npix * (2 * RT_SAMPLE_BLOCK) <= 0x7FFFFFFFull;
     uint32_t ksplit = 0;
     if (split && npix) {
-        const uint64_t k = ((uint64_t)p.max_depth * lanes + 2ull * npix - 1) / (2ull * npix);
+        uint64_t k = blocks_total;
+        if (!(p.flags & RT_FLAG_NO_PRIMARY_CACHE))
+            k = (3ull * p.max_depth * lanes + 2ull * npix - 1) / (2ull * npix);
         ksplit = (uint32_t)(k < 1 ? 1 : (k > blocks_total ? blocks_total : k));
     }
     if (npix) {
@@ -493,6 +500,18 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     K_.tile_wrem = p.width % 8;
     K_.div_8w = make_fastdiv(8 * p.width);
     K_.div_wrem = make_fastdiv(K_.tile_wrem ? K_.tile_wrem : 1);
+    // wide (sphere-parallel) tracing pays ~32 VALU per 64 spheres per ray plus
+    // a reduction; the ray-parallel walk ~34 per 8-sphere group per wave plus
+    // the drain: switch while k rays cost less sphere-parallel. RT_WIDE_MAX
+    // overrides (0 = never).
+    {
+        const uint64_t per_ray = (uint64_t)((ctx->n + 63) / 64) * 32 + 48;
+        uint64_t k = ((uint64_t)ctx->ngroups * 34 + 300) / per_ray;
+        if (k > 16) k = 16;
+        const char* e = getenv("RT_WIDE_MAX");
+        if (e && *e) k = strtoul(e, nullptr, 10);
+        K_.wide_max = (uint32_t)k;
+    }
 
     HIP_TRY(ctx, hipEventRecord(f.ev_t0, stream));
     HIP_TRY(ctx, hipMemsetAsync(f.d_counters, 0, words_pad * sizeof(uint32_t), stream));

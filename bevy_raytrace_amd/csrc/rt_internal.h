@@ -45,6 +45,9 @@ struct KParams {
     // items [main_items, main_items + nsplit*npix) = (pixel, sample
     // split_s0 + j), sample-major. Their colours land after the block sums.
     uint32_t main_blocks, nsplit, main_items, split_s0;
+    // a wave with at most wide_max live rays traces them sphere-parallel
+    // (intersect_wide): the tail of the queue, where waves empty out
+    uint32_t wide_max;
     uint32_t nspheres;
     uint32_t ngroups;      // padded sphere groups of RT_GROUP (see rt_set_scene)
     uint32_t flags;

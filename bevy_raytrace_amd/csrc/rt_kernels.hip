@@ -175,6 +175,7 @@ __device__ __forceinline__ void exact_test(float4 s, int idx, v3 o, v3 d, float 
 }
 
 typedef float f2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(4))) const float4 cfloat4;  // scalar-cache reads
 
 __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f2 bc(float x) { return f2{x, x}; }
@@ -264,17 +265,23 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
     uint32_t ecnt[2] = {0, 0};
 #endif
     for (uint32_t g = 0; g < ngroups; ++g) {
-        const float4* p = grp + (size_t)g * 8;
+        // constant address space: the group is read with s_load into SGPRs
+        // whatever the alias analysis concludes about other stores
+#if defined(__HIP_DEVICE_COMPILE__)
+        const cfloat4* p = (const cfloat4*)(uintptr_t)grp + (size_t)g * 8;
+#else
+        const float4* p = grp + (size_t)g * 8;  // host pass: never executed
+#endif
         const float4 X0 = p[0], X1 = p[1], Y0 = p[2], Y1 = p[3];
         const float4 Z0 = p[4], Z1 = p[5], S0 = p[6], S1 = p[7];
         const f2 g01 = filter2(f2{X0.x, X0.y}, f2{Y0.x, Y0.y}, f2{Z0.x, Z0.y}, f2{S0.x, S0.y}, R);
         const f2 g23 = filter2(f2{X0.z, X0.w}, f2{Y0.z, Y0.w}, f2{Z0.z, Z0.w}, f2{S0.z, S0.w}, R);
         const f2 g45 = filter2(f2{X1.x, X1.y}, f2{Y1.x, Y1.y}, f2{Z1.x, Z1.y}, f2{S1.x, S1.y}, R);
         const f2 g67 = filter2(f2{X1.z, X1.w}, f2{Y1.z, Y1.w}, f2{Z1.z, Z1.w}, f2{S1.z, S1.w}, R);
-        // group test: max of the 8 H (v_max3 tree; a NaN H is dropped by
+        // group test: max of the 8 H (v_max3 chain; a NaN H is dropped by
         // max -- a NaN H never hits) against the ray's threshold
-        const float hmax = fmaxf(fmaxf(fmaxf(g01.x, g01.y), fmaxf(g23.x, g23.y)),
-                                 fmaxf(fmaxf(g45.x, g45.y), fmaxf(g67.x, g67.y)));
+        const float hmax = fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(g01.x, g01.y), g23.x), g23.y),
+                                                   g45.x), g45.y), g67.x), g67.y);
         if (__ballot(hmax >= R.T) != 0) {
             PROF_ADD(5, 1);
             if (__ballot(cnt >= RT_CQ_CAP) != 0) {  // a lane's queue is full: drain all
@@ -309,6 +316,48 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
 #endif
     t_out = best_t;
     return best_i;
+}
+
+// Sphere-parallel closest hit for the few live rays of a nearly empty wave
+// (the end of the work queue, where a wave's remaining paths would otherwise
+// each pay the whole ray-parallel list walk): one ray at a time, the 64 lanes
+// split the list and run the exact reference test (intersect.wgsl:97-115) on
+// their spheres in list order with the strict `<`; the wave reduction then
+// takes the smallest t, ties to the smallest index -- exactly the answer of
+// the sequential strict-`<` scan (intersect.wgsl:133-143).
+__device__ __forceinline__ void intersect_wide(const float4* __restrict__ sph, uint32_t n,
+                                               uint64_t active, v3 o, v3 d, int& hi, float& t) {
+    const uint32_t lane = __lane_id();
+    while (active) {
+        const int src = (int)__builtin_ctzll(active);
+        active &= active - 1;
+        const v3 ro = mk(__shfl(o.x, src), __shfl(o.y, src), __shfl(o.z, src));
+        const v3 rd = mk(__shfl(d.x, src), __shfl(d.y, src), __shfl(d.z, src));
+        const float l = sqrtf(dot(rd, rd));
+        const float a = l * l;  // sqr(length(r.dir)), intersect.wgsl:98
+        float bt = VERY_FAR;
+        int bi = -1;
+        for (uint32_t i = lane; i < n; i += 64) {
+#ifdef RT_PROFILE
+            uint32_t ecnt[2];
+            exact_test(sph[i], (int)i, ro, rd, a, bt, bi, ecnt);
+#else
+            exact_test(sph[i], (int)i, ro, rd, a, bt, bi);
+#endif
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            const float ot = __shfl_xor(bt, off);
+            const int oi = __shfl_xor(bi, off);
+            if (ot < bt || (ot == bt && (uint32_t)oi < (uint32_t)bi)) {
+                bt = ot;
+                bi = oi;
+            }
+        }
+        if ((int)lane == src) {
+            hi = bi;
+            t = bt;
+        }
+    }
 }
 
 __device__ __forceinline__ uint32_t lanemask_lt_count(uint64_t m) {
@@ -623,12 +672,17 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
         // a ray that needs tracing here.
         int hi = -1;
         float t = VERY_FAR;
-        if (has_item) {
+        const uint64_t live = __ballot(has_item);
+        if ((uint32_t)__popcll(live) <= P.wide_max) {  // nearly empty wave: sphere-parallel
+            intersect_wide(sph, P.nspheres, live, st.o, st.d, hi, t);
+        } else if (has_item) {
             hi = intersect_world(grp, sph, P.ngroups, st.o, st.d, t, cq
 #ifdef RT_PROFILE
                                  , prof_
 #endif
                                  );
+        }
+        if (has_item) {
             ++traced;
             if (st.bounce == 0) {  // first sample of the block: remember the primary hit
                 cache_hi = hi;

@@ -111,6 +111,23 @@ def test_multi_pass_scratch_identical(renderer, monkeypatch):
     check_exact(one, ref)
 
 
+@pytest.mark.parametrize("wide", ["0", "64"], ids=["never_wide", "always_wide"])
+@pytest.mark.parametrize("name,mk", [("rtiow", scene.rtiow_final_scene), ("glass", glass_scene),
+                                     ("empty", None)])
+def test_sphere_parallel_tail(renderer, monkeypatch, wide, name, mk):
+    """intersect_wide (the nearly-empty-wave path) and the ray-parallel walk
+    give the same image: forced on for every wave, and forced off."""
+    from bevy_raytrace_amd.abi import MATERIAL_DTYPE, SPHERE_DTYPE
+    sp, mt = arrays(mk()) if mk else (np.zeros(0, SPHERE_DTYPE), np.zeros(0, MATERIAL_DTYPE))
+    cam = default_camera_block()
+    renderer.set_scene(sp, mt)
+    monkeypatch.setenv("RT_WIDE_MAX", wide)
+    img, st = renderer.render(cam, 80, 45, 9, 12, frame0=1, flags=NO_REUSE)
+    ref, segs = O.render(cam, sp, mt, 80, 45, 9, 12, frame0=1)
+    check_exact(img, ref)
+    assert st["segments"] == segs
+
+
 @pytest.mark.parametrize("S", [1, 6, 8, 21, 64])
 def test_tail_split_identical(renderer, monkeypatch, S):
     """The single-sample tail items (last block of a pass, summed in sample

@@ -50,6 +50,10 @@ def trace(S, n=1, k=0, rb=8, D=16):
     late = end > np.percentile(end, 90)
     print(f"   slowest 10% waves: iters after dry mean {after[late].mean():.1f}, "
           f"us per post-dry iter {((end - ex)[late] / np.maximum(after[late], 1)).mean():.1f}")
+    order = np.argsort(end)[-5:]
+    for w in order[::-1]:
+        print(f"   straggler wave {w}: end {end[w]:.0f} us, dry seen {ex[w]:.0f} us, iters {iters[w]}, "
+              f"after dry {after[w]}, items {items[w]}")
     hist, edges = np.histogram(end, bins=20, range=(0, span))
     print("   ends histogram:", hist.tolist())
 
