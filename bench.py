@@ -49,13 +49,15 @@ FLOPS_PER_SPHERE_TEST = 18  # intersect.wgsl:97-102, SURVEY §8d
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=12)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default=HEADLINE, choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=0,
                     help="rows of the frame in the CPU sample (0 = auto, ~10 s)")
-    ap.add_argument("--reuse-steps", type=int, default=3,
+    ap.add_argument("--frames-per-launch", type=int, default=4,
+                    help="frames per persistent launch (rt_render_frames_device)")
+    ap.add_argument("--reuse-steps", type=int, default=4,
                     help="extra frames timed with primary-hit reuse on (0 = skip)")
     return ap.parse_args()
 
@@ -106,34 +108,62 @@ def main():
     # so the library enqueues on it rather than on its own stream).
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
-    image = torch.empty((H, W, 4), dtype=torch.float32, device="cuda") if rank == 0 else None
+    # Frames per launch: consecutive frames (frame i = samples i*spp ...) go
+    # through one persistent launch (rt_render_frames_device), so only the
+    # launch -- not every frame -- pays the drain of its last waves.
+    FPL = max(1, args.frames_per_launch)
+    image = (torch.empty((FPL, H, W, 4), dtype=torch.float32, device="cuda")
+             if rank == 0 else None)
     # N=1: the single shard is the image; render straight into it.
-    shard = image if world == 1 else torch.empty((max_rows, W, 4), dtype=torch.float32,
+    shard = image if world == 1 else torch.empty((FPL, max_rows, W, 4), dtype=torch.float32,
                                                   device="cuda")
-    gathered = (torch.empty((world, max_rows, W, 4), dtype=torch.float32, device="cuda")
+    gathered = (torch.empty((world, FPL, max_rows, W, 4), dtype=torch.float32, device="cuda")
                 if (rank == 0 and world > 1) else None)
 
-    def step(flags):
-        r.render_device(cam, shard.data_ptr(), W, H, S, D, 0, B, world, rank, flags,
-                        stream=stream.cuda_stream)
+    def launch(first, nf, flags):
+        """Enqueue frames [first, first + nf): render, then (N > 1) one RCCL
+        gather of the nf shard slabs to rank 0 and the device re-assembly."""
+        r.render_frames_device(cam, nf, shard.data_ptr(), W, H, S, D, first * S, B, world, rank,
+                               flags, stream=stream.cuda_stream)
         if world > 1:
-            dist.gather(shard, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+            dist.gather(shard[:nf], [gathered[k, :nf] for k in range(world)] if rank == 0
+                        else None, dst=0)
             if rank == 0:
-                r.assemble_shards(gathered.data_ptr(), max_rows, image.data_ptr(), W, H, B, world,
-                                  stream=stream.cuda_stream)
-        return r.wait()
+                for fi in range(nf):
+                    slabs = gathered[:, fi].contiguous()
+                    r.assemble_shards(slabs.data_ptr(), max_rows, image[fi].data_ptr(), W, H, B,
+                                      world, stream=stream.cuda_stream)
+
+    def run(nsteps, flags):
+        """nsteps frames in launches of <= FPL frames (near-equal sizes), two
+        launches in flight on the one stream (the CPU enqueues launch j+1
+        while j runs; the GPU never idles between them)."""
+        nl = max(1, -(-nsteps // FPL))
+        sizes = [nsteps // nl + (1 if j < nsteps % nl else 0) for j in range(nl)]
+        stats, first, pending = [], 0, 0
+        for nf in sizes:
+            if pending == abi.RT_MAX_PENDING:
+                stats.append(r.wait())
+                pending -= 1
+            launch(first, nf, flags)
+            first += nf
+            pending += 1
+        while pending:
+            stats.append(r.wait())
+            pending -= 1
+        return stats, sizes
 
     NO_REUSE = abi.RT_FLAG_NO_PRIMARY_CACHE
 
-    for _ in range(args.warmup):
-        step(NO_REUSE)
+    if args.warmup > 0:
+        run(args.warmup, NO_REUSE)
 
     def timed(nsteps, flags):
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        stats = [step(flags) for _ in range(nsteps)]
+        stats, sizes = run(nsteps, flags)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -142,9 +172,9 @@ def main():
             t = torch.tensor([dt], dtype=torch.float64, device="cuda")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
-        return dt, stats
+        return dt, stats, sizes
 
-    dt, stats = timed(args.steps, NO_REUSE)
+    dt, stats, sizes = timed(args.steps, NO_REUSE)
     segs_local = sum(s["segments"] for s in stats)
     traced_local = sum(s["traced_segments"] for s in stats)
     kms = [s["kernel_ms"] for s in stats]
@@ -155,10 +185,11 @@ def main():
 
     reuse = None
     if args.reuse_steps > 0:
-        step(0)
-        rdt, rstats = timed(args.reuse_steps, 0)
+        run(1, 0)
+        rdt, rstats, _ = timed(args.reuse_steps, 0)
         reuse = {"frame_ms": round(rdt / args.reuse_steps * 1e3, 3),
-                 "kernel_ms": round(float(np.mean([s["kernel_ms"] for s in rstats])), 3),
+                 "kernel_ms_per_frame": round(sum(s["kernel_ms"] for s in rstats)
+                                              / args.reuse_steps, 3),
                  "traced_fraction": round(sum(s["traced_segments"] for s in rstats)
                                           / max(1, sum(s["segments"] for s in rstats)), 4),
                  "note": "RT_FLAG_NO_PRIMARY_CACHE off: the pixel-only primary hit is reused "
@@ -171,11 +202,12 @@ def main():
 
     value = segs_all / dt / 1e6
     ms_per_step = dt / args.steps * 1e3
-    kernel_ms = float(np.mean(kms))
-    launches = stats[-1]["kernel_launches"]
-    traced_per_launch = traced_local / args.steps / launches
-    flops_per_launch = traced_per_launch * FLOPS_PER_SPHERE_TEST * nsph
-    achieved = flops_per_launch / (kernel_ms / launches * 1e-3) / 1e12
+    launches = sum(s["kernel_launches"] for s in stats)
+    kernel_ms_total = float(sum(kms))
+    # render launches: the average launch's algorithmic flops / its average
+    # duration (HIP events on the stream the kernel runs on)
+    flops_total = traced_local * FLOPS_PER_SPHERE_TEST * nsph
+    achieved = flops_total / (kernel_ms_total * 1e-3) / 1e12
     traffic = load_traffic(wl.key)
 
     out = {
@@ -193,14 +225,15 @@ def main():
         "data": f"synthetic: seeded RTIOW final scene ({nsph} spheres), camera (13,2,3)->0",
         "config": {"workload": f"{wl.key}: {W}x{H} {S}spp depth {D}, {nsph} spheres",
                    "width": W, "height": H, "spp": S, "max_depth": D, "spheres": nsph,
+                   "frames_per_launch": FPL, "launch_sizes": sizes,
                    "parallelism": f"row-tiled x{world} (blocks of {B} rows) + RCCL gather"
                    if world > 1 else "single GPU"},
         "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
                      "traffic": traffic,
                      "kernel": "rt_render_kernel",
-                     "kernel_ms_per_launch": round(kernel_ms / launches, 3),
-                     "flops_per_launch": flops_per_launch,
+                     "kernel_ms_per_launch": round(kernel_ms_total / launches, 3),
+                     "flops_per_launch": flops_total / launches,
                      "basis": "traced segments x 18 x N_spheres (fp32 VALU; no MFMA)"},
         "segments_per_frame": int(segs_all / args.steps),
         "traced_segments_per_frame": int(traced_all / args.steps),
@@ -209,7 +242,7 @@ def main():
 
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cam, spheres, mats, W, H, S, D, args.cpu_rows,
-                                           image.cpu().numpy())
+                                           image[0].cpu().numpy())
     print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

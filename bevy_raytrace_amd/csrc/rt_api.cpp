@@ -31,7 +31,8 @@ namespace {
 thread_local std::string g_err;  // errors with no context
 
 struct Pass {
-    uint32_t block_begin, nblocks;
+    uint32_t frame_begin, nframes;   // frames of the launch
+    uint32_t block_begin, nblocks;   // sample blocks of each frame in the launch
 };
 
 }  // namespace
@@ -149,9 +150,31 @@ static size_t scratch_limit() {
 }
 
 // RT_TAIL_SPLIT=0 turns the single-sample tail items off (A/B measurements).
+// RT_SPLIT_ALL=1: without primary reuse, trace EVERY block as single samples
+// (the round-1 policy; A/B measurements).
+static bool split_all_enabled() {
+    const char* s = getenv("RT_SPLIT_ALL");
+    return s && s[0] == '1';
+}
+
+// RT_TAIL="a4,a2,a1": tail region lengths (A/B measurements; see enqueue).
+static void tail_weights(double w[3]) {
+    const char* s = getenv("RT_TAIL");
+    if (!s || !*s) return;
+    double v[3];
+    if (sscanf(s, "%lf,%lf,%lf", &v[0], &v[1], &v[2]) == 3 && v[0] >= 0 && v[1] >= 0 && v[2] >= 0)
+        for (int i = 0; i < 3; ++i) w[i] = v[i];
+}
+
 static bool tail_split_enabled() {
     const char* s = getenv("RT_TAIL_SPLIT");
     return !(s && s[0] == '0');
+}
+
+static bool env_flag(const char* name, bool dflt) {
+    const char* s = getenv(name);
+    if (!s || !*s) return dflt;
+    return s[0] != '0';
 }
 
 extern "C" {
@@ -385,10 +408,21 @@ int rt_update_materials(rt_ctx* ctx, uint32_t first, const rt_material* material
     return RT_OK;
 }
 
-// Validate and enqueue a whole frame on `stream`, writing float4 pixels to d_out.
-// The caller has checked that slot f is free (ctx->npending < RT_MAX_PENDING).
+// Validate and enqueue `nframes` frames of one camera on `stream`: frame i
+// covers samples frame0 + i*spp ... (its seeds, shade.wgsl:216-218) and writes
+// rows*width float4 pixels at d_out + i*rows*width.
+//
+// Work plan. The render kernel deals items from ONE queue per launch; a
+// launch may hold several frames (their items back to back), so a frame's
+// last waves overlap the next frame's first ones and only the launch pays a
+// drain tail. Items are (pixel, block of RT_SAMPLE_BLOCK samples); the launch's
+// tail (the last `ksplit` blocks of every frame, dealt after all block items)
+// is traced as single-sample items, so no wave is left holding an 8-sample
+// item of long paths when the queue runs dry. Frames go in one launch while
+// their block sums fit RT_SCRATCH_BYTES; a single frame larger than that runs
+// in several passes over its blocks (acc carries the partial sum).
 static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params* prm,
-                   float4* d_out, hipStream_t stream, int prog_mode = 0,
+                   uint32_t nframes, float4* d_out, hipStream_t stream, int prog_mode = 0,
                    float prog_total = 0.0f) {
     if (!cam || !prm) return fail(ctx, RT_ERR_INVALID_ARG, "camera or params is NULL");
     if (!ctx->has_scene) return fail(ctx, RT_ERR_NO_SCENE, "rt_render before rt_set_scene");
@@ -396,6 +430,7 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     if (p.width == 0 || p.height == 0 || p.spp == 0 || p.max_depth == 0)
         return fail(ctx, RT_ERR_INVALID_ARG, "width/height/spp/max_depth must be > 0 (%u,%u,%u,%u)",
                     p.width, p.height, p.spp, p.max_depth);
+    if (nframes == 0) return fail(ctx, RT_ERR_INVALID_ARG, "nframes must be > 0");
     const uint32_t K = p.shard_count ? p.shard_count : 1;
     const uint32_t B = p.row_block ? p.row_block : 1;
     if (p.shard_index >= K)
@@ -404,6 +439,8 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         return fail(ctx, RT_ERR_INVALID_ARG, "width/height %u x %u above 65535", p.width, p.height);
     if ((uint64_t)p.width * p.height > 0xFFFFFFFFull)
         return fail(ctx, RT_ERR_INVALID_ARG, "image of %u x %u pixels exceeds 2^32", p.width, p.height);
+    if ((uint64_t)nframes * p.spp > 0xFFFFFFFFull)
+        return fail(ctx, RT_ERR_INVALID_ARG, "nframes * spp exceeds 2^32");
     const uint32_t rows = rt_shard_rows(p.height, B, K, p.shard_index);
     const uint32_t npix = rows * p.width;
     const uint32_t blocks_total = (p.spp + RT_SAMPLE_BLOCK - 1) / RT_SAMPLE_BLOCK;
@@ -411,54 +448,75 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
 
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     std::vector<Pass> passes;
-    // Tail split (KParams::main_blocks): the last `ksplit` blocks of a pass
-    // are traced as single-sample items, so no wave can be left holding an
-    // 8-sample item when the queue runs dry. Without primary-hit reuse every
-    // block is split (nothing is shared between the samples of a block).
-    // With reuse, whole-block items keep the cached primary hit and the
-    // single-sample phase is sized to outlast one whole-block item of
-    // 8 * max_depth segments on a wave running at a third of the mean
-    // iteration rate (waves of 8x8 tiles full of long paths are that slow):
-    // ksplit >= 3 * D * lanes / (2 * npix) at >= ~2 segments per sample.
+    const size_t per_block = (size_t)npix * sizeof(float4);  // one slot per pixel
+    // Tail: per lane ~a1*D single samples, and before them optionally a2*D
+    // samples in 2-sample items and a4*D in 4-sample items (RT_TAIL="a4,a2,a1";
+    // default 0,0,12 = single samples only, the measured best on the RTIOW
+    // frames): a block item (<= 8*D iterations) taken before the tail has
+    // finished when the queue runs dry, and an item taken in the tail leaves
+    // at most one short path per lane to drain. In samples per pixel:
     const uint64_t lanes = (uint64_t)ctx->cu_count * ctx->blocks_per_cu * RT_BLOCK_THREADS;
-    const bool split = tail_split_enabled() &&
-                       (uint64_t)npix * (2 * RT_SAMPLE_BLOCK) <= 0x7FFFFFFFull;
-    uint32_t ksplit = 0;
-    if (split && npix) {
-        uint64_t k = blocks_total;
-        if (!(p.flags & RT_FLAG_NO_PRIMARY_CACHE))
-            k = (3ull * p.max_depth * lanes + 2ull * npix - 1) / (2ull * npix);
-        ksplit = (uint32_t)(k < 1 ? 1 : (k > blocks_total ? blocks_total : k));
-    }
+    bool tail_on = tail_split_enabled();
+    double ta[3] = {0.0, 0.0, 12.0};
+    tail_weights(ta);
+    auto per_px = [&](double a, uint64_t mult) -> uint64_t {
+        if (!npix || a <= 0.0) return 0;
+        const uint64_t v = (uint64_t)std::ceil(a * p.max_depth * (double)lanes / (double)npix);
+        return (v + mult - 1) / mult * mult;
+    };
+    const bool all_single = split_all_enabled() && (p.flags & RT_FLAG_NO_PRIMARY_CACHE);
+    const uint64_t A4 = all_single ? 0 : per_px(ta[0], 4), A2 = all_single ? 0 : per_px(ta[1], 2);
+    const uint64_t A1 = all_single ? ~0ull / 4 : per_px(ta[2], 1);
+    auto tail_pairs = [&](uint64_t pairs) -> uint64_t {
+        if (!tail_on || !npix) return 0;
+        const uint64_t L = (A4 + A2 + A1 + RT_SAMPLE_BLOCK - 1) / RT_SAMPLE_BLOCK;
+        return L < 1 ? 1 : (L > pairs ? pairs : L);
+    };
+    // first launch-relative sample g = f*spp + s of pair q (block b of frame f)
+    auto pair_g = [&](uint64_t q, uint64_t nb, uint64_t bb) -> uint64_t {
+        const uint64_t fr = q / nb;
+        return fr * p.spp + (bb + (q - fr * nb)) * RT_SAMPLE_BLOCK;
+    };
+    // slots (= work items per pixel) of a launch of F frames x blocks [bb, bb + nb)
+    auto launch_slots = [&](uint64_t F, uint64_t nb, uint64_t bb) -> uint64_t {
+        const uint64_t pairs = F * nb, L = tail_pairs(pairs);
+        const uint64_t g_end = (F - 1) * p.spp +
+                               std::min<uint64_t>(p.spp, (bb + nb) * RT_SAMPLE_BLOCK);
+        const uint64_t g0 = L ? pair_g(pairs - L, nb, bb) : g_end;
+        return pairs - L + (g_end - g0);
+    };
     if (npix) {
-        const size_t per_block = (size_t)npix * sizeof(float4);
-        uint64_t slots = scratch_limit() / per_block;  // float4 per pixel per slot
+        uint64_t slots_cap = scratch_limit() / per_block;
         const uint64_t by_index = 0x7FFFFFFFull / npix;  // work items fit in u32
-        if (slots > by_index) slots = by_index;
-        uint64_t pb;  // blocks per pass: (pb - ksplit) block sums + 8 ksplit samples
-        if (!ksplit) {
-            pb = slots;
-        } else if (slots > (uint64_t)ksplit * RT_SAMPLE_BLOCK) {
-            pb = slots - (uint64_t)ksplit * (RT_SAMPLE_BLOCK - 1);
-        } else {  // scratch too small for the full split: every block is split
-            pb = slots / RT_SAMPLE_BLOCK;
-            ksplit = (uint32_t)(pb < 1 ? 1 : (pb > blocks_total ? blocks_total : pb));
+        if (slots_cap > by_index) slots_cap = by_index;
+        if (slots_cap < 1) slots_cap = 1;
+        uint64_t bs_slots = 0;
+        uint64_t fpl = nframes;  // frames per launch: as many whole frames as fit
+        while (fpl > 1 && launch_slots(fpl, blocks_total, 0) > slots_cap) --fpl;
+        if (launch_slots(fpl, blocks_total, 0) <= slots_cap) {
+            for (uint32_t i = 0; i < nframes; i += (uint32_t)fpl) {
+                const uint32_t nf = (uint32_t)std::min<uint64_t>(fpl, nframes - i);
+                passes.push_back(Pass{i, nf, 0, blocks_total});
+                bs_slots = std::max(bs_slots, launch_slots(nf, blocks_total, 0));
+            }
+        } else {  // one frame per launch, several passes over its blocks
+            if (launch_slots(1, 1, 0) > slots_cap) tail_on = false;  // no room for a tail
+            uint64_t pb = blocks_total;
+            while (pb > 1 && launch_slots(1, pb, 0) > slots_cap) --pb;
+            for (uint32_t fi = 0; fi < nframes; ++fi)
+                for (uint32_t b = 0; b < blocks_total; b += (uint32_t)pb) {
+                    const uint32_t nb =
+                        (uint32_t)((blocks_total - b) < pb ? (blocks_total - b) : pb);
+                    passes.push_back(Pass{fi, 1, b, nb});
+                    bs_slots = std::max(bs_slots, launch_slots(1, nb, b));
+                }
+            int rc = ensure(ctx, &f.d_acc, &f.acc_cap, per_block);
+            if (rc) return rc;
         }
-        if (pb < 1) pb = 1;
-        if (pb > blocks_total) pb = blocks_total;
-        const uint64_t extra = (uint64_t)ksplit * (RT_SAMPLE_BLOCK - 1);
-        for (uint32_t b = 0; b < blocks_total; b += (uint32_t)pb) {
-            const uint32_t nb = (uint32_t)((blocks_total - b) < pb ? (blocks_total - b) : pb);
-            passes.push_back(Pass{b, nb});
-        }
-        int rc = ensure(ctx, &f.d_block_sums, &f.bs_cap, per_block * (size_t)(pb + extra));
+        int rc = ensure(ctx, &f.d_block_sums, &f.bs_cap, per_block * (size_t)bs_slots);
         if (rc) return rc;
         rc = ensure(ctx, &f.d_pd, &f.pd_cap, 2 * per_block);  // 32-B pixel table entries
         if (rc) return rc;
-        if (passes.size() > 1) {
-            rc = ensure(ctx, &f.d_acc, &f.acc_cap, per_block);
-            if (rc) return rc;
-        }
     }
     const size_t words = RT_CNT_WORK_OFFSET + passes.size();
     const size_t words_pad = (words + 3) & ~(size_t)3;  // 16-B multiple
@@ -500,6 +558,7 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     K_.tile_wrem = p.width % 8;
     K_.div_8w = make_fastdiv(8 * p.width);
     K_.div_wrem = make_fastdiv(K_.tile_wrem ? K_.tile_wrem : 1);
+    K_.prefetch = env_flag("RT_PREFETCH", true) ? 1u : 0u;
     // wide (sphere-parallel) tracing pays ~32 VALU per 64 spheres per ray plus
     // a reduction; the ray-parallel walk ~34 per 8-sphere group per wave plus
     // the drain: switch while k rays cost less sphere-parallel. RT_WIDE_MAX
@@ -518,21 +577,30 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     const uint32_t grid_full = (uint32_t)(ctx->cu_count * ctx->blocks_per_cu);
     if (npix) HIP_TRY(ctx, rt_launch_primary(&K_, f.d_pd, stream));
     for (size_t i = 0; i < passes.size(); ++i) {
-        K_.block_begin = passes[i].block_begin;
-        K_.nblocks = passes[i].nblocks;
-        if (ksplit) {
-            const uint32_t ks = ksplit < K_.nblocks ? ksplit : K_.nblocks;
-            K_.main_blocks = K_.nblocks - ks;
-            K_.split_s0 = (K_.block_begin + K_.main_blocks) * RT_SAMPLE_BLOCK;
-            const uint32_t s_end = (K_.block_begin + K_.nblocks) * RT_SAMPLE_BLOCK;
-            K_.nsplit = (s_end < p.spp ? s_end : p.spp) - K_.split_s0;
-        } else {
-            K_.main_blocks = K_.nblocks;
-            K_.split_s0 = 0;
-            K_.nsplit = 0;
-        }
-        K_.main_items = npix * K_.main_blocks;
-        const uint64_t items = (uint64_t)K_.main_items + (uint64_t)npix * K_.nsplit;
+        const Pass& ps = passes[i];
+        K_.block_begin = ps.block_begin;
+        K_.nblocks = ps.nblocks;
+        K_.div_nblocks = make_fastdiv(ps.nblocks);
+        K_.nframes = ps.nframes;
+        K_.sample_base = ps.frame_begin * p.spp;
+        const uint64_t pairs = (uint64_t)ps.nframes * ps.nblocks, L = tail_pairs(pairs);
+        const uint64_t g_end = (uint64_t)(ps.nframes - 1) * p.spp +
+                               std::min<uint64_t>(p.spp, (uint64_t)(ps.block_begin + ps.nblocks) *
+                                                             RT_SAMPLE_BLOCK);
+        const uint64_t g0 = L ? pair_g(pairs - L, ps.nblocks, ps.block_begin) : g_end;
+        K_.qmain = (uint32_t)(pairs - L);
+        K_.main_all = K_.qmain * npix;
+        // tail regions from the end: single samples, 2-sample, 4-sample items
+        const uint64_t g2 = g_end - std::min<uint64_t>(A1, g_end - g0);
+        const uint64_t g1 = g2 - std::min<uint64_t>(A2, g2 - g0);
+        K_.g0 = (uint32_t)g0;
+        K_.g1 = (uint32_t)g1;
+        K_.g2 = (uint32_t)g2;
+        K_.g_end = (uint32_t)g_end;
+        K_.ti1 = (uint32_t)((g1 - g0 + 3) / 4 * npix);
+        K_.ti2 = K_.ti1 + (uint32_t)((g2 - g1 + 1) / 2 * npix);
+        K_.tail_items = K_.ti2 + (uint32_t)((g_end - g2) * npix);
+        const uint64_t items = (uint64_t)K_.main_all + K_.tail_items;
         const uint64_t chunks = (items + RT_WAVE_CHUNK - 1) / RT_WAVE_CHUNK;
         const uint64_t need_blocks = (chunks + (RT_BLOCK_THREADS / 64) - 1) / (RT_BLOCK_THREADS / 64);
         const uint32_t grid = (uint32_t)(need_blocks < grid_full ? need_blocks : grid_full);
@@ -545,15 +613,16 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
                                       reinterpret_cast<unsigned long long*>(f.d_counters),
                                       grid, stream));
         HIP_TRY(ctx, hipEventRecord(f.ev[2 * i + 1], stream));
-        HIP_TRY(ctx, rt_launch_collect(f.d_block_sums, npix, K_.main_blocks, K_.nsplit,
-                                       f.d_acc, i == 0,
-                                       i + 1 == passes.size(), (float)p.spp, d_out, ctx->d_prog,
-                                       prog_mode, prog_total, stream));
+        const bool first_pass = ps.block_begin == 0;
+        const bool last_pass = ps.block_begin + ps.nblocks == blocks_total;
+        HIP_TRY(ctx, rt_launch_collect(&K_, f.d_pd, f.d_block_sums, f.d_acc, first_pass, last_pass,
+                                       (float)p.spp, d_out + (size_t)ps.frame_begin * npix,
+                                       ctx->d_prog, prog_mode, prog_total, stream));
     }
     HIP_TRY(ctx, hipMemcpyAsync(f.h_segs, f.d_counters, 18 * sizeof(unsigned long long),
                                 hipMemcpyDeviceToHost, stream));
     f.passes = (uint32_t)passes.size();
-    f.paths = (uint64_t)npix * p.spp;
+    f.paths = (uint64_t)npix * p.spp * nframes;
     return RT_OK;
 }
 
@@ -606,7 +675,21 @@ int rt_render_device(rt_ctx* ctx, const rt_camera* camera, const rt_params* para
     Frame* f = next_slot(ctx, "rt_render_device");
     if (!f) return RT_ERR_INVALID_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : f->stream;
-    int rc = enqueue(ctx, *f, camera, params, reinterpret_cast<float4*>(out_rgba_device), s);
+    int rc = enqueue(ctx, *f, camera, params, 1, reinterpret_cast<float4*>(out_rgba_device), s);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipEventRecord(f->ev_t1, s));
+    f->pending_stream = s;
+    ++ctx->npending;
+    return RT_OK;
+}
+
+int rt_render_frames_device(rt_ctx* ctx, const rt_camera* camera, const rt_params* params,
+                            uint32_t nframes, float* out_rgba_device, void* stream) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_render_frames_device: ctx is NULL");
+    Frame* f = next_slot(ctx, "rt_render_frames_device");
+    if (!f) return RT_ERR_INVALID_ARG;
+    hipStream_t s = stream ? (hipStream_t)stream : f->stream;
+    int rc = enqueue(ctx, *f, camera, params, nframes, reinterpret_cast<float4*>(out_rgba_device), s);
     if (rc) return rc;
     HIP_TRY(ctx, hipEventRecord(f->ev_t1, s));
     f->pending_stream = s;
@@ -625,7 +708,7 @@ int rt_render_async(rt_ctx* ctx, const rt_camera* camera, const rt_params* param
     const size_t bytes = (size_t)rows * params->width * sizeof(float4);
     int rc = ensure(ctx, &f->d_out, &f->out_cap, bytes ? bytes : 16);
     if (rc) return rc;
-    rc = enqueue(ctx, *f, camera, params, f->d_out, f->stream);
+    rc = enqueue(ctx, *f, camera, params, 1, f->d_out, f->stream);
     if (rc) return rc;
     if (bytes)
         HIP_TRY(ctx, hipMemcpyAsync(out_rgba, f->d_out, bytes, hipMemcpyDeviceToHost, f->stream));
@@ -677,7 +760,7 @@ int rt_render_progressive(rt_ctx* ctx, const rt_camera* camera, const rt_params*
     rc = ensure(ctx, &f.d_out, &f.out_cap, bytes ? bytes : 16);
     if (rc) return rc;
     const uint64_t total = (reset ? 0 : ctx->prog_total) + params->spp;
-    rc = enqueue(ctx, f, camera, params, f.d_out, f.stream, reset ? 1 : 2, (float)total);
+    rc = enqueue(ctx, f, camera, params, 1, f.d_out, f.stream, reset ? 1 : 2, (float)total);
     if (rc) return rc;
     if (bytes)
         HIP_TRY(ctx, hipMemcpyAsync(out_rgba, f.d_out, bytes, hipMemcpyDeviceToHost, f.stream));

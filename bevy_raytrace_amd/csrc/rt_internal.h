@@ -13,6 +13,7 @@
 // [0,4) two u64 segment counters, [4,36) 16 u64 diagnostic counters
 // (RT_PROFILE builds), [36, ...) one u32 work counter per pass.
 #define RT_CNT_WORK_OFFSET 36
+#define RT_TAIL_ITEM 0x80000000u  // PathState::item flag: a tail item (per-sample slots)
 #define RT_GROUP 8            // spheres per filter group (SoA, 128 B)
 #ifndef RT_CQ_CAP
 #define RT_CQ_CAP 8           // candidate-queue entries per lane (LDS)
@@ -35,16 +36,22 @@ struct KParams {
     uint32_t npix;         // pixels of this shard (rows * width)
     uint32_t block_begin;  // first sample block of this pass
     uint32_t nblocks;      // sample blocks in this pass
-    // Tail split: the pass's last blocks are dealt as single-sample items (one
-    // path each) so the queue ends on short items -- an 8-sample item of long
-    // paths (up to 8*max_depth iterations) started shortly before the queue
-    // runs dry would otherwise hold its wave while the GPU drains. Enough
-    // blocks are split that the single-sample phase outlasts any whole-block
-    // item (rt_api.cpp: split_blocks).
-    // Items [0, main_items) = (pixel, block) for the first main_blocks blocks;
-    // items [main_items, main_items + nsplit*npix) = (pixel, sample
-    // split_s0 + j), sample-major. Their colours land after the block sums.
-    uint32_t main_blocks, nsplit, main_items, split_s0;
+    // Work queue of one launch. The launch covers nframes frames (samples
+    // sample_base + f*spp + [0, spp) of launch frame f; the seed frame is
+    // frame0 + that) x blocks [block_begin, block_begin + nblocks) of each.
+    // Its (frame, block) pairs q = f*nblocks + b are dealt in order: pairs
+    // q < qmain as block items (pixel, 8 samples), items [0, main_all =
+    // qmain*npix), each storing its block sum at slot = its queue index. The
+    // rest -- the launch's tail, launch samples g = f*spp + s in [g0, g_end)
+    // -- is dealt as shrinking items so no wave holds a long item when the
+    // queue runs dry: 4-sample items over [g0, g1), 2-sample over [g1, g2),
+    // single samples over [g2, g_end), each region sample-major; a tail item
+    // stores every sample's colour at slot main_all + (g - g0)*npix + k.
+    // rt_collect_kernel folds the slots per pixel in sample order.
+    uint32_t nframes, sample_base, qmain, main_all;
+    uint32_t g0, g1, g2, g_end;
+    uint32_t ti1, ti2, tail_items;  // tail item offsets of the 2- and 1-sample regions, count
+    FastDiv div_nblocks;
     // a wave with at most wide_max live rays traces them sphere-parallel
     // (intersect_wide): the tail of the queue, where waves empty out
     uint32_t wide_max;
@@ -61,6 +68,7 @@ struct KParams {
     uint32_t tile_full_cols;  // width / 8
     uint32_t tile_wrem;       // width % 8
     FastDiv div_8w, div_wrem;
+    uint32_t prefetch;  // 1: waves prefetch their next work chunk (RT_PREFETCH=0 off)
 };
 
 extern "C" {
@@ -69,8 +77,8 @@ hipError_t rt_launch_render(const KParams* P, const float4* grp, const float4* s
                             float4* block_sums,
                             uint32_t* work_counter, unsigned long long* seg_counter, uint32_t grid,
                             hipStream_t stream);
-hipError_t rt_launch_collect(const float4* block_sums, uint32_t npix, uint32_t main_blocks,
-                             uint32_t nsplit, float4* acc, int first_pass, int last_pass, float spp, float4* out,
+hipError_t rt_launch_collect(const KParams* P, const float4* pd, const float4* block_sums,
+                             float4* acc, int first_pass, int last_pass, float spp, float4* out,
                              float4* prog, int prog_mode, float prog_total, hipStream_t stream);
 hipError_t rt_launch_srgb8(const float4* in, uchar4* out, uint64_t npix, hipStream_t stream);
 hipError_t rt_launch_assemble(const float4* gathered, uint32_t max_rows, float4* image,

@@ -217,6 +217,75 @@ __device__ __forceinline__ f2 filter2(f2 cx, f2 cy, f2 cz, f2 S, const RayF& r) 
     return pk_fma(r.o2x, cx, pk_fma(r.o2y, cy, pk_fma(r.o2z, cz, pk_fma(hb, hb, S))));
 }
 
+// The same filter for a whole group of 8 spheres in hand-scheduled VOP3P:
+// the ray constants live ONCE in 4 VGPR pairs (r0 = (-dnx, -dny),
+// r1 = (-dnz, k1), r2 = (o2x, o2y), r3 = (o2z, T)) and op_sel / op_sel_hi
+// broadcast one half to both packed lanes -- the compiler's form needs every
+// constant duplicated in a pair (7 VGPRs more at the 80-VGPR occupancy limit).
+// The four pair chains are interleaved, so dependent ops are 4 apart (no
+// wait states, and a lone wave in the queue tail issues back to back). Op
+// order per pair is exactly filter2's.
+struct RayP {
+    f2 r0, r1, r2, r3;
+};
+
+__device__ __forceinline__ RayP ray_pack(const RayF& r) {
+    RayP p;
+    p.r0 = f2{r.dx.x, r.dy.x};
+    p.r1 = f2{r.dz.x, r.k1.x};
+    p.r2 = f2{r.o2x.x, r.o2y.x};
+    p.r3 = f2{r.o2z.x, r.T};
+    return p;
+}
+
+__device__ __forceinline__ void filter8(const RayP& R, f2 cxa, f2 cxb, f2 cxc, f2 cxd, f2 cya,
+                                        f2 cyb, f2 cyc, f2 cyd, f2 cza, f2 czb, f2 czc, f2 czd,
+                                        f2 sa, f2 sb, f2 sc, f2 sd, f2& ha, f2& hb, f2& hc,
+                                        f2& hd, float& hmax) {
+    asm volatile(
+        // hb = k1 + (-dnx) cx + (-dny) cy + (-dnz) cz
+        "v_pk_fma_f32 %[ha], %[r0], %[cxa], %[r1] op_sel:[0,0,1] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[hb], %[r0], %[cxb], %[r1] op_sel:[0,0,1] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[hc], %[r0], %[cxc], %[r1] op_sel:[0,0,1] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[hd], %[r0], %[cxd], %[r1] op_sel:[0,0,1] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[ha], %[r0], %[cya], %[ha] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[hb], %[r0], %[cyb], %[hb] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[hc], %[r0], %[cyc], %[hc] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[hd], %[r0], %[cyd], %[hd] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[ha], %[r1], %[cza], %[ha] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[hb], %[r1], %[czb], %[hb] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[hc], %[r1], %[czc], %[hc] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[hd], %[r1], %[czd], %[hd] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        // H = hb^2 + S + o2z cz + o2y cy + o2x cx
+        "v_pk_fma_f32 %[ha], %[ha], %[ha], %[sa]\n\t"
+        "v_pk_fma_f32 %[hb], %[hb], %[hb], %[sb]\n\t"
+        "v_pk_fma_f32 %[hc], %[hc], %[hc], %[sc]\n\t"
+        "v_pk_fma_f32 %[hd], %[hd], %[hd], %[sd]\n\t"
+        "v_pk_fma_f32 %[ha], %[r3], %[cza], %[ha] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[hb], %[r3], %[czb], %[hb] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[hc], %[r3], %[czc], %[hc] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[hd], %[r3], %[czd], %[hd] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[ha], %[r2], %[cya], %[ha] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[hb], %[r2], %[cyb], %[hb] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[hc], %[r2], %[cyc], %[hc] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[hd], %[r2], %[cyd], %[hd] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[ha], %[r2], %[cxa], %[ha] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[hb], %[r2], %[cxb], %[hb] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[hc], %[r2], %[cxc], %[hc] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[hd], %[r2], %[cxd], %[hd] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        // group max of the 8 H (v_max3 drops a quiet-NaN operand, as fmaxf)
+        "v_max3_f32 %[hm], v40, v41, v42\n\t"
+        "v_max3_f32 %[hm], %[hm], v43, v44\n\t"
+        "v_max3_f32 %[hm], %[hm], v45, v46\n\t"
+        "v_max_f32 %[hm], %[hm], v47"
+        : [ha] "={v[40:41]}"(ha), [hb] "={v[42:43]}"(hb), [hc] "={v[44:45]}"(hc),
+          [hd] "={v[46:47]}"(hd), [hm] "=&v"(hmax)
+        : [r0] "v"(R.r0), [r1] "v"(R.r1), [r2] "v"(R.r2), [r3] "v"(R.r3), [cxa] "s"(cxa),
+          [cxb] "s"(cxb), [cxc] "s"(cxc), [cxd] "s"(cxd), [cya] "s"(cya), [cyb] "s"(cyb),
+          [cyc] "s"(cyc), [cyd] "s"(cyd), [cza] "s"(cza), [czb] "s"(czb), [czc] "s"(czc),
+          [czd] "s"(czd), [sa] "s"(sa), [sb] "s"(sb), [sc] "s"(sc), [sd] "s"(sd));
+}
+
 __device__ __forceinline__ uint32_t ge(float h, float t) { return h >= t ? 1u : 0u; }
 
 // Run the exact test for every queued candidate of this lane, in list order.
@@ -256,7 +325,13 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
                                                ) {
     const float l = sqrtf(dot(d, d));
     const float a = l * l;  // sqr(length(r.dir)), intersect.wgsl:98
+#if defined(RT_ASM_FILTER) && defined(__HIP_DEVICE_COMPILE__)
+    const RayP RP = ray_pack(ray_filter_consts(o, d));
+    const float RT_T = RP.r3.y;
+#else
     const RayF R = ray_filter_consts(o, d);
+    const float RT_T = R.T;
+#endif
     const uint32_t lane = __lane_id();
     float best_t = VERY_FAR;
     int best_i = -1;
@@ -264,32 +339,43 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
 #ifdef RT_PROFILE
     uint32_t ecnt[2] = {0, 0};
 #endif
-    for (uint32_t g = 0; g < ngroups; ++g) {
-        // constant address space: the group is read with s_load into SGPRs
-        // whatever the alias analysis concludes about other stores
+    // constant address space: the groups are read with s_load into SGPRs
+    // whatever the alias analysis concludes about other stores
 #if defined(__HIP_DEVICE_COMPILE__)
-        const cfloat4* p = (const cfloat4*)(uintptr_t)grp + (size_t)g * 8;
+    const cfloat4* gp = (const cfloat4*)(uintptr_t)grp;
 #else
-        const float4* p = grp + (size_t)g * 8;  // host pass: never executed
+    const float4* gp = grp;  // host pass: never executed
 #endif
+    for (uint32_t g = 0; g < ngroups; ++g) {
+        const auto* p = gp + (size_t)g * 8;
         const float4 X0 = p[0], X1 = p[1], Y0 = p[2], Y1 = p[3];
         const float4 Z0 = p[4], Z1 = p[5], S0 = p[6], S1 = p[7];
+#if defined(RT_ASM_FILTER) && defined(__HIP_DEVICE_COMPILE__)
+        f2 g01, g23, g45, g67;
+        float hmax;
+        filter8(RP, f2{X0.x, X0.y}, f2{X0.z, X0.w}, f2{X1.x, X1.y}, f2{X1.z, X1.w},
+                f2{Y0.x, Y0.y}, f2{Y0.z, Y0.w}, f2{Y1.x, Y1.y}, f2{Y1.z, Y1.w},
+                f2{Z0.x, Z0.y}, f2{Z0.z, Z0.w}, f2{Z1.x, Z1.y}, f2{Z1.z, Z1.w},
+                f2{S0.x, S0.y}, f2{S0.z, S0.w}, f2{S1.x, S1.y}, f2{S1.z, S1.w}, g01, g23, g45, g67,
+                hmax);
+#else
+        // group test below: max of the 8 H (v_max3 chain; a NaN H is dropped
+        // by max -- a NaN H never hits) against the ray's threshold
         const f2 g01 = filter2(f2{X0.x, X0.y}, f2{Y0.x, Y0.y}, f2{Z0.x, Z0.y}, f2{S0.x, S0.y}, R);
         const f2 g23 = filter2(f2{X0.z, X0.w}, f2{Y0.z, Y0.w}, f2{Z0.z, Z0.w}, f2{S0.z, S0.w}, R);
         const f2 g45 = filter2(f2{X1.x, X1.y}, f2{Y1.x, Y1.y}, f2{Z1.x, Z1.y}, f2{S1.x, S1.y}, R);
         const f2 g67 = filter2(f2{X1.z, X1.w}, f2{Y1.z, Y1.w}, f2{Z1.z, Z1.w}, f2{S1.z, S1.w}, R);
-        // group test: max of the 8 H (v_max3 chain; a NaN H is dropped by
-        // max -- a NaN H never hits) against the ray's threshold
         const float hmax = fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(g01.x, g01.y), g23.x), g23.y),
                                                    g45.x), g45.y), g67.x), g67.y);
-        if (__ballot(hmax >= R.T) != 0) {
+#endif
+        if (__ballot(hmax >= RT_T) != 0) {
             PROF_ADD(5, 1);
             if (__ballot(cnt >= RT_CQ_CAP) != 0) {  // a lane's queue is full: drain all
                 PROF_ADD(11, 1);
                 drain_candidates(cq, cnt, sph, o, d, a, best_t, best_i EXACT_PASS);
                 cnt = 0;
             }
-            const float T = R.T;
+            const float T = RT_T;
             const uint32_t m = ge(g01.x, T) | (ge(g01.y, T) << 1) | (ge(g23.x, T) << 2) |
                                (ge(g23.y, T) << 3) | (ge(g45.x, T) << 4) | (ge(g45.y, T) << 5) |
                                (ge(g67.x, T) << 6) | (ge(g67.y, T) << 7);
@@ -450,20 +536,39 @@ struct PixelEntry {
 
 __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint32_t item,
                                            const PixelEntry* __restrict__ tab) {
-    const bool split = item >= P.main_items;  // single-sample tail item
-    const uint32_t j = split ? item - P.main_items : item;
-    const uint32_t bl = fdiv(j, P.div_npix);  // block (main) or sample offset (split)
-    const PixelEntry& e = tab[j - bl * P.npix];
+    uint32_t k, s0, s1;  // pixel in processing order; the item's samples [s0, s1)
+    if (item < P.main_all) {  // block item of pair q = (frame f, block b)
+        const uint32_t q = fdiv(item, P.div_npix);
+        k = item - q * P.npix;
+        const uint32_t f = fdiv(q, P.div_nblocks);
+        const uint32_t sl = (P.block_begin + (q - f * P.nblocks)) * RT_SAMPLE_BLOCK;
+        s0 = P.sample_base + f * P.spp + sl;
+        s1 = P.sample_base + f * P.spp + min(P.spp, sl + RT_SAMPLE_BLOCK);
+    } else {  // tail item: z = 4, 2 or 1 consecutive samples, each stored on its own
+        uint32_t j = item - P.main_all, z, gb, ge;
+        if (j < P.ti1) {
+            z = 4; gb = P.g0; ge = P.g1;
+        } else if (j < P.ti2) {
+            j -= P.ti1; z = 2; gb = P.g1; ge = P.g2;
+        } else {
+            j -= P.ti2; z = 1; gb = P.g2; ge = P.g_end;
+        }
+        const uint32_t g = fdiv(j, P.div_npix);
+        k = j - g * P.npix;
+        s0 = P.sample_base + gb + g * z;
+        s1 = P.sample_base + min(gb + g * z + z, ge);
+    }
+    const PixelEntry& e = tab[k];
     const uint4 pxy = *reinterpret_cast<const uint4*>(&e.p);
-    const float4 q = e.d;
-    // output slot: block sums first, then the split samples (same row layout)
-    st.item = (split ? P.main_blocks + bl : bl) * P.npix + pxy.x;
+    const float4 q4 = e.d;
+    // block item: its output slot (= queue index); tail item: RT_TAIL_ITEM | k
+    st.item = item < P.main_all ? item : (RT_TAIL_ITEM | k);
     st.x = pxy.y & 0xFFFFu;
     st.y = pxy.y >> 16;
-    st.s = split ? P.split_s0 + bl : (P.block_begin + bl) * RT_SAMPLE_BLOCK;
-    st.s_end = split ? st.s + 1 : min(P.spp, st.s + RT_SAMPLE_BLOCK);
+    st.s = s0;
+    st.s_end = s1;
     st.bsum = mk(0.0f, 0.0f, 0.0f);
-    st.pd = mk(q.x, q.y, q.z);
+    st.pd = mk(q4.x, q4.y, q4.z);
     start_sample(P, st);
 }
 
@@ -566,6 +671,11 @@ __device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, f
     return false;
 }
 
+#ifdef RT_CHUNK_TRACE
+#define RT_CHUNK_TRACE_MAX (1u << 22)
+__device__ unsigned long long g_chunk_trace[RT_CHUNK_TRACE_MAX];
+__device__ unsigned long long g_chunk_clk[RT_CHUNK_TRACE_MAX];  // shader clock (s_memtime)
+#endif
 #ifdef RT_WAVE_TRACE
 // Diagnostic build only (-DRT_WAVE_TRACE): per wave (start, end, exhausted-at)
 // in s_memrealtime ticks (100 MHz) and (iterations, items) -- the schedule's
@@ -596,7 +706,7 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
     __syncthreads();
     grp = s_grp;
 #endif
-    const uint32_t total = P.main_items + P.nsplit * P.npix;
+    const uint32_t total = P.main_all + P.tail_items;
 #ifdef RT_WAVE_TRACE
 #ifdef RT_WAVE_TRACE_LITE
     if (lane == 0) {  // stored at once: nothing stays live across the loop
@@ -624,6 +734,14 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
     uint32_t traced = 0, segs = 0;
     int cache_hi = -1;      // primary hit of this item's pixel (generate.wgsl: pixel-only ray)
     float cache_t = 0.0f;
+    // Chunk prefetch: the atomic for the wave's NEXT chunk is issued as soon as
+    // the current one is taken, so its round trip to the device-scope counter
+    // (one address shared by every wave of the chip) overlaps a whole filter
+    // walk instead of stalling the refill. Every prefetched chunk is consumed:
+    // a wave only stops after consuming a base >= total, and issues no further
+    // prefetch from then on.
+    uint32_t pref = 0;            // lane 0: base of the prefetched chunk
+    uint32_t pref_chunk = 0;      // its size (0 = none in flight)
 
     for (;;) {
         // ---- refill: lanes without an item take the next ones (wave ballot)
@@ -632,10 +750,16 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
             if (q_next >= q_end) {
                 // big chunks keep the counter cold; small ones near the end of
                 // the queue keep the waves' finishing times together
-                const uint32_t chunk = q_end >= P.tail_start ? RT_WAVE_CHUNK_TAIL : RT_WAVE_CHUNK;
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(work_counter, chunk);
+                uint32_t chunk, base = 0;
+                if (pref_chunk) {
+                    chunk = pref_chunk;
+                    base = pref;
+                } else {
+                    chunk = q_end >= P.tail_start ? RT_WAVE_CHUNK_TAIL : RT_WAVE_CHUNK;
+                    if (lane == 0) base = atomicAdd(work_counter, chunk);
+                }
                 base = __shfl(base, 0);
+                pref_chunk = 0;
                 if (base >= total) {
 #ifdef RT_WAVE_TRACE
                     TR_COUNT(tr_ex = __builtin_amdgcn_s_memrealtime());
@@ -645,6 +769,17 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
                 }
                 q_next = base;
                 q_end = min(base + chunk, total);
+#ifdef RT_CHUNK_TRACE
+                // diagnostic: time at which each 64-item slice of the queue is taken
+                if (lane == 0 && (base >> 6) < RT_CHUNK_TRACE_MAX) {
+                    g_chunk_trace[base >> 6] = __builtin_amdgcn_s_memrealtime();
+                    g_chunk_clk[base >> 6] = __builtin_amdgcn_s_memtime();
+                }
+#endif
+                if (P.prefetch) {
+                    pref_chunk = q_end >= P.tail_start ? RT_WAVE_CHUNK_TAIL : RT_WAVE_CHUNK;
+                    if (lane == 0) pref = atomicAdd(work_counter, pref_chunk);
+                }
             }
             const uint32_t avail = q_end - q_next;
             const uint32_t rank = lanemask_lt_count(need);
@@ -698,8 +833,16 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
             const bool done = shade(P, st, hi, t, sph, sph_rm, mats);
             shading = false;
             if (done) {
-                // path finished: accumulate (collect.wgsl:115-120, blocked)
-                st.bsum = add(st.bsum, st.color);
+                // path finished: accumulate (collect.wgsl:115-120, blocked);
+                // a tail item stores every sample's colour for the collect
+                if (st.item & RT_TAIL_ITEM) {
+                    const v3 c = add(mk(0.0f, 0.0f, 0.0f), st.color);
+                    block_sums[P.main_all +
+                               (st.s - P.sample_base - P.g0) * P.npix + (st.item & ~RT_TAIL_ITEM)] =
+                        make_float4(c.x, c.y, c.z, 0.0f);
+                } else {
+                    st.bsum = add(st.bsum, st.color);
+                }
                 ++st.s;
                 if (st.s < st.s_end) {
                     start_sample(P, st);
@@ -709,7 +852,8 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
                         shading = true;
                     }
                 } else {
-                    block_sums[st.item] = make_float4(st.bsum.x, st.bsum.y, st.bsum.z, 0.0f);
+                    if (!(st.item & RT_TAIL_ITEM))
+                        block_sums[st.item] = make_float4(st.bsum.x, st.bsum.y, st.bsum.z, 0.0f);
                     has_item = false;
                 }
             }
@@ -795,38 +939,44 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_kernel(
     out_t[i] = t;
 }
 
-// Fold this pass's block sums into acc (block order) and, on the last pass,
-// write out = acc / spp with alpha 1 (collect.wgsl:115-125). The pass's last
-// blocks were traced as single samples (KParams tail split): each of their
-// block sums is formed here exactly as a lane forms it, ((0 + c0) + c1) + ...,
+// Fold one frame's block sums (launch frame f = blockIdx.y) into acc (block
+// order) and, on the frame's last pass, write out = acc / spp with alpha 1
+// (collect.wgsl:115-125). One thread per pixel of the processing order k
+// (pixel table -> image pixel p). Block b of frame f is pair q = f*nblocks +
+// b: a block item's sum at slot q*npix + k if q < qmain, else a tail block
+// whose samples' colours sit at main_all + (g - g0)*npix + k (g = f*spp + s)
+// and are summed here exactly as a lane sums a block, ((0 + c0) + c1) + ...,
 // in sample order, then folded like any other block.
 // Progressive mode (rt_render_progressive): on the last pass the frame's sum
 // is folded into the running sum, prog = prog + sum (prog_mode 2) or
 // prog = sum (1, reset), and out = prog / total_spp.
-__global__ void rt_collect_kernel(const float4* __restrict__ block_sums, uint32_t npix,
-                                  uint32_t main_blocks, uint32_t nsplit,
+__global__ void rt_collect_kernel(KParams P, const PixelEntry* __restrict__ tab,
+                                  const float4* __restrict__ block_sums,
                                   float4* __restrict__ acc, int first_pass,
                                   int last_pass, float spp, float4* __restrict__ out,
                                   float4* __restrict__ prog, int prog_mode, float prog_total) {
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= npix) return;
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= P.npix) return;
+    const uint32_t f = blockIdx.y;
+    out += (size_t)f * P.npix;
+    const uint32_t p = tab[k].p;
     float ax = 0.0f, ay = 0.0f, az = 0.0f;
     bool have = !first_pass;
     if (have) {
         const float4 v = acc[p];
         ax = v.x; ay = v.y; az = v.z;
     }
-    const uint32_t nb = main_blocks + (nsplit + RT_SAMPLE_BLOCK - 1) / RT_SAMPLE_BLOCK;
-    for (uint32_t b = 0; b < nb; ++b) {
+    for (uint32_t b = 0; b < P.nblocks; ++b) {
+        const uint32_t q = f * P.nblocks + b;
         float4 v;
-        if (b < main_blocks) {
-            v = block_sums[(size_t)b * npix + p];
-        } else {  // a split block: its samples' colours, summed in sample order
-            const uint32_t j0 = (b - main_blocks) * RT_SAMPLE_BLOCK;
-            const uint32_t j1 = min(nsplit, j0 + RT_SAMPLE_BLOCK);
+        if (q < P.qmain) {
+            v = block_sums[(size_t)q * P.npix + k];
+        } else {  // a tail block: its samples' colours, summed in sample order
+            const uint32_t sl = (P.block_begin + b) * RT_SAMPLE_BLOCK;
+            const uint32_t g_end = f * P.spp + min(P.spp, sl + RT_SAMPLE_BLOCK);
             v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            for (uint32_t j = j0; j < j1; ++j) {
-                const float4 c = block_sums[(size_t)(main_blocks + j) * npix + p];
+            for (uint32_t g = f * P.spp + sl; g < g_end; ++g) {
+                const float4 c = block_sums[(size_t)P.main_all + (size_t)(g - P.g0) * P.npix + k];
                 v.x = v.x + c.x; v.y = v.y + c.y; v.z = v.z + c.z;
             }
         }
@@ -907,14 +1057,13 @@ hipError_t rt_launch_primary(const KParams* P, float4* pd, hipStream_t stream) {
     return hipGetLastError();
 }
 
-hipError_t rt_launch_collect(const float4* block_sums, uint32_t npix, uint32_t main_blocks,
-                             uint32_t nsplit, float4* acc, int first_pass, int last_pass, float spp,
-                             float4* out, float4* prog, int prog_mode, float prog_total,
-                             hipStream_t stream) {
+hipError_t rt_launch_collect(const KParams* P, const float4* pd, const float4* block_sums,
+                             float4* acc, int first_pass, int last_pass, float spp, float4* out,
+                             float4* prog, int prog_mode, float prog_total, hipStream_t stream) {
     const uint32_t T = 256;
-    hipLaunchKernelGGL(rt_collect_kernel, dim3((npix + T - 1) / T), dim3(T), 0, stream,
-                       block_sums, npix, main_blocks, nsplit, acc, first_pass, last_pass, spp, out, prog,
-                       prog_mode, prog_total);
+    hipLaunchKernelGGL(rt_collect_kernel, dim3((P->npix + T - 1) / T, P->nframes), dim3(T), 0, stream, *P,
+                       reinterpret_cast<const PixelEntry*>(pd), block_sums, acc, first_pass,
+                       last_pass, spp, out, prog, prog_mode, prog_total);
     return hipGetLastError();
 }
 
@@ -950,6 +1099,15 @@ int rt_debug_wave_trace(unsigned long long* out, uint32_t max_waves) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_trace),
                                (size_t)max_waves * 4 * sizeof(unsigned long long)) == hipSuccess
                ? (int)max_waves : -1;
+}
+#endif
+
+#ifdef RT_CHUNK_TRACE
+int rt_debug_chunk_trace(unsigned long long* out, unsigned long long* clk, uint32_t n) {
+    if (n > RT_CHUNK_TRACE_MAX) n = RT_CHUNK_TRACE_MAX;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chunk_trace), (size_t)n * 8) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(clk, HIP_SYMBOL(g_chunk_clk), (size_t)n * 8) != hipSuccess) return -1;
+    return (int)n;
 }
 #endif
 

@@ -119,6 +119,21 @@ class Renderer:
                                        ctypes.c_void_p(int(stream)) if stream else None)
         check(self.lib, self.ctx, rc)
 
+    def render_frames_device(self, camera: np.ndarray, nframes: int, out_ptr: int, width, height,
+                             spp, max_depth, frame0=0, row_block=8, shard_count=1, shard_index=0,
+                             flags=0, stream=None):
+        """Enqueue `nframes` frames (frame i = samples frame0 + i*spp ...) in one
+        launch into consecutive device images at out_ptr. Call wait() for stats."""
+        cam = np.ascontiguousarray(camera, dtype=abi.CAMERA_DTYPE)
+        p = make_params(width, height, spp, max_depth, frame0, row_block, shard_count, shard_index,
+                        flags)
+        self._keep = (cam, p)
+        rc = self.lib.rt_render_frames_device(self.ctx, cam.ctypes.data_as(ctypes.c_void_p),
+                                              ctypes.byref(p), int(nframes),
+                                              ctypes.c_void_p(int(out_ptr)),
+                                              ctypes.c_void_p(int(stream)) if stream else None)
+        check(self.lib, self.ctx, rc)
+
     def wait(self):
         st = RtStats()
         rc = self.lib.rt_wait(self.ctx, ctypes.byref(st))

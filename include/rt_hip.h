@@ -189,6 +189,18 @@ int rt_render(rt_ctx* ctx, const rt_camera* camera, const rt_params* params,
 int rt_render_device(rt_ctx* ctx, const rt_camera* camera, const rt_params* params,
                      float* out_rgba_device, void* stream);
 
+/* Several frames of one camera in ONE persistent launch (an animation's or a
+ * progressive viewer's consecutive frames; the reference renders one frame
+ * per RayTraceNode::run, src/ray_trace_node.rs:195-224, with globals.frame
+ * advancing per frame, src/ray_trace_globals.rs:56-68). Frame i renders
+ * samples frame0 + i*spp ... frame0 + i*spp + spp - 1 (bit-identical to
+ * rt_render_device with frame0 + i*spp) into the DEVICE buffer
+ * out_rgba_device + i * rt_shard_rows(...) * width * 4. The frames' work
+ * items share one queue, so only the launch (not every frame) pays the drain
+ * of its last waves. Same pending/stream rules as rt_render_device. */
+int rt_render_frames_device(rt_ctx* ctx, const rt_camera* camera, const rt_params* params,
+                            uint32_t nframes, float* out_rgba_device, void* stream);
+
 /* Asynchronous host-output variant: enqueue, return; rt_wait() completes the
  * device->host copy into out_rgba and fills stats. */
 int rt_render_async(rt_ctx* ctx, const rt_camera* camera, const rt_params* params,

@@ -397,3 +397,55 @@ def test_srgb8_encode(renderer):
     assert np.abs(got[:, :3] - exp).max() <= 1
     assert (got[:, 3] == 255).all()
     assert got[0, 0] == 0 and got[1, 0] == 255 and got[2, 0] == 0
+
+
+@pytest.mark.parametrize("flags", [0, NO_REUSE], ids=["reuse", "noreuse"])
+@pytest.mark.parametrize("K,k,scratch", [(1, 0, None), (3, 2, None), (1, 0, "frame"),
+                                         (1, 0, "pass")], ids=["one_launch", "shard",
+                                                                "launch_per_frame", "multi_pass"])
+def test_frames_batch_identical(renderer, monkeypatch, flags, K, k, scratch):
+    """rt_render_frames_device: frame i of one launch == rt_render with
+    frame0 + i*spp (bit-identical, same total segments), also when the scratch
+    limit splits the frames over launches or a frame over passes."""
+    import torch
+    sp, mt = arrays(scene.rtiow_final_scene())
+    cam = default_camera_block()
+    renderer.set_scene(sp, mt)
+    W, H, S, D, F, f0 = 88, 50, 20, 10, 3, 7
+    B = 4
+    rows = len(abi.shard_rows(H, B, K, k))
+    refs = [renderer.render(cam, W, H, S, D, frame0=f0 + i * S, row_block=B, shard_count=K,
+                            shard_index=k, flags=flags) for i in range(F)]
+    if scratch == "frame":   # room for one frame's slots per launch
+        monkeypatch.setenv("RT_SCRATCH_BYTES", str(rows * W * 16 * 3 * 8))
+    elif scratch == "pass":  # less than one frame: several passes per frame
+        monkeypatch.setenv("RT_SCRATCH_BYTES", str(rows * W * 16 * 9))
+    out = torch.full((F, rows, W, 4), -1.0, dtype=torch.float32, device="cuda")
+    renderer.render_frames_device(cam, F, out.data_ptr(), W, H, S, D, frame0=f0, row_block=B,
+                                  shard_count=K, shard_index=k, flags=flags)
+    st = renderer.wait()
+    got = out.cpu().numpy()
+    for i in range(F):
+        check_exact(got[i], refs[i][0])
+    assert st["segments"] == sum(r[1]["segments"] for r in refs)
+    if scratch is None:
+        assert st["kernel_launches"] == 1
+    else:
+        assert st["kernel_launches"] >= F
+    if k == 0 and K == 1:
+        ref, segs = O.render(cam, sp, mt, W, H, S, D, frame0=f0 + 2 * S)
+        check_exact(got[2], ref)
+        assert refs[2][1]["segments"] == segs
+
+
+def test_frames_batch_errors(renderer):
+    import torch
+    sp, mt = arrays(scene.config1_scene())
+    renderer.set_scene(sp, mt)
+    cam = default_camera_block()
+    buf = torch.empty((2, 8, 8, 4), dtype=torch.float32, device="cuda")
+    with pytest.raises(abi.RayTraceError) as e:
+        renderer.render_frames_device(cam, 0, buf.data_ptr(), 8, 8, 1, 1)
+    assert e.value.status == abi.RT_ERR_INVALID_ARG
+    with pytest.raises(abi.RayTraceError):
+        renderer.render_frames_device(cam, 2, 0, 8, 8, 1, 1)

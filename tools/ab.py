@@ -14,6 +14,8 @@ ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--config", default="rtiow1080")
 ap.add_argument("--spp", type=int, default=0)
 ap.add_argument("--flags", type=int, default=abi.RT_FLAG_NO_PRIMARY_CACHE)
+ap.add_argument("--shards", type=int, default=1, help="render one row shard of N (tail-heavy)")
+ap.add_argument("--shard-index", type=int, default=0)
 a = ap.parse_args()
 wl = WORKLOADS[a.config]
 sc = wl.make_scene(); sp, mt = sc.objects_gpu(), sc.materials_gpu()
@@ -26,7 +28,10 @@ ref = None
 times = {p: [] for p in a.libs}
 for rep in range(a.reps + 1):
     for p, r in zip(a.libs, rs):
-        img, st = r.render(cam, wl.width, wl.height, S, wl.max_depth, flags=a.flags)
+        from bevy_raytrace_amd.configs import pick_row_block
+        img, st = r.render(cam, wl.width, wl.height, S, wl.max_depth, flags=a.flags,
+                           row_block=pick_row_block(wl.height, a.shards), shard_count=a.shards,
+                           shard_index=a.shard_index)
         if rep == 0:
             if ref is None:
                 ref = img
