@@ -55,6 +55,13 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=0,
                     help="rows of the frame in the CPU sample (0 = auto, ~10 s)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL over xGMI, the product path); gloo = host-staged "
+                         "gather, for rehearsing N>1 on a one-GPU box")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank on cuda:0 (rehearsal with --dist-backend gloo)")
+    ap.add_argument("--check", action="store_true",
+                    help="add a checksum of the assembled frames to the JSON line")
     ap.add_argument("--frames-per-launch", type=int, default=4,
                     help="frames per persistent launch (rt_render_frames_device)")
     ap.add_argument("--reuse-steps", type=int, default=4,
@@ -86,9 +93,15 @@ def main():
             print(f"--gpus {args.gpus} needs torch.distributed.run (one process per GPU)",
                   file=sys.stderr)
             sys.exit(2)
+    if args.same_device:
+        local = 0
+    red_dev = "cuda" if args.dist_backend == "nccl" else "cpu"  # scalar reductions
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     from bevy_raytrace_amd.renderer import Renderer
 
@@ -126,8 +139,16 @@ def main():
         r.render_frames_device(cam, nf, shard.data_ptr(), W, H, S, D, first * S, B, world, rank,
                                flags, stream=stream.cuda_stream)
         if world > 1:
-            dist.gather(shard[:nf], [gathered[k, :nf] for k in range(world)] if rank == 0
-                        else None, dst=0)
+            if args.dist_backend == "nccl":
+                dist.gather(shard[:nf], [gathered[k, :nf] for k in range(world)] if rank == 0
+                            else None, dst=0)
+            else:  # rehearsal: host-staged gather
+                host = shard[:nf].cpu()
+                parts = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
+                dist.gather(host, parts, dst=0)
+                if rank == 0:
+                    for k in range(world):
+                        gathered[k, :nf].copy_(parts[k])
             if rank == 0:
                 for fi in range(nf):
                     slabs = gathered[:, fi].contiguous()
@@ -169,7 +190,7 @@ def main():
             dist.barrier()
         dt = time.perf_counter() - t0
         if world > 1:
-            t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+            t = torch.tensor([dt], dtype=torch.float64, device=red_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
         return dt, stats, sizes
@@ -178,7 +199,7 @@ def main():
     segs_local = sum(s["segments"] for s in stats)
     traced_local = sum(s["traced_segments"] for s in stats)
     kms = [s["kernel_ms"] for s in stats]
-    tot = torch.tensor([segs_local, traced_local], dtype=torch.float64, device="cuda")
+    tot = torch.tensor([segs_local, traced_local], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(tot)
     segs_all, traced_all = float(tot[0].item()), float(tot[1].item())
@@ -226,7 +247,9 @@ def main():
         "config": {"workload": f"{wl.key}: {W}x{H} {S}spp depth {D}, {nsph} spheres",
                    "width": W, "height": H, "spp": S, "max_depth": D, "spheres": nsph,
                    "frames_per_launch": FPL, "launch_sizes": sizes,
-                   "parallelism": f"row-tiled x{world} (blocks of {B} rows) + RCCL gather"
+                   "parallelism": (f"row-tiled x{world} (blocks of {B} rows) + "
+                                   + ("RCCL gather" if args.dist_backend == "nccl"
+                                      else "host-staged gloo gather (rehearsal)"))
                    if world > 1 else "single GPU"},
         "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
@@ -240,6 +263,12 @@ def main():
         "primary_reuse": reuse,
     }
 
+    if args.check:
+        import hashlib
+        last = sizes[-1]
+        out["check"] = {f"frame{args.steps - last + i}":
+                        hashlib.sha1(image[i].cpu().numpy().tobytes()).hexdigest()[:16]
+                        for i in range(last)}
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cam, spheres, mats, W, H, S, D, args.cpu_rows,
                                            image[0].cpu().numpy())
