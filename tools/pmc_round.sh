@@ -1,19 +1,22 @@
 #!/bin/bash
-# PMC passes (one counter group per rocprofv3 run, --kernel-trace only; no
-# sys/runtime trace with --pmc). Output under gpurun_out/pmc_*.
+# PMC passes over the headline bench command (one counter group per rocprofv3
+# run, --kernel-trace only; no sys/runtime trace with --pmc), each pass under
+# its own time limit. The command renders exactly one 4-frame launch
+# (--steps 4 --warmup 0), so every rt_render_kernel dispatch is the same
+# launch the bench line reports. Output under gpurun_out/pmc_*;
+# tools/pmc_summary.py turns it into profiles/.
 set -uo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 120 rocprofv3 -L > "$R/gpurun_out/pmc_list.txt" 2>&1
-CMD="python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --reuse-steps 0"
+CMD="python3 $R/bench.py --steps 4 --warmup 0 --frames-per-launch 4 --no-cpu-baseline --reuse-steps 0"
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS" \
            "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \
            "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d "$R/gpurun_out/pmc_$i" -o run --output-format csv -- $CMD \
-      > "$R/gpurun_out/pmc_$i.log" 2>&1
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $grp -d "$R/gpurun_out/pmc_$i" -o run \
+      --output-format csv -- $CMD > "$R/gpurun_out/pmc_$i.log" 2>&1
   rc=$?
   echo "pass $i ($grp) rc=$rc"
-  if [ $rc -eq 124 ] || [ $rc -eq 137 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then exit $rc; fi
+  if [ $rc -ne 0 ]; then exit $rc; fi
 done

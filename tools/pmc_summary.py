@@ -1,0 +1,61 @@
+"""Summarise the rocprofv3 PMC passes of tools/pmc_round.sh (gpurun_out/pmc_*)
+into profiles/<round>_pmc_<workload>.json and profiles/pmc_traffic.json.
+
+HBM bytes per render launch follow /opt/skills/guides/MI355X_MICROARCH.md
+(HBM section): FETCH_SIZE and WRITE_SIZE in separate passes, in KB (x1024);
+gfx950's FETCH_SIZE counts half the bytes of wide streaming reads (x2)."""
+import csv, glob, json, os, sys
+from collections import defaultdict
+
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+out_dir = sys.argv[1] if len(sys.argv) > 1 else os.path.join(root, "gpurun_out")
+tag = sys.argv[2] if len(sys.argv) > 2 else "r01"
+wl = sys.argv[3] if len(sys.argv) > 3 else "rtiow1080"
+
+vals = defaultdict(lambda: defaultdict(list))   # kernel -> counter -> per-dispatch values
+durs = defaultdict(list)
+for f in sorted(glob.glob(os.path.join(out_dir, "pmc_*", "**", "*counter_collection.csv"),
+                          recursive=True)):
+    per = defaultdict(float)
+    names = {}
+    with open(f) as fh:
+        for row in csv.DictReader(fh):
+            k = row["Kernel_Name"].split("(")[0]
+            key = (row["Dispatch_Id"], row["Counter_Name"])
+            per[key] += float(row["Counter_Value"])   # summed over dimensions
+            names[row["Dispatch_Id"]] = k
+    for (d, c), v in per.items():
+        vals[names[d]][c].append(v)
+for f in glob.glob(os.path.join(out_dir, "pmc_*", "**", "*kernel_trace.csv"), recursive=True):
+    with open(f) as fh:
+        for row in csv.DictReader(fh):
+            k = row["Kernel_Name"].split("(")[0]
+            durs[k].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-6)
+
+mean = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in vals.items()}
+rk = mean.get("rt_render_kernel", {})
+summary = {"command": "tools/pmc_round.sh: rocprofv3 --kernel-trace --pmc <group> -- python3 bench.py "
+                      "--steps 4 --warmup 0 --frames-per-launch 4 --no-cpu-baseline --reuse-steps 0",
+           "per_dispatch_mean": mean,
+           "render_kernel_ms_under_pmc": (sum(durs["rt_render_kernel"]) / len(durs["rt_render_kernel"])
+                                          if durs["rt_render_kernel"] else None)}
+if rk:
+    w = rk.get("SQ_WAVE_CYCLES"), rk.get("SQ_BUSY_CYCLES"), rk.get("GRBM_GUI_ACTIVE")
+    if rk.get("SQ_ACTIVE_INST_VALU") and rk.get("SQ_WAVES"):
+        summary["valu_inst_per_wave"] = rk["SQ_INSTS_VALU"] / rk["SQ_WAVES"]
+with open(os.path.join(root, "profiles", f"{tag}_pmc_{wl}.json"), "w") as fh:
+    json.dump(summary, fh, indent=1)
+if "FETCH_SIZE" in rk and "WRITE_SIZE" in rk:
+    fetch = rk["FETCH_SIZE"] * 1024 * 2
+    write = rk["WRITE_SIZE"] * 1024
+    tp = os.path.join(root, "profiles", "pmc_traffic.json")
+    d = json.load(open(tp)) if os.path.exists(tp) else {}
+    d[wl] = {"hbm_bytes_per_launch": int(fetch + write), "fetch_bytes": int(fetch),
+             "write_bytes": int(write), "frames_per_launch": 4,
+             "source": f"profiles/{tag}_pmc_{wl}.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
+                       "separate passes; FETCH_SIZE x2 per gfx950 correction, x1024 KB->B)",
+             "note": "per 4-frame render launch: block-sum / tail-sample writes dominate; "
+                     "the sphere list is cache-resident"}
+    json.dump(d, open(tp, "w"), indent=1)
+print(json.dumps({k: summary[k] for k in summary if k != "per_dispatch_mean"}, indent=1))
+print(json.dumps(rk, indent=1))
