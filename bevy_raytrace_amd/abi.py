@@ -34,6 +34,8 @@ RT_DIELECTRIC = 2
 
 RT_SAMPLE_BLOCK = 8
 RT_FLAG_NO_PRIMARY_CACHE = 0x1
+RT_FLAG_JITTER = 0x2             # opt-in sub-pixel jitter (include/rt_hip.h)
+RT_FLAG_THIN_LENS = 0x4          # opt-in thin-lens sample (generate.wgsl:85-107)
 RT_MAX_PENDING = 2          # frames in flight per ctx (rt_render_device / rt_render_async)
 
 SPHERE_DTYPE = np.dtype(

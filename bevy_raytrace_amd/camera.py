@@ -87,17 +87,22 @@ class RayTraceCamera:
         return camera_block(self.transform)
 
 
-def camera_block(transform: Transform, fov=CAMERA_FOV) -> np.ndarray:
+def camera_block(transform: Transform, fov=CAMERA_FOV, image_plane_distance=None,
+                 lens_focal_length=None, fstop=None) -> np.ndarray:
+    """CameraGPU block (ray_trace_camera.rs:43-68); the lens constants default
+    to the reference's (ray_trace_camera.rs:59-62) and only matter to the
+    opt-in thin-lens sampling (RT_FLAG_THIN_LENS) and the focus plane."""
     c = np.zeros((), dtype=CAMERA_DTYPE)
     c["transform"] = transform.compute_matrix()
     c["forward"] = transform.forward()
     c["fov"] = F(fov)
     c["up"] = transform.up()
-    c["image_plane_distance"] = IMAGE_PLANE_DISTANCE
+    c["image_plane_distance"] = (IMAGE_PLANE_DISTANCE if image_plane_distance is None
+                                 else F(image_plane_distance))
     c["right"] = transform.right()
-    c["lens_focal_length"] = LENS_FOCAL_LENGTH
+    c["lens_focal_length"] = LENS_FOCAL_LENGTH if lens_focal_length is None else F(lens_focal_length)
     c["position"] = transform.translation
-    c["fstop"] = FSTOP
+    c["fstop"] = FSTOP if fstop is None else F(fstop)
     return c
 
 

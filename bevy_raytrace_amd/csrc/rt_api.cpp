@@ -547,6 +547,7 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     K_.tan_half = (float)std::tan((double)(cam->fov / 2.0f));                 // generate.wgsl:67
     K_.focus_plane = (cam->image_plane_distance * cam->lens_focal_length) /  // generate.wgsl:94-95
                      (cam->image_plane_distance - cam->lens_focal_length);
+    K_.coc = cam->lens_focal_length / (2.0f * cam->fstop);  // generate.wgsl:97
     K_.aspect = (float)p.width;
     K_.half_w = (float)p.width / 2.0f;
     K_.half_h = (float)p.height / 2.0f;

@@ -60,6 +60,7 @@ struct KParams {
     uint32_t flags;
     float T[16];           // camera transform, column-major
     float tan_half, focus_plane, aspect, half_w, half_h;
+    float coc;             // lens_focal_length / (2 * fstop), generate.wgsl:97 (thin-lens flag)
     FastDiv div_npix, div_width, div_row_block;
     uint32_t tail_start;   // queue position from which waves take RT_WAVE_CHUNK_TAIL items
     // processing order of a block's pixels: 8x8 tiles (rows of tiles), then the

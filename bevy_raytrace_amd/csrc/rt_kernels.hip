@@ -93,6 +93,65 @@ __device__ __forceinline__ void primary_ray(const KParams& P, uint32_t x, uint32
     d.z = ((T[2] * dir.x + T[6] * dir.y) + T[10] * dir.z) + T[14] * 0.0f;
 }
 
+// rt_sincos of the opt-in thin-lens sampling (include/rt_hip.h): Cody-Waite
+// reduction by pi/2, Taylor polynomials, quadrant swap; plain f32 ops in the
+// oracle's order (oracle/rt_oracle.c rto_sincos).
+__device__ __forceinline__ void rt_sincos(float theta, float& s, float& c) {
+    const float q = rintf(theta * 0x1.45f306p-1f);
+    float r = theta - q * 0x1.92p+0f;
+    r = r - q * 0x1.fb5444p-12f;
+    r = r - q * 0x1.68cp-39f;
+    const float r2 = r * r;
+    const float sr = r + r * (r2 * (-0x1.555556p-3f +
+                                    r2 * (0x1.111112p-7f +
+                                          r2 * (-0x1.a01a02p-13f + r2 * 0x1.71de3ap-19f))));
+    const float cr = 1.0f + r2 * (-0x1p-1f +
+                                  r2 * (0x1.555556p-5f +
+                                        r2 * (-0x1.6c16c2p-10f +
+                                              r2 * (0x1.a01a02p-16f + r2 * -0x1.27e4fcp-22f))));
+    switch ((int)q & 3) {
+        case 0: s = sr; c = cr; break;
+        case 1: s = cr; c = -sr; break;
+        case 2: s = -sr; c = -cr; break;
+        default: s = -cr; c = sr; break;
+    }
+}
+
+// Opt-in camera sampling (RT_FLAG_JITTER / RT_FLAG_THIN_LENS, rt_hip.h):
+// generate.wgsl:66-129 with a jittered pixel position and/or a lens sample
+// fed to thin_lens_ray (generate.wgsl:85-107) verbatim. idx = the seed index.
+__device__ __forceinline__ void sampled_primary_ray(const KParams& P, uint32_t x, uint32_t y,
+                                                 uint32_t idx, v3& o, v3& d) {
+    float px = (float)x, py = (float)y;
+    if (P.flags & RT_FLAG_JITTER) {
+        const v3 j = hash3(idx * RT_JITTER_HASH_MUL);
+        px = px + (j.x - 0.5f);
+        py = py + (j.y - 0.5f);
+    }
+    v3 dir = mk(((px - P.half_w) * P.tan_half) / P.aspect,
+                ((-py + P.half_h) * P.tan_half) / P.aspect, -1.0f);
+    dir = normalize(dir);
+    const float denom = dot(dir, mk(0.0f, 0.0f, -1.0f));
+    const v3 fpnt = scale(dir, P.focus_plane / denom);
+    v3 origin = mk(0.0f, 0.0f, 0.0f);
+    if (P.flags & RT_FLAG_THIN_LENS) {
+        const v3 l = hash3(idx * RT_LENS_HASH_MUL);
+        const float pi2 = 2.0f * 3.14159265358979f;
+        const float theta = pi2 * l.x + pi2;
+        const float sr = sqrtf(l.y);
+        float sn, cs;
+        rt_sincos(theta, sn, cs);
+        const float a = (cs * sr) * P.coc, b = (sn * sr) * P.coc;
+        origin = add(mk(1.0f * a, 0.0f * a, 0.0f * a), mk(0.0f * b, 1.0f * b, 0.0f * b));
+    }
+    dir = normalize(sub(fpnt, origin));
+    const float* T = P.T;
+    o = add(origin, mk(T[12], T[13], T[14]));
+    d.x = ((T[0] * dir.x + T[4] * dir.y) + T[8] * dir.z) + T[12] * 0.0f;
+    d.y = ((T[1] * dir.x + T[5] * dir.y) + T[9] * dir.z) + T[13] * 0.0f;
+    d.z = ((T[2] * dir.x + T[6] * dir.y) + T[10] * dir.z) + T[14] * 0.0f;
+}
+
 // shade.wgsl:189-197
 __device__ __forceinline__ v3 sky(v3 d) {
     v3 unit = normalize(d);
@@ -471,9 +530,12 @@ struct PathState {
 // item since it depends on the pixel only), throughput 1 (clear.wgsl:86).
 __device__ __forceinline__ void start_sample(const KParams& P, PathState& st) {
     const uint32_t frame = P.frame0 + st.s;
-    const v3 seed = hash3(st.x + P.width * st.y + (P.width * P.height) * frame);
+    const uint32_t idx = st.x + P.width * st.y + (P.width * P.height) * frame;
+    const v3 seed = hash3(idx);
     st.seedx = seed.x;
     st.nseed = normalize(seed);
+    // (with the opt-in camera sampling the main loop replaces this primary
+    // ray before tracing it: one call site for sampled_primary_ray)
     st.o = mk(0.0f + P.T[12], 0.0f + P.T[13], 0.0f + P.T[14]);
     st.d = st.pd;
     st.color = mk(1.0f, 1.0f, 1.0f);
@@ -725,7 +787,10 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
 #define TR_COUNT(x) x
 #endif
 #endif
-    const bool use_cache = (P.flags & RT_FLAG_NO_PRIMARY_CACHE) == 0;
+    // primary-hit reuse: the primary ray is pixel-only unless the opt-in
+    // camera sampling varies it per sample
+    const bool use_cache =
+        (P.flags & (RT_FLAG_NO_PRIMARY_CACHE | RT_FLAG_JITTER | RT_FLAG_THIN_LENS)) == 0;
 
     PathState st;
     bool has_item = false;
@@ -802,6 +867,13 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
         PROF_MARK(0);
         PROF_ADD(4, 1);
         PROF_ADD(9, (unsigned long long)__popcll(__ballot(has_item)));
+
+        // ---- opt-in camera sampling: a lane at bounce 0 holds a fresh sample
+        // whose primary ray varies per sample (no primary-hit reuse then)
+        if ((P.flags & (RT_FLAG_JITTER | RT_FLAG_THIN_LENS)) && has_item && st.bounce == 0) {
+            const uint32_t idx = st.x + P.width * st.y + (P.width * P.height) * (P.frame0 + st.s);
+            sampled_primary_ray(P, st.x, st.y, idx, st.o, st.d);
+        }
 
         // ---- intersect (intersect.wgsl:145-163): every lane with an item holds
         // a ray that needs tracing here.

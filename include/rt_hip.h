@@ -126,6 +126,30 @@ typedef struct rt_params {
                                           hit is reused across the samples of a
                                           sample block; results are identical) */
 
+/* Opt-in camera sampling: the reference's thin_lens_ray
+ * (generate.wgsl:85-107) is called with lens_offset = (0, 0) and integer
+ * pixel coordinates (generate.wgsl:117-121), so both are latent. These flags
+ * turn them on; they change the image, so they are off by default, and they
+ * disable the primary-hit reuse (the primary ray then varies per sample).
+ * For pixel (x, y) and seed frame f, with idx = x + W*y + W*H*f (u32 wrap,
+ * the shade seed's index, shade.wgsl:216-218):
+ *   RT_FLAG_JITTER    : j = hash3(idx * RT_JITTER_HASH_MUL);
+ *                       pixel = (x + (j.x - 0.5), y + (j.y - 0.5))
+ *   RT_FLAG_THIN_LENS : l = hash3(idx * RT_LENS_HASH_MUL);
+ *                       lens_offset = (2*PI * l.x, l.y), then thin_lens_ray
+ *                       verbatim: theta = lens_offset.x + 2*PI, radius =
+ *                       lens_offset.y, (u, v) = (cos, sin)(theta) * sqrt(radius),
+ *                       origin = (1,0,0)*(u*coc) + (0,1,0)*(v*coc),
+ *                       coc = lens_focal_length / (2 * fstop),
+ *                       dir = normalize(focus_point - origin).
+ * cos/sin are this library's rt_sincos (Cody-Waite reduction by pi/2, Taylor
+ * polynomials of degree 9 / 10, plain f32 ops; |error| < 2e-7), restated
+ * identically by the oracle -- the WGSL leaves them to the driver. */
+#define RT_FLAG_JITTER    0x2u
+#define RT_FLAG_THIN_LENS 0x4u
+#define RT_JITTER_HASH_MUL 0x9E3779B1u
+#define RT_LENS_HASH_MUL   0x85EBCA77u
+
 /* Per-call statistics. */
 typedef struct rt_stats {
     uint64_t segments;         /* algorithmic ray segments = intersect_world calls

@@ -41,6 +41,7 @@ def load():
         lib.rto_tan_half.restype = ctypes.c_float
         lib.rto_primary_ray.argtypes = [vp, u32, u32, u32, u32, fp, fp]
         lib.rto_sky.argtypes = [fp, fp]
+        lib.rto_sincos.argtypes = [ctypes.c_float, fp, fp]
         lib.rto_intersect.argtypes = [vp, u32, fp, fp, fp, fp, fp, ctypes.POINTER(u32)]
         lib.rto_intersect.restype = ctypes.c_int
         lib.rto_intersect_batch.argtypes = [vp, u32, vp, u32, vp, vp, ctypes.c_int]
@@ -81,6 +82,13 @@ def primary_ray(cam, width, height, x, y):
     return np.array(o[:], np.float32), np.array(d[:], np.float32)
 
 
+def sincos(theta):
+    """rt_sincos of the opt-in thin-lens sampling (include/rt_hip.h)."""
+    s, c = ctypes.c_float(0), ctypes.c_float(0)
+    load().rto_sincos(float(theta), ctypes.byref(s), ctypes.byref(c))
+    return np.float32(s.value), np.float32(c.value)
+
+
 def sky(d):
     out = _f3()
     load().rto_sky(_f3(d), out)
@@ -119,7 +127,7 @@ def _params(width, height, spp, max_depth, frame0, row_block, shard_count, shard
 
 
 def render(cam, spheres, materials, width, height, spp, max_depth, frame0=0, row_block=8,
-           shard_count=1, shard_index=0, nthreads=None, raw_sums=False):
+           shard_count=1, shard_index=0, nthreads=None, raw_sums=False, flags=0):
     """Render the shard's rows -> (rows, W, 4) float32, segments.
     raw_sums: the block-folded sample sums instead of sum / spp (alpha 0)."""
     cam = np.ascontiguousarray(cam)
@@ -129,7 +137,7 @@ def render(cam, spheres, materials, width, height, spp, max_depth, frame0=0, row
     out = np.zeros((nrows, width, 4), dtype=np.float32)
     segs = ctypes.c_uint64(0)
     p = _params(width, height, spp, max_depth, frame0, row_block, shard_count, shard_index,
-                RAW_SUMS if raw_sums else 0)
+                (RAW_SUMS if raw_sums else 0) | flags)
     rc = load().rto_render(cam.ctypes.data_as(ctypes.c_void_p), _ptr(spheres), len(spheres),
                            _ptr(materials), len(materials), ctypes.byref(p),
                            out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(segs), nthreads)
@@ -139,13 +147,13 @@ def render(cam, spheres, materials, width, height, spp, max_depth, frame0=0, row
 
 
 def render_rows(cam, spheres, materials, width, height, spp, max_depth, rows, frame0=0,
-                nthreads=None):
+                nthreads=None, flags=0):
     cam = np.ascontiguousarray(cam)
     nthreads = nthreads or os.cpu_count() or 1
     rows = np.ascontiguousarray(rows, dtype=np.uint32)
     out = np.zeros((rows.size, width, 4), dtype=np.float32)
     segs = ctypes.c_uint64(0)
-    p = _params(width, height, spp, max_depth, frame0, 1, 1, 0)
+    p = _params(width, height, spp, max_depth, frame0, 1, 1, 0, flags)
     rc = load().rto_render_rows(cam.ctypes.data_as(ctypes.c_void_p), _ptr(spheres), len(spheres),
                                 _ptr(materials), len(materials), ctypes.byref(p),
                                 rows.ctypes.data_as(ctypes.c_void_p), rows.size,

@@ -68,11 +68,38 @@ void rto_hash3(uint32_t n, float out[3]) {
 
 float rto_tan_half(float fov) { return (float)tan((double)(fov / 2.0f)); }
 
+/* rt_sincos (rt_hip.h "Opt-in camera sampling"): q = rint(theta * 2/pi),
+ * r = theta - q*(pi/2) by a 3-constant Cody-Waite split, Taylor polynomials
+ * on |r| <= pi/4, quadrant swap. Plain f32 ops (no FMA), as the kernel. */
+void rto_sincos(float theta, float* s_out, float* c_out) {
+    const float q = rintf(theta * 0x1.45f306p-1f);
+    float r = theta - q * 0x1.92p+0f;
+    r = r - q * 0x1.fb5444p-12f;
+    r = r - q * 0x1.68cp-39f;
+    const float r2 = r * r;
+    const float sr = r + r * (r2 * (-0x1.555556p-3f +
+                                    r2 * (0x1.111112p-7f +
+                                          r2 * (-0x1.a01a02p-13f + r2 * 0x1.71de3ap-19f))));
+    const float cr = 1.0f + r2 * (-0x1p-1f +
+                                  r2 * (0x1.555556p-5f +
+                                        r2 * (-0x1.6c16c2p-10f +
+                                              r2 * (0x1.a01a02p-16f + r2 * -0x1.27e4fcp-22f))));
+    switch ((int)q & 3) {
+        case 0: *s_out = sr; *c_out = cr; break;
+        case 1: *s_out = cr; *c_out = -sr; break;
+        case 2: *s_out = -sr; *c_out = -cr; break;
+        default: *s_out = -cr; *c_out = sr; break;
+    }
+}
+
 typedef struct {
     float T[16];
     float tan_half;
     float focus_plane;
     float aspect, half_w, half_h;
+    float coc;           /* lens_focal_length / (2 * fstop), generate.wgsl:97 */
+    uint32_t flags;      /* RT_FLAG_JITTER / RT_FLAG_THIN_LENS */
+    uint32_t width, height;
 } cam_t;
 
 static void cam_prepare(const rt_camera* c, uint32_t width, uint32_t height, cam_t* out) {
@@ -84,20 +111,43 @@ static void cam_prepare(const rt_camera* c, uint32_t width, uint32_t height, cam
     out->aspect = (float)width;                 /* generate.wgsl:70 */
     out->half_w = (float)width / 2.0f;          /* generate.wgsl:75 */
     out->half_h = (float)height / 2.0f;         /* generate.wgsl:76 */
+    out->coc = c->lens_focal_length / (2.0f * c->fstop);
+    out->flags = 0;
+    out->width = width;
+    out->height = height;
 }
 
-/* generate.wgsl:66-129 for pixel (x, y). */
-static void primary(const cam_t* c, uint32_t x, uint32_t y, v3* o, v3* d) {
+/* generate.wgsl:66-129 for pixel (x, y) and seed frame `frame` (the frame
+ * only matters with the opt-in jitter / thin-lens flags). */
+static void primary(const cam_t* c, uint32_t x, uint32_t y, uint32_t frame, v3* o, v3* d) {
     float px = (float)x, py = (float)y;
+    const uint32_t idx = x + c->width * y + (c->width * c->height) * frame;
+    if (c->flags & RT_FLAG_JITTER) {            /* opt-in sub-pixel jitter */
+        float j[3];
+        rto_hash3(idx * RT_JITTER_HASH_MUL, j);
+        px = px + (j[0] - 0.5f);
+        py = py + (j[1] - 0.5f);
+    }
     /* pinhole_ray, generate.wgsl:78-79 */
     v3 dir = mk(((px - c->half_w) * c->tan_half) / c->aspect,
                 ((-py + c->half_h) * c->tan_half) / c->aspect, -1.0f);
     dir = normalize(dir);
-    /* thin_lens_ray, generate.wgsl:85-107, lens_offset = (0,0): radius 0 =>
-     * u = v = 0 exactly whatever cos/sin(2*PI) round to, so origin = 0. */
+    /* thin_lens_ray, generate.wgsl:85-107. lens_offset = (0,0) (the
+     * reference): radius 0 => u = v = 0 exactly whatever cos/sin(2*PI) round
+     * to, so origin = 0. */
     float denom = dot(dir, mk(0.0f, 0.0f, -1.0f));
     v3 focus_point = scale(dir, c->focus_plane / denom);
     v3 origin = mk(0.0f, 0.0f, 0.0f);
+    if (c->flags & RT_FLAG_THIN_LENS) {         /* opt-in lens sample */
+        float l[3], sn, cs;
+        rto_hash3(idx * RT_LENS_HASH_MUL, l);
+        const float theta = (2.0f * PI_F) * l[0] + 2.0f * PI_F;   /* :89 */
+        const float sr = sqrtf(l[1]);                                /* :90-93 */
+        rto_sincos(theta, &sn, &cs);
+        const float u = cs * sr, v = sn * sr;
+        const float a = u * c->coc, b = v * c->coc;                  /* :99-100 */
+        origin = add(mk(1.0f * a, 0.0f * a, 0.0f * a), mk(0.0f * b, 1.0f * b, 0.0f * b));
+    }
     dir = normalize(sub(focus_point, origin));
     /* generate.wgsl:125-126 */
     const float* T = c->T;
@@ -115,7 +165,7 @@ void rto_primary_ray(const rt_camera* cam, uint32_t width, uint32_t height, uint
     cam_t c;
     cam_prepare(cam, width, height, &c);
     v3 o, d;
-    primary(&c, x, y, &o, &d);
+    primary(&c, x, y, 0, &o, &d);
     origin[0] = o.x; origin[1] = o.y; origin[2] = o.z;
     dir[0] = d.x; dir[1] = d.y; dir[2] = d.z;
 }
@@ -258,7 +308,7 @@ static v3 trace_path(const cam_t* cam, const rt_sphere* sph, uint32_t n,
                      const rt_material* mats, uint32_t width, uint32_t height, uint32_t x,
                      uint32_t y, uint32_t frame, uint32_t D, uint32_t* segs) {
     v3 o, d;
-    primary(cam, x, y, &o, &d);
+    primary(cam, x, y, frame, &o, &d);
     v3 color = mk(1.0f, 1.0f, 1.0f);                            /* clear.wgsl:82-86 */
     /* seed, shade.wgsl:216-218: identical for every bounce of (pixel, frame) */
     float sd[3];
@@ -402,6 +452,7 @@ int rto_render_rows(const rt_camera* cam, const rt_sphere* spheres, uint32_t n,
     if (nthreads <= 0) nthreads = 1;
     cam_t c;
     cam_prepare(cam, params->width, params->height, &c);
+    c.flags = params->flags & (RT_FLAG_JITTER | RT_FLAG_THIN_LENS);
     job_t* jobs = (job_t*)calloc((size_t)nthreads, sizeof(job_t));
     pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
     for (int t = 0; t < nthreads; ++t) {

@@ -31,6 +31,9 @@ void rto_hash3(uint32_t n, float out[3]);
 /* tan(fov/2) as the renderer uses it (generate.wgsl:67), computed once on the host. */
 float rto_tan_half(float fov);
 
+/* rt_sincos of the opt-in thin-lens sampling (rt_hip.h). */
+void rto_sincos(float theta, float* s, float* c);
+
 /* Primary ray of pixel (x, y): generate.wgsl:66-129 with lens_offset = 0. */
 void rto_primary_ray(const rt_camera* cam, uint32_t width, uint32_t height,
                      uint32_t x, uint32_t y, float origin[3], float dir[3]);
@@ -48,7 +51,8 @@ int rto_intersect(const rt_sphere* spheres, uint32_t n, const float origin[3],
 void rto_intersect_batch(const rt_sphere* spheres, uint32_t n, const float* rays,
                          uint32_t nrays, int32_t* idx, float* t, int nthreads);
 
-/* One path: colour of sample `frame` of pixel (x, y), and its segment count. */
+/* One path: colour of sample `frame` of pixel (x, y), and its segment count
+ * (reference camera sampling: no jitter, lens offset 0). */
 void rto_trace_path(const rt_camera* cam, const rt_sphere* spheres, uint32_t n,
                     const rt_material* materials, uint32_t m, uint32_t width,
                     uint32_t height, uint32_t x, uint32_t y, uint32_t frame,

@@ -49,11 +49,36 @@ def tan_half(fov):
     return F(math.tan(float(F(fov) / F(2.0))))
 
 
-def camera_consts(cam_floats, width, height):
+RT_FLAG_JITTER, RT_FLAG_THIN_LENS = 0x2, 0x4
+JITTER_MUL, LENS_MUL = np.uint32(0x9E3779B1), np.uint32(0x85EBCA77)
+PI2 = F(F(2.0) * F(3.14159265358979))
+
+
+def sincos(theta):
+    """rt_sincos of the opt-in thin-lens sampling (include/rt_hip.h): the same
+    f32 op sequence as the C oracle and the kernel, written independently."""
+    theta = np.asarray(theta, dtype=np.float32)
+    h = float.fromhex
+    q = np.rint(theta * F(h("0x1.45f306p-1")))
+    r = theta - q * F(h("0x1.92p+0"))
+    r = r - q * F(h("0x1.fb5444p-12"))
+    r = r - q * F(h("0x1.68cp-39"))
+    r2 = r * r
+    sr = r + r * (r2 * (F(h("-0x1.555556p-3")) + r2 * (F(h("0x1.111112p-7")) + r2 * (
+        F(h("-0x1.a01a02p-13")) + r2 * F(h("0x1.71de3ap-19"))))))
+    cr = F(1.0) + r2 * (F(-0.5) + r2 * (F(h("0x1.555556p-5")) + r2 * (F(h("-0x1.6c16c2p-10")) + r2 * (
+        F(h("0x1.a01a02p-16")) + r2 * F(h("-0x1.27e4fcp-22"))))))
+    quad = q.astype(np.int64) & 3
+    s = np.select([quad == 0, quad == 1, quad == 2], [sr, cr, -sr], -cr).astype(np.float32)
+    c = np.select([quad == 0, quad == 1, quad == 2], [cr, -sr, -cr], sr).astype(np.float32)
+    return s, c
+
+
+def camera_consts(cam_floats, width, height, flags=0):
     """cam_floats: the 32 f32 of the 128-B CameraGPU block."""
     c = np.asarray(cam_floats, dtype=np.float32)
     T = c[0:16]
-    fov, ipd, lfl = c[19], c[23], c[27]
+    fov, ipd, lfl, fstop = c[19], c[23], c[27], c[31]
     return dict(
         T=T,
         tan=tan_half(fov),
@@ -61,22 +86,45 @@ def camera_consts(cam_floats, width, height):
         aspect=F(width),
         hw=F(F(width) / F(2.0)),
         hh=F(F(height) / F(2.0)),
+        coc=F(lfl / (F(2.0) * fstop)),
+        flags=flags, W=width, H=height,
     )
 
 
-def primary_rays(cc, xs, ys):
-    """generate.wgsl:66-129 for integer pixel arrays -> origins, dirs (N,3)."""
+def primary_rays(cc, xs, ys, frame=0):
+    """generate.wgsl:66-129 for integer pixel arrays -> origins, dirs (N,3).
+    `frame` (the seed frame) only matters with the opt-in jitter / lens flags."""
     px = xs.astype(np.float32)
     py = ys.astype(np.float32)
+    flags = cc.get("flags", 0)
+    if flags & (RT_FLAG_JITTER | RT_FLAG_THIN_LENS):
+        with np.errstate(over="ignore"):
+            idx = (xs.astype(np.uint32) + np.uint32(cc["W"]) * ys.astype(np.uint32)
+                   + np.uint32(cc["W"] * cc["H"] % (1 << 32)) * np.uint32(frame))
+    if flags & RT_FLAG_JITTER:
+        with np.errstate(over="ignore"):
+            j = hash3(idx * JITTER_MUL)
+        px = px + (j[:, 0] - F(0.5))
+        py = py + (j[:, 1] - F(0.5))
     dx = ((px - cc["hw"]) * cc["tan"]) / cc["aspect"]
     dy = ((-py + cc["hh"]) * cc["tan"]) / cc["aspect"]
     d = np.stack([dx, dy, np.full_like(dx, F(-1.0))], -1)
     d = _normalize(d)
     denom = _dot(d, np.array([0.0, 0.0, -1.0], dtype=np.float32))
     fp = d * (cc["fp"] / denom)[..., None]
-    d = _normalize(fp - F(0.0))
+    origin = np.zeros_like(d)
+    if flags & RT_FLAG_THIN_LENS:
+        with np.errstate(over="ignore"):
+            l = hash3(idx * LENS_MUL)
+        theta = PI2 * l[:, 0] + PI2
+        sr = np.sqrt(l[:, 1])
+        sn, cs = sincos(theta)
+        a, b = (cs * sr) * cc["coc"], (sn * sr) * cc["coc"]
+        origin = np.stack([F(1.0) * a + F(0.0) * b, F(0.0) * a + F(1.0) * b,
+                           F(0.0) * a + F(0.0) * b], -1)
+    d = _normalize(fp - origin)
     T = cc["T"]
-    o = np.zeros_like(d) + T[12:15]
+    o = origin + T[12:15]
     td = np.empty_like(d)
     for r in range(3):
         td[:, r] = ((T[0 + r] * d[:, 0] + T[4 + r] * d[:, 1]) + T[8 + r] * d[:, 2]) + T[12 + r] * F(0.0)
@@ -122,7 +170,7 @@ def intersect(spheres, o, d):
 
 def trace(spheres, mats, cc, width, height, xs, ys, frame, D):
     """One sample (frame) for pixel arrays -> colours (N,3), segment count."""
-    o, d = primary_rays(cc, xs, ys)
+    o, d = primary_rays(cc, xs, ys, frame)
     n = o.shape[0]
     color = np.ones((n, 3), dtype=np.float32)
     with np.errstate(over="ignore"):
@@ -211,7 +259,7 @@ def trace(spheres, mats, cc, width, height, xs, ys, frame, D):
     return color, segs
 
 
-def render(cam_floats, spheres_arr, mats_arr, width, height, spp, D, frame0=0, rows=None):
+def render(cam_floats, spheres_arr, mats_arr, width, height, spp, D, frame0=0, rows=None, flags=0):
     """Render rows (default all) -> (len(rows), W, 4) float32, segments.
 
     spheres_arr: structured array / (N,8) float32 view of the 32-B SphereGPU
@@ -225,7 +273,7 @@ def render(cam_floats, spheres_arr, mats_arr, width, height, spp, D, frame0=0, r
     mi = mt.view(np.int32).reshape(-1, 8) if mt.size else np.zeros((0, 8), np.int32)
     mats = dict(index=sph_mat, color=mf[:, 0:3].copy(), refl=mi[:, 4].copy(), fuzz=mf[:, 5].copy(),
                 ior=mf[:, 6].copy())
-    cc = camera_consts(cam_floats, width, height)
+    cc = camera_consts(cam_floats, width, height, flags)
     rows = list(range(height)) if rows is None else list(rows)
     ys = np.repeat(np.asarray(rows, dtype=np.int64), width)
     xs = np.tile(np.arange(width, dtype=np.int64), len(rows))

@@ -13,7 +13,7 @@ import pytest
 
 from bevy_raytrace_amd import scene
 from bevy_raytrace_amd.abi import MATERIAL_DTYPE, SPHERE_DTYPE
-from bevy_raytrace_amd.camera import default_camera_block
+from bevy_raytrace_amd.camera import Transform, camera_block, default_camera_block
 from oracle import oracle as O
 from oracle import rt_oracle_np as N
 
@@ -199,3 +199,39 @@ def test_golden_fixture(path):
 
 def test_golden_fixtures_present():
     assert len(GOLDEN) >= 4
+
+
+# ------------------------------------------- opt-in camera sampling (§8f row 4)
+def test_sincos_accuracy_and_restatements():
+    """rt_sincos (include/rt_hip.h): C == numpy bit for bit, |err| < 2e-7
+    against the double-precision sin/cos of the same f32 angle."""
+    two_pi = np.float32(2.0) * np.float32(3.14159265358979)
+    th = np.concatenate([np.linspace(two_pi, 2 * two_pi, 4001, dtype=np.float32),
+                         np.linspace(-7.0, 7.0, 2001, dtype=np.float32),
+                         np.float32([0.0, two_pi, 2 * two_pi, 1e-30])])
+    ns, nc = N.sincos(th)
+    for i in range(0, th.size, 7):
+        cs, cc = O.sincos(th[i])
+        assert cs == ns[i] and cc == nc[i], th[i]
+    assert np.abs(ns.astype(np.float64) - np.sin(th.astype(np.float64))).max() < 2e-7
+    assert np.abs(nc.astype(np.float64) - np.cos(th.astype(np.float64))).max() < 2e-7
+
+
+SAMPLING = [("jitter", 0x2), ("thin_lens", 0x4), ("both", 0x6)]
+
+
+@pytest.mark.parametrize("fname,flags", SAMPLING, ids=[s[0] for s in SAMPLING])
+@pytest.mark.parametrize("name,mk", [("config1", scene.config1_scene), ("glass", glass_scene)])
+def test_c_vs_numpy_camera_sampling(fname, flags, name, mk):
+    """Jitter / thin-lens camera sampling: the two restatements agree bit for
+    bit, and the flags change the image (they are not the reference default)."""
+    sp, mt = _scene_arrays(mk())
+    cam = camera_block(Transform.from_xyz(13.0, 2.0, 3.0).looking_at((0.0, 0.0, 0.0)),
+                       lens_focal_length=0.05, fstop=8.0)
+    W, H, S, D, f0 = 36, 20, 3, 8, 2
+    a, sa = O.render(cam, sp, mt, W, H, S, D, frame0=f0, nthreads=4, flags=flags)
+    b, sb = N.render(camf(cam), sp, mt, W, H, S, D, frame0=f0, flags=flags)
+    assert sa == sb
+    assert np.array_equal(a, b, equal_nan=True)
+    base, _ = O.render(cam, sp, mt, W, H, S, D, frame0=f0, nthreads=4)
+    assert not np.array_equal(a, base, equal_nan=True)
