@@ -37,6 +37,10 @@ pub struct rt_stats {
 }
 
 pub const RT_FLAG_NO_PRIMARY_CACHE: u32 = 0x1;
+/// Opt-in camera sampling (rt_hip.h): sub-pixel jitter and thin-lens samples
+/// through the reference's thin_lens_ray (generate.wgsl:85-107).
+pub const RT_FLAG_JITTER: u32 = 0x2;
+pub const RT_FLAG_THIN_LENS: u32 = 0x4;
 
 extern "C" {
     pub fn rt_version() -> c_int;
@@ -50,6 +54,12 @@ extern "C" {
                      out_rgba: *mut f32, stats: *mut rt_stats) -> c_int;
     pub fn rt_render_progressive(ctx: *mut rt_ctx, camera: *const c_void, params: *const rt_params,
                                  reset: c_int, out_rgba: *mut f32, total_spp: *mut u64) -> c_int;
+    // nframes consecutive frames (frame i = samples frame0 + i*spp ...) in one
+    // persistent launch, into device memory; complete with rt_wait
+    pub fn rt_render_frames_device(ctx: *mut rt_ctx, camera: *const c_void, params: *const rt_params,
+                                   nframes: u32, out_rgba_device: *mut f32,
+                                   stream: *mut c_void) -> c_int;
+    pub fn rt_wait(ctx: *mut rt_ctx, stats: *mut rt_stats) -> c_int;
     pub fn rt_intersect(ctx: *mut rt_ctx, rays: *const f32, n: u32, hit_index: *mut i32,
                         hit_t: *mut f32) -> c_int;
     pub fn rt_last_error(ctx: *const rt_ctx) -> *const c_char;
