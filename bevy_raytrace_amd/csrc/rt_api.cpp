@@ -171,6 +171,12 @@ static bool tail_split_enabled() {
     return !(s && s[0] == '0');
 }
 
+static uint32_t env_uint(const char* name, uint32_t dflt) {
+    const char* s = getenv(name);
+    if (!s || !*s) return dflt;
+    return (uint32_t)strtoul(s, nullptr, 10);
+}
+
 static bool env_flag(const char* name, bool dflt) {
     const char* s = getenv(name);
     if (!s || !*s) return dflt;
@@ -560,6 +566,8 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     K_.div_8w = make_fastdiv(8 * p.width);
     K_.div_wrem = make_fastdiv(K_.tile_wrem ? K_.tile_wrem : 1);
     K_.prefetch = env_flag("RT_PREFETCH", true) ? 1u : 0u;
+    K_.prio_mode = env_uint("RT_PRIO", 1);
+    K_.prio_shift = env_uint("RT_PRIO_SHIFT", 14);
     // wide (sphere-parallel) tracing pays ~32 VALU per 64 spheres per ray plus
     // a reduction; the ray-parallel walk ~34 per 8-sphere group per wave plus
     // the drain: switch while k rays cost less sphere-parallel. RT_WIDE_MAX
@@ -575,7 +583,10 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
 
     HIP_TRY(ctx, hipEventRecord(f.ev_t0, stream));
     HIP_TRY(ctx, hipMemsetAsync(f.d_counters, 0, words_pad * sizeof(uint32_t), stream));
-    const uint32_t grid_full = (uint32_t)(ctx->cu_count * ctx->blocks_per_cu);
+    // RT_WG_PER_CU < occupancy: fewer co-resident waves per SIMD (A/B)
+    const uint32_t wg_per_cu = std::min<uint32_t>(env_uint("RT_WG_PER_CU", ctx->blocks_per_cu),
+                                                  ctx->blocks_per_cu);
+    const uint32_t grid_full = (uint32_t)(ctx->cu_count * (wg_per_cu ? wg_per_cu : 1));
     if (npix) HIP_TRY(ctx, rt_launch_primary(&K_, f.d_pd, stream));
     for (size_t i = 0; i < passes.size(); ++i) {
         const Pass& ps = passes[i];

@@ -70,6 +70,8 @@ struct KParams {
     uint32_t tile_wrem;       // width % 8
     FastDiv div_8w, div_wrem;
     uint32_t prefetch;  // 1: waves prefetch their next work chunk (RT_PREFETCH=0 off)
+    uint32_t prio_mode;   // s_setprio rotation (RT_PRIO): 0 off, 1 by iteration, 3 by wall time
+    uint32_t prio_shift;  // mode 3: one step per 2^prio_shift ticks of 10 ns (RT_PRIO_SHIFT)
 };
 
 extern "C" {

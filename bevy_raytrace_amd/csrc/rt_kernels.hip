@@ -805,6 +805,9 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
     // walk instead of stalling the refill. Every prefetched chunk is consumed:
     // a wave only stops after consuming a base >= total, and issues no further
     // prefetch from then on.
+    uint32_t iter = 0;            // loop iterations of this wave (wave-uniform)
+    // hardware wave slot on its SIMD (HW_ID[3:0]): distinct for co-resident waves
+    const uint32_t wave_slot = __builtin_amdgcn_s_getreg((3 << 11) | 4);
     uint32_t pref = 0;            // lane 0: base of the prefetched chunk
     uint32_t pref_chunk = 0;      // its size (0 = none in flight)
 
@@ -860,6 +863,28 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
             need = __ballot(!has_item);
         }
         if (__ballot(has_item) == 0) break;
+        // ---- issue fairness: the SIMD arbiter issues by priority, then age
+        // (MI355X_MICROARCH.md "Two waves per SIMD"), so in a persistent
+        // launch the waves of a SIMD progress at geometrically falling rates
+        // by dispatch order (measured per iteration, 1st..6th wave: 17, 21,
+        // 33, 57, 113, 248 us) and the youngest waves' items become the
+        // launch's stragglers. Mode 1 (default) rotates the priority level
+        // with the wave's iteration count offset by its hardware wave slot
+        // (20, 24, 30, 42, 69, 144 us); mode 3 rotates it by wall time
+        // (s_memrealtime >> prio_shift), all waves of a SIMD stepping together.
+        if (P.prio_mode) {
+            const uint32_t lvl =
+                P.prio_mode == 1
+                    ? (iter + wave_slot) & 3u
+                    : ((uint32_t)(__builtin_amdgcn_s_memrealtime() >> P.prio_shift) + wave_slot) & 3u;
+            switch (lvl) {
+                case 0: __builtin_amdgcn_s_setprio(0); break;
+                case 1: __builtin_amdgcn_s_setprio(1); break;
+                case 2: __builtin_amdgcn_s_setprio(2); break;
+                default: __builtin_amdgcn_s_setprio(3); break;
+            }
+        }
+        ++iter;
 #ifdef RT_WAVE_TRACE
         TR_COUNT(++tr_iters);
         TR_COUNT(tr_after += exhausted ? 1u : 0u);
@@ -949,9 +974,21 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
             (void)tr_t0;
 #endif
             g_wave_trace[wid * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+#ifdef RT_PROFILE  // combined diagnostic build: where the wave ran (HW_ID, XCC_ID)
+            g_wave_trace[wid * 4 + 2] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                                        ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20)
+                                         << 32);
+            (void)tr_ex;
+#else
             g_wave_trace[wid * 4 + 2] = tr_ex;
+#endif
+#ifdef RT_PROFILE  // combined diagnostic build: exact tests (wave max, summed) instead of items
+            g_wave_trace[wid * 4 + 3] = ((unsigned long long)min(prof_.c[13], 0xFFFFFFFFull) << 32) |
+                                        (min(tr_after, 65535u) << 16) | min(tr_iters, 65535u);
+#else
             g_wave_trace[wid * 4 + 3] = ((unsigned long long)tr_items << 32) |
                                         (min(tr_after, 65535u) << 16) | min(tr_iters, 65535u);
+#endif
         }
     }
 #endif

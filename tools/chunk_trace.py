@@ -65,6 +65,9 @@ def trace(F, n=1, k=0, tail=None):
     print(f"   first 1% of queue taken by {t[one]:.0f} us; 50% at {t[(last + 1) // 2]:.0f} us")
 
 
-for F, n, k, tail in [(1, 1, 0, "0,0,12"), (8, 1, 0, "0,0,12"), (1, 1, 0, "0,0,0.001"),
-                      (4, 8, 7, "0,0,12"), (8, 8, 7, "0,0,12")]:
-    trace(F, n, k, tail)
+CASES = [(1, 1, 0), (4, 1, 0), (8, 1, 0), (4, 8, 7), (8, 8, 7), (4, 8, 0), (8, 8, 0)]
+if len(sys.argv) > 1:
+    CASES = [tuple(int(v) for v in c.split(",")) for c in sys.argv[1:]]
+for F, n, k in CASES:
+    for rep in range(2):
+        trace(F, n, k)

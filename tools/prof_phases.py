@@ -1,29 +1,48 @@
-"""Phase breakdown of rt_render_kernel from the -DRT_PROFILE diagnostic build.
-Shares (not absolute times) are meaningful: the stamps perturb the kernel."""
+"""Phase breakdown of rt_render_kernel from the -DRT_PROFILE diagnostic build
+(tools/librt_hip_prof.so), per launch shape / item policy. Shares (not
+absolute times) are meaningful: the stamps perturb the kernel.
+usage: python tools/prof_phases.py [F,n,k,ENV=VAL;...] ..."""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from bevy_raytrace_amd import abi, scene
+import torch
+from bevy_raytrace_amd import abi, configs
 from bevy_raytrace_amd.camera import default_camera_block
 from bevy_raytrace_amd.renderer import Renderer
 
-lib = sys.argv[1] if len(sys.argv) > 1 else "tools/librt_hip_prof.so"
-cam = default_camera_block()
+LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librt_hip_prof.so")
 NAMES = {0: "refill", 1: "filter", 2: "drain", 12: "bookkeep", 3: "shade", 7: "tail"}
-for key, sc, W, H, S, D in [("rtiow1080", scene.rtiow_final_scene(), 1920, 1080, 64, 16),
-                            ("spheres10k", scene.ten_thousand_scene(), 1920, 1080, 8, 16)]:
-    r = Renderer(0, lib_path=lib)
-    sp, mt = sc.objects_gpu(), sc.materials_gpu()
-    r.set_scene(sp, mt)
-    for flags in (abi.RT_FLAG_NO_PRIMARY_CACHE, 0):
-        img, st = r.render(cam, W, H, S, D, flags=flags)
-        c = r.debug_counters()
-        tot = sum(c[i] for i in NAMES)
-        print(f"{key} flags={flags} kernel_ms={st['kernel_ms']:.2f} traced={st['traced_segments']}")
-        print("  phase shares: " + ", ".join(f"{NAMES[i]}={c[i]/tot:.3f}" for i in NAMES))
-        it = max(c[4], 1)
-        print(f"  wave iterations={c[4]} lanes/iter={c[9]/it:.1f} cand-groups/iter={c[5]/it:.1f} "
-              f"of {(len(sp)+7)//8} drain-max/iter={c[6]/it:.2f} flushes/iter={c[11]/it:.3f} "
-              f"wave-cycles total={c[8]} per-iter={c[8]/it:.0f}")
-        print(f"  exact tests per iter: wave-max {c[13]/it:.2f}  wave-max full-path {c[14]/it:.2f}  "
-              f"lane-sum {c[15]/it:.1f} (per lane {c[15]/max(c[9],1):.2f})")
-    r.close()
+wl = configs.WORKLOADS["rtiow1080"]
+sc = wl.make_scene()
+cam = default_camera_block()
+r = Renderer(0, lib_path=LIB)
+r.set_scene(sc.objects_gpu(), sc.materials_gpu())
+W, H, S, D = wl.width, wl.height, wl.spp, wl.max_depth
+nsp = len(sc.objects_gpu())
+buf = torch.empty((8, H, W, 4), dtype=torch.float32, device="cuda:0")
+cases = sys.argv[1:] or ["4,1,0", "4,1,0,RT_SPLIT_ALL=1", "4,8,7", "8,8,7"]
+for case in cases:
+    parts = case.split(",")
+    F, n, k = int(parts[0]), int(parts[1]), int(parts[2])
+    env = dict(p.split("=") for p in parts[3:])
+    old = {e: os.environ.get(e) for e in env}
+    os.environ.update(env)
+    rb = configs.pick_row_block(H, n)
+    for _ in range(2):
+        r.render_frames_device(cam, F, buf.data_ptr(), W, H, S, D, row_block=rb, shard_count=n,
+                               shard_index=k, flags=abi.RT_FLAG_NO_PRIMARY_CACHE)
+        st = r.wait()
+    c = r.debug_counters()
+    for e, v in old.items():
+        if v is None:
+            os.environ.pop(e)
+        else:
+            os.environ[e] = v
+    tot = sum(c[i] for i in NAMES)
+    it = max(c[4], 1)
+    print(f"{case}: kernel {st['kernel_ms']:.2f} ms ({st['kernel_ms'] / F:.2f}/frame), "
+          f"traced {st['traced_segments']}, wave-iters {c[4]}, lanes/iter {c[9] / it:.1f}, "
+          f"wave-cycles/iter {c[8] / it:.0f}", flush=True)
+    print("   shares: " + ", ".join(f"{NAMES[i]}={c[i] / tot:.3f}" for i in NAMES) +
+          f" | cand-groups/iter {c[5] / it:.2f} drain-max/iter {c[6] / it:.2f} "
+          f"exact wave-max {c[13] / it:.2f} full {c[14] / it:.2f} flushes/iter {c[11] / it:.3f}",
+          flush=True)

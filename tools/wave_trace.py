@@ -16,14 +16,14 @@ r = Renderer(0, lib_path=LIB)
 r.lib.rt_debug_wave_trace.restype = ctypes.c_int
 r.set_scene(sc.objects_gpu(), sc.materials_gpu())
 W, H = wl.width, wl.height
-buf = torch.empty((H, W, 4), dtype=torch.float32, device="cuda:0")
+buf = torch.empty((8, H, W, 4), dtype=torch.float32, device="cuda:0")
 MAXW = 32768
 
 
-def trace(S, n=1, k=0, rb=8, D=16):
+def trace(S, n=1, k=0, rb=8, D=16, F=1):
     for _ in range(2):
-        r.render_device(cam, buf.data_ptr(), W, H, S, D, row_block=rb, shard_count=n,
-                        shard_index=k, flags=1)
+        r.render_frames_device(cam, F, buf.data_ptr(), W, H, S, D, row_block=rb, shard_count=n,
+                               shard_index=k, flags=1)
         st = r.wait()
     out = np.zeros(MAXW * 4, dtype=np.uint64)
     r.lib.rt_debug_wave_trace(out.ctypes.data_as(ctypes.c_void_p), MAXW)
@@ -40,7 +40,7 @@ def trace(S, n=1, k=0, rb=8, D=16):
     span = end.max()
     eff = (end - start).sum() / (len(t) * span)
     q = np.percentile(end, [0, 10, 50, 90, 99, 100])
-    print(f"S={S} n={n} k={k}: kernel {st['kernel_ms']:.3f} ms, waves {len(t)}, span {span:.1f} us, "
+    print(f"F={F} S={S} n={n} k={k}: kernel {st['kernel_ms']:.3f} ms, waves {len(t)}, span {span:.1f} us, "
           f"start max {start.max():.1f} us, queue dry at {np.nanmin(ex):.1f} us, "
           f"wave-busy eff {eff:.3f}", flush=True)
     print("   end pct (0/10/50/90/99/100) us: " + " ".join(f"{v:.0f}" for v in q))
@@ -58,6 +58,5 @@ def trace(S, n=1, k=0, rb=8, D=16):
     print("   ends histogram:", hist.tolist())
 
 
-for S in (8, 64):
-    trace(S)
-trace(64, 8, 0, 5)
+for F, n, k in [(4, 8, 7), (8, 8, 7), (8, 8, 7), (4, 1, 0)]:
+    trace(64, n, k, configs.pick_row_block(H, n), F=F)
