@@ -68,7 +68,7 @@ class RtStats(ctypes.Structure):
     _fields_ = [("segments", ctypes.c_uint64), ("traced_segments", ctypes.c_uint64),
                 ("sphere_tests", ctypes.c_uint64), ("paths", ctypes.c_uint64),
                 ("kernel_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
-                ("kernel_launches", ctypes.c_uint32), ("_pad", ctypes.c_uint32)]
+                ("kernel_launches", ctypes.c_uint32), ("short_math", ctypes.c_uint32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_ if not k.startswith("_")}
@@ -167,6 +167,9 @@ def load(path=None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if hasattr(lib, "rt_debug_math"):  # internal diagnostic symbol (tests/test_gpu_math.py)
+        lib.rt_debug_math.restype = ctypes.c_int
+        lib.rt_debug_math.argtypes = [ctypes.c_int, _VP, ctypes.c_uint32, _VP]
     if hasattr(lib, "rt_debug_counters"):  # internal diagnostic symbol
         lib.rt_debug_counters.restype = ctypes.c_int
         lib.rt_debug_counters.argtypes = [_VP, ctypes.POINTER(ctypes.c_uint64)]

@@ -57,6 +57,7 @@ struct Frame {
     hipStream_t pending_stream = nullptr;
     uint32_t passes = 0;
     uint64_t paths = 0;
+    uint32_t short_math = 0;        // KParams.scene_fast of the call
 };
 
 struct rt_ctx {
@@ -67,6 +68,7 @@ struct rt_ctx {
 
     // scene
     bool has_scene = false;
+    bool scene_fast = false;  // scene_fast_ok(): the exact tests may take the short divide/sqrt
     uint32_t n = 0, ngroups = 0, m = 0;
     float4* d_grp = nullptr;        // groups of 4 spheres, SoA (cx[4], cy[4], cz[4], r2[4])
     float4* d_sph = nullptr;        // (cx, cy, cz, r*r)
@@ -287,6 +289,23 @@ static void pack_record(rt_ctx* ctx, uint32_t i, const rt_sphere& s) {
     ctx->h_rm[i] = make_float2(r, mbits);
 }
 
+// The exact sphere test's short correctly-rounded sqrt/divide forms (rt_math.h)
+// need their operands inside [2^-100, 2^100] / [2^-60, 2^60]. The kernel checks
+// the ray side per segment (|origin_i| <= 2^32, |d|^2 in [2^-20, 2^20]); the
+// sphere side is checked here once per scene: |centre_i| <= 2^30 and
+// r^2 in [2^-40, 2^60]. Then |oc|^2 <= 2^68, |half_b| < 2^46, dis < 2^92 and
+// both root numerators < 2^47; and the lower ends need no guard (rt_kernels.hip
+// exact_body). Any other scene keeps the IEEE operations everywhere.
+static bool scene_fast_ok(const rt_ctx* ctx) {
+    for (uint32_t i = 0; i < ctx->n; ++i) {
+        const float4 q = ctx->h_sph[i];
+        if (!(std::fabs(q.x) <= 0x1p30f && std::fabs(q.y) <= 0x1p30f && std::fabs(q.z) <= 0x1p30f))
+            return false;
+        if (!(q.w >= 0x1p-40f && q.w <= 0x1p60f)) return false;
+    }
+    return true;
+}
+
 static void pack_group(rt_ctx* ctx, size_t g) {
     const float4* q = &ctx->h_sph[RT_GROUP * g];
     const float* sg = &ctx->h_S[RT_GROUP * g];
@@ -367,6 +386,7 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n, const rt_mat
     ctx->n = n;
     ctx->ngroups = ngroups;
     ctx->m = m;
+    ctx->scene_fast = scene_fast_ok(ctx);
     ctx->has_scene = true;
     return RT_OK;
 }
@@ -392,6 +412,7 @@ int rt_update_spheres(rt_ctx* ctx, uint32_t first, const rt_sphere* spheres, uin
                            hipMemcpyHostToDevice));
     HIP_TRY(ctx, hipMemcpy(ctx->d_grp + RT_GROUP * g0, &ctx->h_grp[RT_GROUP * g0],
                            sizeof(float4) * RT_GROUP * (g1 - g0), hipMemcpyHostToDevice));
+    ctx->scene_fast = scene_fast_ok(ctx);
     return RT_OK;
 }
 
@@ -548,6 +569,7 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     K_.npix = npix;
     K_.nspheres = ctx->n;
     K_.ngroups = ctx->ngroups;
+    K_.scene_fast = ctx->scene_fast && env_flag("RT_FAST_EXACT", true) ? 1u : 0u;
     K_.flags = p.flags;
     std::memcpy(K_.T, cam->transform, sizeof(K_.T));
     K_.tan_half = (float)std::tan((double)(cam->fov / 2.0f));                 // generate.wgsl:67
@@ -634,6 +656,7 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     HIP_TRY(ctx, hipMemcpyAsync(f.h_segs, f.d_counters, 18 * sizeof(unsigned long long),
                                 hipMemcpyDeviceToHost, stream));
     f.passes = (uint32_t)passes.size();
+    f.short_math = K_.scene_fast;
     f.paths = (uint64_t)npix * p.spp * nframes;
     return RT_OK;
 }
@@ -660,6 +683,7 @@ static int finish(rt_ctx* ctx, Frame& f, rt_stats* st) {
     st->kernel_ms = kms;
     st->total_ms = tms;
     st->kernel_launches = f.passes;
+    st->short_math = f.short_math;
     return RT_OK;
 }
 
@@ -833,7 +857,9 @@ int rt_intersect(rt_ctx* ctx, const float* rays, uint32_t n, int32_t* hit_index,
     char* b = (char*)buf;
     hipError_t e = hipMemcpyAsync(b, rays, rb, hipMemcpyHostToDevice, ctx->stream);
     if (e == hipSuccess)
-        e = rt_launch_intersect(ctx->d_grp, ctx->d_sph, ctx->ngroups, (const float*)b, n,
+        e = rt_launch_intersect(ctx->d_grp, ctx->d_sph, ctx->ngroups,
+                                ctx->scene_fast && env_flag("RT_FAST_EXACT", true) ? 1u : 0u,
+                                (const float*)b, n,
                                 (int*)(b + rb), (float*)(b + rb + ob), ctx->stream);
     if (e == hipSuccess)
         e = hipMemcpyAsync(hit_index, b + rb, ob, hipMemcpyDeviceToHost, ctx->stream);

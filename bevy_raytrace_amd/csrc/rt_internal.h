@@ -57,6 +57,7 @@ struct KParams {
     uint32_t wide_max;
     uint32_t nspheres;
     uint32_t ngroups;      // padded sphere groups of RT_GROUP (see rt_set_scene)
+    uint32_t scene_fast;   // 1: spheres inside the short-math domain (rt_api.cpp scene_fast_ok)
     uint32_t flags;
     float T[16];           // camera transform, column-major
     float tan_half, focus_plane, aspect, half_w, half_h;
@@ -88,7 +89,7 @@ hipError_t rt_launch_assemble(const float4* gathered, uint32_t max_rows, float4*
                               uint32_t width, uint32_t height, uint32_t row_block,
                               uint32_t shard_count, hipStream_t stream);
 hipError_t rt_launch_intersect(const float4* grp, const float4* sph, uint32_t ngroups,
-                               const float* rays, uint32_t n, int* out_i, float* out_t,
+                               uint32_t scene_fast, const float* rays, uint32_t n, int* out_i, float* out_t,
                                hipStream_t stream);
 hipError_t rt_render_occupancy(int* blocks_per_cu);
 hipError_t rt_launch_primary(const KParams* P, float4* pd, hipStream_t stream);

@@ -35,6 +35,21 @@
 #include <stdint.h>
 
 #include "rt_internal.h"
+#include "rt_math.h"
+
+// Wave ballot on a bool straight into the intrinsic: HIP's __ballot(int)
+// round-trips the lane mask through a VGPR (v_cndmask + v_cmp, 2 VALU) when
+// the predicate comes from another block.
+__device__ __forceinline__ uint64_t rt_ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
+// Keeps a rare fallback in its branch: LLVM prices sqrt / fdiv as one IR
+// instruction and speculates them out of the branch (then the backend's
+// 11-17 instruction IEEE expansion runs on every pass, measured). A volatile
+// asm cannot be speculated.
+__device__ __forceinline__ float rt_cold(float x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
 
 #define VERY_FAR 1e20f
 #define EPSILON 0.001f
@@ -62,6 +77,101 @@ __device__ __forceinline__ v3 normalize(v3 a) {
     float l = length(a);
     return mk(a.x / l, a.y / l, a.z / l);
 }
+
+// ---- the hot path's correctly rounded ops (rt_math.h): the short forms on
+// their checked domain; lanes outside it recompute with the plain IEEE op in
+// a branch the wave skips when no lane needs it. The result is the IEEE one
+// in every case (GPU parity tests; rt_debug_math + tests/test_gpu_math.py on
+// zeros, denormals, huge, inf and NaN operands).
+#ifdef RT_FAST_NOGUARD  // measurement only (NOT exact): no IEEE fallback lanes
+#define RT_GUARD_ON 0
+#else
+#define RT_GUARD_ON 1
+#endif
+#if defined(RT_NO_FAST_MATH) || defined(RT_SHADE_IEEE)  // A/B: plain IEEE operations
+__device__ __forceinline__ float sqrt_x(float x) { return sqrtf(x); }
+__device__ __forceinline__ float length_x(v3 a) { return sqrtf(dot(a, a)); }
+__device__ __forceinline__ float div_x(float n, float b, float) { return n / b; }
+__device__ __forceinline__ float recip_or_nan(float b) { return b; }
+__device__ __forceinline__ v3 div3_x(v3 v, float b) { return mk(v.x / b, v.y / b, v.z / b); }
+__device__ __forceinline__ v3 normalize_x(v3 v) { return normalize(v); }
+__device__ __forceinline__ v3 normalize_seed(v3 v) { return normalize(v); }
+#else
+// Each guard's ballot takes a single compare (no && / ||): the compare's lane
+// mask is then the ballot, with no round trip through a VGPR.
+__device__ __forceinline__ float sqrt_x(float x) {
+    float r = rt_sqrt_rn(x);
+    // x outside [2^-100, 2^100] (0, NaN, inf, < 0: IEEE) as one unsigned compare
+    const bool bad = __float_as_uint(x) - 0x0D800000u > 0x71800000u - 0x0D800000u;
+    if (RT_GUARD_ON && rt_ballot(bad) != 0) {
+        if (bad) r = sqrtf(rt_cold(x));
+    }
+    return r;
+}
+__device__ __forceinline__ float length_x(v3 a) { return sqrt_x(dot(a, a)); }
+
+// n / b for a denominator b > 0 with yb = rt_recip_rn(b), or yb = NaN when b
+// is outside rt_recip_rn's domain (every lane then takes the IEEE divide).
+__device__ __forceinline__ float div_x(float n, float b, float yb) {
+    float r = rt_div_rn(n, b, yb);
+    const bool ok = yb == yb && rt_num_ok(n);
+    if (RT_GUARD_ON && rt_ballot(!ok) != 0) {
+        if (!ok) r = n / b;
+    }
+    return r;
+}
+__device__ __forceinline__ float recip_or_nan(float b) {
+    return b > 0.0f && rt_den_ok(b) ? rt_recip_rn(b) : __builtin_nanf("");
+}
+
+// v / b componentwise, any sign of b: short form when b and every component
+// lie within [2^-40, 2^40] in magnitude (no zeros, so the sign rule of
+// rt_div_rn does not arise). The range test runs on the magnitudes' bit
+// patterns (integer min/max: same order as the floats, NaN above inf), so no
+// canonicalising float min/max is needed.
+__device__ __forceinline__ v3 div3_x(v3 v, float b) {
+    const float y = rt_recip_rn(b);
+    v3 r = mk(rt_div_rn(v.x, b, y), rt_div_rn(v.y, b, y), rt_div_rn(v.z, b, y));
+    const uint32_t ax = __float_as_uint(v.x) & 0x7FFFFFFFu, ay = __float_as_uint(v.y) & 0x7FFFFFFFu;
+    const uint32_t az = __float_as_uint(v.z) & 0x7FFFFFFFu, ab = __float_as_uint(b) & 0x7FFFFFFFu;
+    const uint32_t lo = min(min(min(ax, ay), az), ab), hi = max(max(max(ax, ay), az), ab);
+    const bool small = lo < 0x2B800000u /* 2^-40 */, big = hi > 0x53800000u /* 2^40 */;
+    if (RT_GUARD_ON && (rt_ballot(small) | rt_ballot(big)) != 0) {
+        if (small || big) {
+            const float bb = rt_cold(b);
+            r = mk(v.x / bb, v.y / bb, v.z / bb);
+        }
+    }
+    return r;
+}
+
+// normalize(v) = v / sqrt(dot(v, v)): short form when every squared component
+// is at least 2^-80 and dot(v, v) <= 2^80 (false for NaN / inf): then every
+// |v_i| >= 2^-40 (1 - 2^-24), dot(v, v) lies in rt_sqrt_rn's domain, the
+// length l in [2^-40, 2^40] > 0 and every numerator in rt_div_rn's. The
+// squares are dot's own products, so the guard costs a v_min3 and 2 compares.
+__device__ __forceinline__ v3 normalize_x(v3 v) {
+    const float px = v.x * v.x, py = v.y * v.y, pz = v.z * v.z;
+    const float d2 = (px + py) + pz;  // = dot(v, v), same op order
+    const float l = rt_sqrt_rn(d2);
+    const float y = rt_recip_rn(l);
+    v3 r = mk(rt_div_rn(v.x, l, y), rt_div_rn(v.y, l, y), rt_div_rn(v.z, l, y));
+    const bool small = !(fminf(fminf(px, py), pz) >= 0x1p-80f), big = !(d2 <= 0x1p80f);
+    if (RT_GUARD_ON && (rt_ballot(small) | rt_ballot(big)) != 0) {
+        if (small || big) r = normalize(mk(rt_cold(v.x), v.y, v.z));
+    }
+    return r;
+}
+
+// normalize(hash3(n)) needs no guard: hash3's components are k / 2^31 with k
+// odd (shade.wgsl:105-116: n is odd after the first step), so each lies in
+// [2^-31, 1], dot in [3*2^-62, 3] and the length in [2^-31, 2].
+__device__ __forceinline__ v3 normalize_seed(v3 v) {
+    const float l = rt_sqrt_rn(dot(v, v));
+    const float y = rt_recip_rn(l);
+    return mk(rt_div_rn(v.x, l, y), rt_div_rn(v.y, l, y), rt_div_rn(v.z, l, y));
+}
+#endif  // RT_NO_FAST_MATH
 
 // shade.wgsl:105-116
 __device__ __forceinline__ v3 hash3(uint32_t n) {
@@ -205,7 +315,19 @@ __device__ uint32_t g_prof_dummy;
 #define EXACT_ARGS
 #define EXACT_PASS
 #endif
-__device__ __forceinline__ void exact_test(float4 s, int idx, v3 o, v3 d, float a,
+// FAST (wave-uniform, ray_fast below): the short correctly-rounded forms of
+// rt_math.h, unguarded. Their domains hold without per-candidate checks:
+// the scene (rt_api.cpp scene_fast_ok) has |centre_i| <= 2^30 and
+// r^2 in [2^-40, 2^60], the ray |origin_i| <= 2^32 and a in [2^-20, 2^20], so
+// qq < 2^67, |half_b| < 2^44, dis < 2^88 and the numerators < 2^45. Low ends:
+//  - qq < 2^-100 (incl. 0): lo^2 < 2^-99 is below half an ulp of s.w >= 2^-40,
+//    so c = -s.w whichever lo (IEEE or short) the square root returned;
+//  - dis < 2^-100: the IEEE sqrtf (a rare branch; dis < 0 returns as before);
+//  - |numerator| < 2^-60 (incl. +-0): IEEE and short quotients both have
+//    |root| < 2^-40 < EPSILON and are rejected alike.
+// Otherwise the IEEE operations (sqrtf, '/'). ya = rt_recip_rn(a) when FAST.
+template <bool FAST>
+__device__ __forceinline__ void exact_body(float4 s, int idx, v3 o, v3 d, float a, float ya,
                                            float& best_t, int& best_i EXACT_ARGS) {
     EXACT_COUNT(0);
     const v3 oc = mk(o.x - s.x, o.y - s.y, o.z - s.z);
@@ -217,20 +339,51 @@ __device__ __forceinline__ void exact_test(float4 s, int idx, v3 o, v3 d, float 
     // <= 0 < EPSILON, exactly as the full evaluation below would find.
     if (half_b >= 0.0f && qq >= s.w * (1.0f + 0x1p-20f)) return;
     EXACT_COUNT(1);
-    const float lo = sqrtf(qq);
+    const float lo = FAST ? rt_sqrt_rn(qq) : sqrtf(qq);
     const float c = lo * lo - s.w;
     const float dis = half_b * half_b - a * c;
-    if (dis < 0.0f) return;
-    const float sqrtd = sqrtf(dis);
-    float root = (-half_b - sqrtd) / a;
+    float sqrtd;
+    if (FAST) {
+        if (dis < 0x1p-100f) {
+            if (dis < 0.0f) return;
+            sqrtd = sqrtf(rt_cold(dis));
+        } else {
+            sqrtd = rt_sqrt_rn(dis);
+        }
+    } else {
+        if (dis < 0.0f) return;
+        sqrtd = sqrtf(dis);
+    }
+    float root = FAST ? rt_div_rn(-half_b - sqrtd, a, ya) : (-half_b - sqrtd) / a;
     if (root < EPSILON || VERY_FAR < root) {
-        root = (-half_b + sqrtd) / a;
+        root = FAST ? rt_div_rn(-half_b + sqrtd, a, ya) : (-half_b + sqrtd) / a;
         if (root < EPSILON || VERY_FAR < root) return;
     }
     if (root < best_t) {
         best_t = root;
         best_i = idx;
     }
+}
+
+__device__ __forceinline__ void exact_test(float4 s, int idx, v3 o, v3 d, float a, float ya,
+                                           bool fast, float& best_t, int& best_i EXACT_ARGS) {
+    if (fast)
+        exact_body<true>(s, idx, o, d, a, ya, best_t, best_i EXACT_PASS);
+    else
+        exact_body<false>(s, idx, o, d, a, ya, best_t, best_i EXACT_PASS);
+}
+
+// The ray side of the short-math domain (exact_body), for the whole wave.
+__device__ __forceinline__ bool ray_fast(uint32_t scene_fast, v3 o, float a) {
+#ifdef RT_NO_FAST_MATH
+    return false;
+#else
+    // (a NaN origin component makes every exact test of the lane NaN in both
+    // forms: no hit either way)
+    const float om = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+    return scene_fast != 0 && (rt_ballot(!(om <= 0x1p32f)) | rt_ballot(!(a >= 0x1p-20f)) |
+                               rt_ballot(!(a <= 0x1p20f))) == 0;
+#endif
 }
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -347,11 +500,10 @@ __device__ __forceinline__ void filter8(const RayP& R, f2 cxa, f2 cxb, f2 cxc, f
 
 __device__ __forceinline__ uint32_t ge(float h, float t) { return h >= t ? 1u : 0u; }
 
-// Run the exact test for every queued candidate of this lane, in list order.
-// Queue entries are (group << 8 | 8-bit candidate mask), one column per lane.
-__device__ __forceinline__ void drain_candidates(const uint32_t* cq, uint32_t cnt,
-                                                 const float4* __restrict__ sph, v3 o, v3 d,
-                                                 float a, float& best_t, int& best_i EXACT_ARGS) {
+template <bool FAST>
+__device__ __forceinline__ void drain_list(const uint32_t* cq, uint32_t cnt,
+                                           const float4* __restrict__ sph, v3 o, v3 d, float a,
+                                           float ya, float& best_t, int& best_i EXACT_ARGS) {
     const uint32_t lane = __lane_id();
     for (uint32_t k = 0; k < cnt; ++k) {
         const uint32_t e = cq[k * 64 + lane];
@@ -360,9 +512,21 @@ __device__ __forceinline__ void drain_candidates(const uint32_t* cq, uint32_t cn
         while (m) {
             const uint32_t j = __builtin_ctz(m);
             m &= m - 1;
-            exact_test(sph[base + j], (int)(base + j), o, d, a, best_t, best_i EXACT_PASS);
+            exact_body<FAST>(sph[base + j], (int)(base + j), o, d, a, ya, best_t, best_i EXACT_PASS);
         }
     }
+}
+
+// Run the exact test for every queued candidate of this lane, in list order.
+// Queue entries are (group << 8 | 8-bit candidate mask), one column per lane.
+__device__ __forceinline__ void drain_candidates(const uint32_t* cq, uint32_t cnt,
+                                                 const float4* __restrict__ sph, v3 o, v3 d,
+                                                 float a, bool fast, float& best_t,
+                                                 int& best_i EXACT_ARGS) {
+    if (fast)
+        drain_list<true>(cq, cnt, sph, o, d, a, rt_recip_rn(a), best_t, best_i EXACT_PASS);
+    else
+        drain_list<false>(cq, cnt, sph, o, d, a, a, best_t, best_i EXACT_PASS);
 }
 
 // Closest hit over the whole list (intersect.wgsl:133-143).
@@ -377,13 +541,15 @@ __device__ __forceinline__ void drain_candidates(const uint32_t* cq, uint32_t cn
 // Returns the best index (-1 = miss) and t.
 __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
                                                const float4* __restrict__ sph, uint32_t ngroups,
-                                               v3 o, v3 d, float& t_out, uint32_t* cq
+                                               uint32_t scene_fast, v3 o, v3 d, float& t_out,
+                                               uint32_t* cq
 #ifdef RT_PROFILE
                                                , Prof& prof_
 #endif
                                                ) {
-    const float l = sqrtf(dot(d, d));
+    const float l = sqrt_x(dot(d, d));
     const float a = l * l;  // sqr(length(r.dir)), intersect.wgsl:98
+    const bool fast = ray_fast(scene_fast, o, a);
 #if defined(RT_ASM_FILTER) && defined(__HIP_DEVICE_COMPILE__)
     const RayP RP = ray_pack(ray_filter_consts(o, d));
     const float RT_T = RP.r3.y;
@@ -427,11 +593,11 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
         const float hmax = fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(g01.x, g01.y), g23.x), g23.y),
                                                    g45.x), g45.y), g67.x), g67.y);
 #endif
-        if (__ballot(hmax >= RT_T) != 0) {
+        if (rt_ballot(hmax >= RT_T) != 0) {
             PROF_ADD(5, 1);
-            if (__ballot(cnt >= RT_CQ_CAP) != 0) {  // a lane's queue is full: drain all
+            if (rt_ballot(cnt >= RT_CQ_CAP) != 0) {  // a lane's queue is full: drain all
                 PROF_ADD(11, 1);
-                drain_candidates(cq, cnt, sph, o, d, a, best_t, best_i EXACT_PASS);
+                drain_candidates(cq, cnt, sph, o, d, a, fast, best_t, best_i EXACT_PASS);
                 cnt = 0;
             }
             const float T = RT_T;
@@ -448,7 +614,7 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
 #ifdef RT_PROFILE
     PROF_ADD(6, wave_max_u32(cnt));
 #endif
-    drain_candidates(cq, cnt, sph, o, d, a, best_t, best_i EXACT_PASS);
+    drain_candidates(cq, cnt, sph, o, d, a, fast, best_t, best_i EXACT_PASS);
     PROF_MARK(2);
 #ifdef RT_PROFILE
     PROF_ADD(13, wave_max_u32(ecnt[0]));
@@ -471,23 +637,26 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
 // takes the smallest t, ties to the smallest index -- exactly the answer of
 // the sequential strict-`<` scan (intersect.wgsl:133-143).
 __device__ __forceinline__ void intersect_wide(const float4* __restrict__ sph, uint32_t n,
-                                               uint64_t active, v3 o, v3 d, int& hi, float& t) {
+                                               uint32_t scene_fast, uint64_t active, v3 o, v3 d,
+                                               int& hi, float& t) {
     const uint32_t lane = __lane_id();
     while (active) {
         const int src = (int)__builtin_ctzll(active);
         active &= active - 1;
         const v3 ro = mk(__shfl(o.x, src), __shfl(o.y, src), __shfl(o.z, src));
         const v3 rd = mk(__shfl(d.x, src), __shfl(d.y, src), __shfl(d.z, src));
-        const float l = sqrtf(dot(rd, rd));
+        const float l = sqrt_x(dot(rd, rd));
         const float a = l * l;  // sqr(length(r.dir)), intersect.wgsl:98
+        const bool fast = ray_fast(scene_fast, ro, a);
+        const float ya = fast ? rt_recip_rn(a) : a;
         float bt = VERY_FAR;
         int bi = -1;
         for (uint32_t i = lane; i < n; i += 64) {
 #ifdef RT_PROFILE
             uint32_t ecnt[2];
-            exact_test(sph[i], (int)i, ro, rd, a, bt, bi, ecnt);
+            exact_test(sph[i], (int)i, ro, rd, a, ya, fast, bt, bi, ecnt);
 #else
-            exact_test(sph[i], (int)i, ro, rd, a, bt, bi);
+            exact_test(sph[i], (int)i, ro, rd, a, ya, fast, bt, bi);
 #endif
         }
         for (int off = 32; off > 0; off >>= 1) {
@@ -533,7 +702,7 @@ __device__ __forceinline__ void start_sample(const KParams& P, PathState& st) {
     const uint32_t idx = st.x + P.width * st.y + (P.width * P.height) * frame;
     const v3 seed = hash3(idx);
     st.seedx = seed.x;
-    st.nseed = normalize(seed);
+    st.nseed = normalize_seed(seed);
     // (with the opt-in camera sampling the main loop replaces this primary
     // ray before tracing it: one call site for sampled_primary_ray)
     st.o = mk(0.0f + P.T[12], 0.0f + P.T[13], 0.0f + P.T[14]);
@@ -665,7 +834,7 @@ __device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, f
         const uint32_t mi = __float_as_uint(rm.y);
         pos = add(st.o, scale(st.d, t));
         const v3 q = sub(pos, mk(s.x, s.y, s.z));
-        nrm = normalize(mk(q.x / radius, q.y / radius, q.z / radius));
+        nrm = normalize_x(div3_x(q, radius));
         if (dot(st.d, nrm) > 0.0f) {
             nrm = neg(nrm);
             front = false;
@@ -680,7 +849,7 @@ __device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, f
     //      dielectric unit_dir = normalize(d) (shade.wgsl:169)
     v3 un = mk(0.0f, 0.0f, 0.0f);
     if (refl == RT_METALLIC || refl == RT_DIELECTRIC)
-        un = normalize(refl == RT_METALLIC ? reflect(st.d, nrm) : st.d);
+        un = normalize_x(refl == RT_METALLIC ? reflect(st.d, nrm) : st.d);
     // ---- select
     v3 v = st.d;           // vector to normalize (sky: d, shade.wgsl:190)
     bool post = true;      // false: dielectric reflection keeps reflect(d, n) unnormalized
@@ -694,7 +863,7 @@ __device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, f
         float ratio = ior;
         if (front) ratio = 1.0f / ior;
         const float cos_theta = fminf(dot(neg(un), nrm), 1.0f);
-        const float sin_theta = sqrtf(1.0f - cos_theta * cos_theta);
+        const float sin_theta = sqrt_x(1.0f - cos_theta * cos_theta);
         const bool cannot_refract = ratio * sin_theta > 1.0f;
         float r0 = (1.0f - ratio) / (1.0f + ratio);  // reflectance(), shade.wgsl:156-161
         r0 = r0 * r0;
@@ -706,14 +875,14 @@ __device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, f
             post = false;
         } else {  // refract(unit_dir, n, ratio), shade.wgsl:148-153
             const v3 perp = scale(add(un, scale(nrm, cos_theta)), ratio);
-            const float lp = length(perp);
-            const float par = -sqrtf(fabsf(1.0f - (lp * lp)));
+            const float lp = length_x(perp);
+            const float par = -sqrt_x(fabsf(1.0f - (lp * lp)));
             v = add(perp, scale(nrm, par));
         }
     }
     // ---- post-normalize
     v3 vn = mk(0.0f, 0.0f, 0.0f);
-    if (post) vn = normalize(v);
+    if (post) vn = normalize_x(v);
     if (miss) {  // miss(), shade.wgsl:189-197, color *= sky
         const float tt = 0.5f * vn.y + 1.0f;
         const float omt = (1.0f - tt) * 1.0f;
@@ -796,7 +965,7 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
     bool has_item = false;
     uint32_t q_next = 0, q_end = 0;  // wave-uniform chunk of work items
     bool exhausted = false;
-    uint32_t traced = 0, segs = 0;
+    uint32_t traced = 0, segs = 0;  // wave totals (wave-uniform: SGPRs, not a VGPR per lane)
     int cache_hi = -1;      // primary hit of this item's pixel (generate.wgsl: pixel-only ray)
     float cache_t = 0.0f;
     // Chunk prefetch: the atomic for the wave's NEXT chunk is issued as soon as
@@ -813,7 +982,7 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
 
     for (;;) {
         // ---- refill: lanes without an item take the next ones (wave ballot)
-        uint64_t need = __ballot(!has_item);
+        uint64_t need = rt_ballot(!has_item);
         while (need != 0 && !exhausted) {
             if (q_next >= q_end) {
                 // big chunks keep the counter cold; small ones near the end of
@@ -860,9 +1029,9 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
             TR_COUNT(tr_items += min(avail, cnt));
 #endif
             q_next += min(avail, cnt);
-            need = __ballot(!has_item);
+            need = rt_ballot(!has_item);
         }
-        if (__ballot(has_item) == 0) break;
+        if (rt_ballot(has_item) == 0) break;
         // ---- issue fairness: the SIMD arbiter issues by priority, then age
         // (MI355X_MICROARCH.md "Two waves per SIMD"), so in a persistent
         // launch the waves of a SIMD progress at geometrically falling rates
@@ -891,7 +1060,7 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
 #endif
         PROF_MARK(0);
         PROF_ADD(4, 1);
-        PROF_ADD(9, (unsigned long long)__popcll(__ballot(has_item)));
+        PROF_ADD(9, (unsigned long long)__popcll(rt_ballot(has_item)));
 
         // ---- opt-in camera sampling: a lane at bounce 0 holds a fresh sample
         // whose primary ray varies per sample (no primary-hit reuse then)
@@ -904,18 +1073,18 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
         // a ray that needs tracing here.
         int hi = -1;
         float t = VERY_FAR;
-        const uint64_t live = __ballot(has_item);
+        const uint64_t live = rt_ballot(has_item);
         if ((uint32_t)__popcll(live) <= P.wide_max) {  // nearly empty wave: sphere-parallel
-            intersect_wide(sph, P.nspheres, live, st.o, st.d, hi, t);
+            intersect_wide(sph, P.nspheres, P.scene_fast, live, st.o, st.d, hi, t);
         } else if (has_item) {
-            hi = intersect_world(grp, sph, P.ngroups, st.o, st.d, t, cq
+            hi = intersect_world(grp, sph, P.ngroups, P.scene_fast, st.o, st.d, t, cq
 #ifdef RT_PROFILE
                                  , prof_
 #endif
                                  );
         }
+        traced += (uint32_t)__popcll(live);
         if (has_item) {
-            ++traced;
             if (st.bounce == 0) {  // first sample of the block: remember the primary hit
                 cache_hi = hi;
                 cache_t = t;
@@ -925,33 +1094,39 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
         // is reused (result-identical) so the lane goes on to its bounce-1 ray.
         bool shading = has_item;
         PROF_MARK(12);  // bookkeeping between the drain and the shading loop
-        while (shading) {
-            ++segs;
-            const bool done = shade(P, st, hi, t, sph, sph_rm, mats);
-            shading = false;
-            if (done) {
-                // path finished: accumulate (collect.wgsl:115-120, blocked);
-                // a tail item stores every sample's colour for the collect
-                if (st.item & RT_TAIL_ITEM) {
-                    const v3 c = add(mk(0.0f, 0.0f, 0.0f), st.color);
-                    block_sums[P.main_all +
-                               (st.s - P.sample_base - P.g0) * P.npix + (st.item & ~RT_TAIL_ITEM)] =
-                        make_float4(c.x, c.y, c.z, 0.0f);
-                } else {
-                    st.bsum = add(st.bsum, st.color);
-                }
-                ++st.s;
-                if (st.s < st.s_end) {
-                    start_sample(P, st);
-                    if (use_cache) {
-                        hi = cache_hi;
-                        t = cache_t;
-                        shading = true;
+        // uniform loop (the segment count is a wave total): one round per
+        // path step, lanes without a step to shade idle through the round
+        for (;;) {
+            const uint64_t sh = rt_ballot(shading);
+            if (sh == 0) break;
+            segs += (uint32_t)__popcll(sh);
+            if (shading) {
+                const bool done = shade(P, st, hi, t, sph, sph_rm, mats);
+                shading = false;
+                if (done) {
+                    // path finished: accumulate (collect.wgsl:115-120, blocked);
+                    // a tail item stores every sample's colour for the collect
+                    if (st.item & RT_TAIL_ITEM) {
+                        const v3 c = add(mk(0.0f, 0.0f, 0.0f), st.color);
+                        block_sums[P.main_all +
+                                   (st.s - P.sample_base - P.g0) * P.npix + (st.item & ~RT_TAIL_ITEM)] =
+                            make_float4(c.x, c.y, c.z, 0.0f);
+                    } else {
+                        st.bsum = add(st.bsum, st.color);
                     }
-                } else {
-                    if (!(st.item & RT_TAIL_ITEM))
-                        block_sums[st.item] = make_float4(st.bsum.x, st.bsum.y, st.bsum.z, 0.0f);
-                    has_item = false;
+                    ++st.s;
+                    if (st.s < st.s_end) {
+                        start_sample(P, st);
+                        if (use_cache) {
+                            hi = cache_hi;
+                            t = cache_t;
+                            shading = true;
+                        }
+                    } else {
+                        if (!(st.item & RT_TAIL_ITEM))
+                            block_sums[st.item] = make_float4(st.bsum.x, st.bsum.y, st.bsum.z, 0.0f);
+                        has_item = false;
+                    }
                 }
             }
         }
@@ -992,15 +1167,10 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
         }
     }
 #endif
-    // ---- segment counts: wave reduce, one atomic per wave
-    unsigned long long v = segs, w = traced;
-    for (int off = 32; off > 0; off >>= 1) {
-        v += __shfl_xor(v, off);
-        w += __shfl_xor(w, off);
-    }
+    // ---- segment counts: one atomic per wave
     if (lane == 0) {
-        atomicAdd(seg_counter, v);
-        atomicAdd(seg_counter + 1, w);
+        atomicAdd(seg_counter, (unsigned long long)segs);
+        atomicAdd(seg_counter + 1, (unsigned long long)traced);
     }
 }
 
@@ -1027,7 +1197,8 @@ __global__ void rt_primary_kernel(KParams P, PixelEntry* __restrict__ tab) {
 // Batch closest-hit query (rt_intersect): one ray per lane, same intersect_world.
 __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_kernel(
     const float4* __restrict__ grp, const float4* __restrict__ sph, uint32_t ngroups,
-    const float* __restrict__ rays, uint32_t n, int* __restrict__ out_i, float* __restrict__ out_t) {
+    uint32_t scene_fast, const float* __restrict__ rays, uint32_t n, int* __restrict__ out_i,
+    float* __restrict__ out_t) {
     __shared__ uint32_t s_cq[RT_BLOCK_THREADS * RT_CQ_CAP];
     uint32_t* cq = s_cq + (threadIdx.x / 64u) * (64u * RT_CQ_CAP);
 #ifdef RT_PROFILE
@@ -1038,7 +1209,8 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_kernel(
     if (i >= n) return;
     const float* r = rays + (size_t)i * 6;
     float t;
-    const int hi = intersect_world(grp, sph, ngroups, mk(r[0], r[1], r[2]), mk(r[3], r[4], r[5]),
+    const int hi = intersect_world(grp, sph, ngroups, scene_fast, mk(r[0], r[1], r[2]),
+                                   mk(r[3], r[4], r[5]),
                                    t, cq
 #ifdef RT_PROFILE
                                    , prof_
@@ -1194,11 +1366,11 @@ hipError_t rt_launch_assemble(const float4* gathered, uint32_t max_rows, float4*
 }
 
 hipError_t rt_launch_intersect(const float4* grp, const float4* sph, uint32_t ngroups,
-                               const float* rays, uint32_t n, int* out_i, float* out_t,
-                               hipStream_t stream) {
+                               uint32_t scene_fast, const float* rays, uint32_t n, int* out_i,
+                               float* out_t, hipStream_t stream) {
     const uint32_t T = RT_BLOCK_THREADS;
     hipLaunchKernelGGL(rt_intersect_kernel, dim3((n + T - 1) / T), dim3(T), 0, stream, grp, sph,
-                       ngroups, rays, n, out_i, out_t);
+                       ngroups, scene_fast, rays, n, out_i, out_t);
     return hipGetLastError();
 }
 
@@ -1219,6 +1391,37 @@ int rt_debug_chunk_trace(unsigned long long* out, unsigned long long* clk, uint3
     return (int)n;
 }
 #endif
+
+// Diagnostic entry (not part of include/rt_hip.h; tests/test_gpu_math.py):
+// the hot path's guarded short forms on caller-given operands, to compare with
+// the IEEE operations on zeros, denormals, huge values, inf and NaN.
+// mode 0: out[i] = sqrt_x(in[i]); 1: out[3i..3i+2] = normalize_x(in[3i..3i+2]);
+// 2: out[3i..3i+2] = div3_x(in[4i..4i+2], in[4i+3]);
+// 3: out[i] = div_x(in[2i], in[2i+1], recip_or_nan(in[2i+1])).
+__global__ void rt_math_kernel(int mode, const float* __restrict__ in, uint32_t n,
+                               float* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (mode == 0) {
+        out[i] = sqrt_x(in[i]);
+    } else if (mode == 1) {
+        const v3 r = normalize_x(mk(in[3 * i], in[3 * i + 1], in[3 * i + 2]));
+        out[3 * i] = r.x; out[3 * i + 1] = r.y; out[3 * i + 2] = r.z;
+    } else if (mode == 2) {
+        const v3 r = div3_x(mk(in[4 * i], in[4 * i + 1], in[4 * i + 2]), in[4 * i + 3]);
+        out[3 * i] = r.x; out[3 * i + 1] = r.y; out[3 * i + 2] = r.z;
+    } else {
+        out[i] = div_x(in[2 * i], in[2 * i + 1], recip_or_nan(in[2 * i + 1]));
+    }
+}
+
+int rt_debug_math(int mode, const float* in_device, uint32_t n, float* out_device) {
+    if (mode < 0 || mode > 3 || (n && (!in_device || !out_device))) return -1;
+    if (!n) return 0;
+    hipLaunchKernelGGL(rt_math_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, mode, in_device, n,
+                       out_device);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -3;
+}
 
 hipError_t rt_render_occupancy(int* blocks_per_cu) {
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_render_kernel,

@@ -33,7 +33,7 @@ pub struct rt_stats {
     pub kernel_ms: f64,
     pub total_ms: f64,
     pub kernel_launches: u32,
-    pub _pad: u32,
+    pub short_math: u32,
 }
 
 pub const RT_FLAG_NO_PRIMARY_CACHE: u32 = 0x1;

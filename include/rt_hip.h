@@ -160,7 +160,10 @@ typedef struct rt_stats {
     double   kernel_ms;        /* sum of render-kernel durations (HIP events)     */
     double   total_ms;         /* whole call incl. collect / copies               */
     uint32_t kernel_launches;  /* number of render-kernel launches                */
-    uint32_t _pad;
+    uint32_t short_math;       /* 1: the scene lies inside the domain of the exact
+                                  sphere test's short correctly-rounded sqrt and
+                                  divide, which waves whose rays do too then use;
+                                  0: IEEE operations only. Same bits either way. */
 } rt_stats;
 
 typedef struct rt_ctx rt_ctx;

@@ -3,7 +3,8 @@
 Grazing rays pass at distance r(1 + k eps) from sphere centres (the filter's
 decision boundary), surface rays start on / just off a sphere (the t ~ EPSILON
 boundary and self-hits, intersect.wgsl:110), plus far origins, rays from
-inside spheres, unnormalised and degenerate directions."""
+inside spheres (some exactly at the centre), unnormalised and degenerate
+directions."""
 from __future__ import annotations
 
 import numpy as np
@@ -57,7 +58,9 @@ def adversarial_rays(spheres: np.ndarray, n: int, seed: int = 0) -> np.ndarray:
     out.append(np.hstack([o, d]))
     # 6 inside spheres
     i = rng.integers(0, len(r), k)
-    o = c[i] + _unit(rng.normal(size=(k, 3))) * (np.abs(r[i]) * rng.uniform(0, 0.999, k))[:, None]
+    frac = rng.uniform(0, 0.999, k)
+    frac[rng.random(k) < 0.1] = 0.0  # exactly at the centre: |oc|^2 = 0
+    o = c[i] + _unit(rng.normal(size=(k, 3))) * (np.abs(r[i]) * frac)[:, None]
     d = _unit(rng.normal(size=(k, 3)))
     out.append(np.hstack([o, d]))
     # 7 unnormalised directions (|d| 1e-3 .. 1e3)

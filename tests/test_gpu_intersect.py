@@ -14,8 +14,10 @@ from raygen import adversarial_rays
 pytestmark = pytest.mark.gpu
 
 
-def mixed_scene():
-    """Huge + tiny + negative-radius spheres, overlapping and nested."""
+def mixed_scene(zero_radius=True):
+    """Huge + tiny + negative-radius spheres, overlapping and nested. With the
+    zero-radius sphere the scene is outside the short-math domain (r^2 < 2^-40,
+    rt_api.cpp scene_fast_ok) and every exact test takes the IEEE forms."""
     mats = scene.MaterialCache()
     mats.insert("a", scene.RayTraceMaterial((0.5, 0.5, 0.5, 1), scene.Reflectance.Lambertian, 1, 0))
     sp = [scene.Sphere((0, -1000, -1), 1000, 0), scene.Sphere((0, 1, 0), 1, 0),
@@ -23,6 +25,8 @@ def mixed_scene():
           scene.Sphere((3, 0.01, 2), 1e-3, 0), scene.Sphere((-3, 2, 1), 2e-5, 0),
           scene.Sphere((1, 1, 1), 0.0, 0), scene.Sphere((2, 3, -4), 50, 0),
           scene.Sphere((0, 1, 0), 1, 0)]  # duplicate: tie broken by list order
+    if not zero_radius:
+        sp = [x for x in sp if x.radius != 0.0]
     return scene.Scene(sp, mats, "mixed")
 
 
@@ -32,12 +36,18 @@ SCENES = {  # name -> (spheres, translation applied to spheres and rays)
     "spheres10k": lambda: (scene.ten_thousand_scene().objects_gpu(), None),
     "reference": lambda: (scene.reference_scene().objects_gpu(), None),
     "mixed": lambda: (mixed_scene().objects_gpu(), None),
+    "mixed_short_math": lambda: (mixed_scene(zero_radius=False).objects_gpu(), None),
     "far_from_origin": lambda: (scene.rtiow_final_scene().objects_gpu(), FAR),
 }
 
 
+@pytest.mark.parametrize("fast", [True, False], ids=["short_math", "ieee"])
 @pytest.mark.parametrize("name", sorted(SCENES))
-def test_intersect_bit_exact(renderer, name):
+def test_intersect_bit_exact(renderer, name, fast, monkeypatch):
+    """fast=False forces the IEEE exact tests (RT_FAST_EXACT=0): both forms
+    must give the oracle's bits."""
+    if not fast:
+        monkeypatch.setenv("RT_FAST_EXACT", "0")
     sp, off = SCENES[name]()
     from bevy_raytrace_amd.abi import MATERIAL_DTYPE
     mt = np.zeros(int(sp["material"].max()) + 1, dtype=MATERIAL_DTYPE)

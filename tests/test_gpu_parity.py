@@ -491,3 +491,30 @@ def test_camera_sampling_frames_and_shards(renderer):
         ref, _ = O.render(cam, sp, mt, W, H, S, D, frame0=3 + i * S, row_block=B, shard_count=K,
                           shard_index=k, flags=fl)
         check_exact(got[i], ref)
+
+
+@pytest.mark.parametrize("name,mk", [("rtiow", scene.rtiow_final_scene), ("glass", glass_scene)])
+def test_short_math_and_ieee_identical(renderer, monkeypatch, name, mk):
+    """The exact sphere test's short correctly-rounded sqrt/divide (in-domain
+    scenes) and the IEEE forms (RT_FAST_EXACT=0) render the oracle's bits; a
+    zero-radius sphere takes the scene out of the short domain."""
+    sp, mt = arrays(mk())
+    cam = default_camera_block()
+    ref, segs = O.render(cam, sp, mt, 128, 72, 6, 10)
+    renderer.set_scene(sp, mt)
+    img, st = renderer.render(cam, 128, 72, 6, 10)
+    check_exact(img, ref)
+    assert st["segments"] == segs and st["short_math"] == 1
+    monkeypatch.setenv("RT_FAST_EXACT", "0")
+    img, st = renderer.render(cam, 128, 72, 6, 10)
+    check_exact(img, ref)
+    assert st["short_math"] == 0
+    monkeypatch.delenv("RT_FAST_EXACT")
+    sp0 = np.concatenate([sp, sp[:1]])
+    sp0["radius"][-1] = 0.0
+    sp0["center"][-1] = (0.0, 30.0, 0.0)  # out of view; only the domain check changes
+    renderer.set_scene(sp0, mt)
+    img, st = renderer.render(cam, 128, 72, 6, 10)
+    ref0, _ = O.render(cam, sp0, mt, 128, 72, 6, 10)
+    check_exact(img, ref0)
+    assert st["short_math"] == 0
