@@ -62,21 +62,24 @@ def parse():
                     help="every rank on cuda:0 (rehearsal with --dist-backend gloo)")
     ap.add_argument("--check", action="store_true",
                     help="add a checksum of the assembled frames to the JSON line")
-    ap.add_argument("--frames-per-launch", type=int, default=4,
+    ap.add_argument("--frames-per-launch", type=int, default=12,
                     help="frames per persistent launch (rt_render_frames_device)")
     ap.add_argument("--reuse-steps", type=int, default=4,
                     help="extra frames timed with primary-hit reuse on (0 = skip)")
     return ap.parse_args()
 
 
-def load_traffic(workload_key):
-    """HBM bytes per render launch from the committed rocprofv3 PMC summary."""
+def load_traffic(workload_key, frames_per_launch):
+    """HBM bytes per render launch from the committed rocprofv3 PMC summary
+    (measured over one launch of the fixture's frames_per_launch frames; per
+    frame it does not depend on the launch size: block sums and tail samples
+    are per frame), scaled to this run's average launch."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            d = json.load(f)
-        return d.get(workload_key, {}).get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
+            e = json.load(f).get(workload_key, {})
+        return int(e["hbm_bytes_per_launch"] / e["frames_per_launch"] * frames_per_launch)
+    except (OSError, ValueError, KeyError, ZeroDivisionError):
         return None
 
 
@@ -229,7 +232,7 @@ def main():
     # duration (HIP events on the stream the kernel runs on)
     flops_total = traced_local * FLOPS_PER_SPHERE_TEST * nsph
     achieved = flops_total / (kernel_ms_total * 1e-3) / 1e12
-    traffic = load_traffic(wl.key)
+    traffic = load_traffic(wl.key, args.steps / max(1, len(sizes)))
 
     out = {
         "metric": METRIC,

@@ -99,7 +99,14 @@ def shard_rows(height, row_block, shard_count, shard_index):
     """Rows owned by a shard, increasing y (mirror of rt_shard_rows)."""
     B = max(1, int(row_block))
     K = max(1, int(shard_count))
-    return [y for y in range(int(height)) if (y // B) % K == int(shard_index)]
+    return [y for y in range(int(height)) if block_owner(y // B, K) == int(shard_index)]
+
+
+def block_owner(b, K):
+    """Row block b -> owning shard: groups of K blocks dealt serpentine
+    (rt_hip.h rt_params; rt_internal.h rt_block_owner)."""
+    g, i = divmod(int(b), int(K))
+    return K - 1 - i if g & 1 else i
 
 
 _VP = ctypes.c_void_p

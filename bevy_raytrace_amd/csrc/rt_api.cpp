@@ -196,7 +196,8 @@ uint32_t rt_shard_rows(uint32_t height, uint32_t row_block, uint32_t shard_count
     if (shard_index >= shard_count) return 0;
     uint32_t rows = 0;
     const uint32_t nblk = (height + row_block - 1) / row_block;
-    for (uint32_t b = shard_index; b < nblk; b += shard_count) {
+    for (uint32_t b = 0; b < nblk; ++b) {
+        if (rt_block_owner(b, shard_count) != shard_index) continue;
         const uint32_t y0 = b * row_block;
         const uint32_t y1 = y0 + row_block < height ? y0 + row_block : height;
         rows += y1 - y0;

@@ -75,6 +75,16 @@ struct KParams {
     uint32_t prio_shift;  // mode 3: one step per 2^prio_shift ticks of 10 ns (RT_PRIO_SHIFT)
 };
 
+// Row block b of the image -> owning shard (rt_params: serpentine deal).
+__host__ __device__ inline uint32_t rt_block_owner(uint32_t b, uint32_t K) {
+    const uint32_t g = b / K, i = b - g * K;
+    return (g & 1u) ? K - 1u - i : i;
+}
+// j-th block of shard k -> image row block.
+__host__ __device__ inline uint32_t rt_shard_block(uint32_t j, uint32_t K, uint32_t k) {
+    return j * K + ((j & 1u) ? K - 1u - k : k);
+}
+
 extern "C" {
 hipError_t rt_launch_render(const KParams* P, const float4* grp, const float4* sph,
                             const float2* sph_rm, const rt_material* mats, const float4* pd,

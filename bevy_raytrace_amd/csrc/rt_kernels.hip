@@ -716,12 +716,13 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
     return (t + ((n - t) >> f.sh1)) >> f.sh2;
 }
 
-// Shard pixel p -> global (x, y): rows are interleaved blocks of row_block.
+// Shard pixel p -> global (x, y): rows are blocks of row_block dealt
+// serpentine to the shards (rt_block_owner).
 __device__ __forceinline__ void pixel_xy(const KParams& P, uint32_t p, uint32_t& x, uint32_t& y) {
     const uint32_t r = fdiv(p, P.div_width);
     x = p - r * P.width;
     const uint32_t rb = fdiv(r, P.div_row_block);
-    y = (rb * P.shard_count + P.shard_index) * P.row_block + (r - rb * P.row_block);
+    y = rt_shard_block(rb, P.shard_count, P.shard_index) * P.row_block + (r - rb * P.row_block);
 }
 
 // k-th pixel of a block in processing order -> shard-local pixel index
@@ -1309,7 +1310,7 @@ __global__ void rt_assemble_kernel(const float4* __restrict__ gathered, uint32_t
     const uint32_t y = (uint32_t)(i / width);
     const uint32_t x = (uint32_t)(i - (size_t)y * width);
     const uint32_t blk = y / row_block;
-    const uint32_t k = blk % shard_count;
+    const uint32_t k = rt_block_owner(blk, shard_count);
     const uint32_t r = (blk / shard_count) * row_block + (y % row_block);
     image[i] = gathered[((size_t)k * max_rows + r) * width + x];
 }

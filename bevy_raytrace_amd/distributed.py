@@ -3,8 +3,9 @@
 One process per GPU. Every pixel is independent (intersect/shade/collect are
 index-local, intersect.wgsl:153-162, shade.wgsl:207-257, collect.wgsl:116-117;
 the seed depends only on the GLOBAL pixel and frame, shade.wgsl:216-218), so
-the image is split into interleaved blocks of `row_block` rows: rank k owns
-blocks b with b % world == k. Each rank renders its rows into a slab padded to
+the image is split into blocks of `row_block` rows dealt to the ranks in
+groups of `world`, serpentine (abi.block_owner: group g deals to ranks
+0..world-1 when g is even, world-1..0 when odd). Each rank renders its rows into a slab padded to
 `max_rows`; one gather (RCCL over xGMI for backend "nccl", gloo in CPU tests)
 lands the slabs on rank 0, which re-assembles the image (rt_assemble_shards on
 the device; `assemble_host` is the numpy statement of the same mapping).
@@ -16,7 +17,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from .abi import shard_rows
+from .abi import block_owner, shard_rows
 
 
 @dataclass(frozen=True)
@@ -35,7 +36,8 @@ class ShardLayout:
     def source_index(self, y):
         """(rank, local row) holding global row y."""
         blk = y // self.row_block
-        return blk % self.world, (blk // self.world) * self.row_block + y % self.row_block
+        return (block_owner(blk, self.world),
+                (blk // self.world) * self.row_block + y % self.row_block)
 
 
 def assemble_host(gathered: np.ndarray, layout: ShardLayout) -> np.ndarray:

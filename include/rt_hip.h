@@ -95,9 +95,12 @@ typedef struct rt_camera {
  *   frame0        : frame index of sample 0 (the RNG seed input)
  *   row_block, shard_count, shard_index :
  *                   row tiling for multi-GPU. Rows are grouped in blocks of
- *                   row_block rows; shard k owns blocks b with b % shard_count
- *                   == k. The output of a call holds only the owned rows, in
- *                   increasing y, packed. shard_count = 1 -> whole image.
+ *                   row_block rows, dealt to the K = shard_count shards in
+ *                   groups of K, serpentine: in group g = b / K, block b goes
+ *                   to shard b % K (g even) or K-1 - b % K (g odd), so a
+ *                   top-to-bottom cost trend cancels between shards. The
+ *                   output of a call holds only the owned rows, in increasing
+ *                   y, packed. shard_count = 1 -> whole image.
  *   flags         : RT_FLAG_* bits.                                          */
 typedef struct rt_params {
     uint32_t width;

@@ -118,6 +118,12 @@ def trace_path(cam, spheres, materials, width, height, x, y, frame, max_depth):
 RAW_SUMS = 0x80000000
 
 
+def _block_owner(b, K):
+    """Row block -> shard, serpentine (mirror of rto_block_owner)."""
+    g, i = divmod(b, K)
+    return K - 1 - i if g & 1 else i
+
+
 def _params(width, height, spp, max_depth, frame0, row_block, shard_count, shard_index, flags=0):
     p = _Params()
     p.width, p.height, p.spp, p.max_depth = width, height, spp, max_depth
@@ -133,7 +139,8 @@ def render(cam, spheres, materials, width, height, spp, max_depth, frame0=0, row
     cam = np.ascontiguousarray(cam)
     nthreads = nthreads or os.cpu_count() or 1
     B = max(1, row_block)
-    nrows = sum(1 for y in range(height) if (y // B) % shard_count == shard_index)
+    nrows = sum(1 for y in range(height)
+                if _block_owner(y // B, shard_count) == shard_index)
     out = np.zeros((nrows, width, 4), dtype=np.float32)
     segs = ctypes.c_uint64(0)
     p = _params(width, height, spp, max_depth, frame0, row_block, shard_count, shard_index,

@@ -474,6 +474,14 @@ int rto_render_rows(const rt_camera* cam, const rt_sphere* spheres, uint32_t n,
     return 0;
 }
 
+/* Row block b -> owning shard (rt_hip.h rt_params: groups of K blocks dealt
+ * serpentine). The row tiling is this build's own multi-GPU design (the
+ * reference renders on one adapter), so there is no reference line to cite. */
+static uint32_t rto_block_owner(uint32_t b, uint32_t K) {
+    uint32_t g = b / K, i = b % K;
+    return (g & 1u) ? K - 1u - i : i;
+}
+
 int rto_render(const rt_camera* cam, const rt_sphere* spheres, uint32_t n,
                const rt_material* materials, uint32_t m, const rt_params* params,
                float* out_rgba, uint64_t* segments, int nthreads) {
@@ -485,7 +493,7 @@ int rto_render(const rt_camera* cam, const rt_sphere* spheres, uint32_t n,
     uint32_t* rows = (uint32_t*)malloc(sizeof(uint32_t) * (params->height + 1));
     uint32_t nr = 0;
     for (uint32_t y = 0; y < params->height; ++y)
-        if ((y / B) % K == k) rows[nr++] = y;
+        if (rto_block_owner(y / B, K) == k) rows[nr++] = y;
     int rc = rto_render_rows(cam, spheres, n, materials, m, params, rows, nr, out_rgba,
                              segments, nthreads);
     free(rows);

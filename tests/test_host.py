@@ -113,6 +113,21 @@ def test_shard_rows_host(H, B, K):
     assert lib.rt_shard_rows(H, B, K, K) == 0
 
 
+def test_serpentine_block_deal():
+    """Blocks go to shards in groups of K, alternating direction, so every
+    shard's rows sit at the same mean height (up to the last group)."""
+    from bevy_raytrace_amd.distributed import ShardLayout
+    assert [abi.block_owner(b, 4) for b in range(12)] == [0, 1, 2, 3, 3, 2, 1, 0, 0, 1, 2, 3]
+    assert abi.shard_rows(20, 2, 3, 0) == [0, 1, 10, 11, 12, 13]
+    H, B, K = 1080, 5, 8
+    means = [np.mean(abi.shard_rows(H, B, K, k)) for k in range(K)]
+    assert max(means) - min(means) < B * K / 4  # plain b % K would spread them by B*(K-1)
+    lay = ShardLayout(H, B, K)
+    for y in (0, 39, 40, 41, 79, 80, 1079):
+        k, r = lay.source_index(y)
+        assert abi.shard_rows(H, B, K, k)[r] == y
+
+
 def test_null_context_errors_do_not_crash():
     lib = abi.load()
     p = abi.make_params(8, 8, 1, 1)

@@ -1,5 +1,7 @@
 #!/bin/bash
-# One GPU round: smoke -> bench -> rocprofv3 kernel trace of the bench command.
+# One GPU round: smoke -> bench -> rocprofv3 kernel trace of the bench command
+# (warmup = one launch of the timed size, so the rocprof average per render
+# launch is the timed launch's duration).
 set -euo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
@@ -12,6 +14,6 @@ timeout -k 10 400 python bench.py --config spheres10k1080 --steps 2 --warmup 1 -
     --reuse-steps 0 --frames-per-launch 2 > gpurun_out/bench_10k.json 2>> gpurun_out/bench.err
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv \
-    -- python3 "$R/bench.py" --no-cpu-baseline --reuse-steps 0 \
+    -- python3 "$R/bench.py" --no-cpu-baseline --reuse-steps 0 --warmup 12 \
     > "$R/gpurun_out/prof.log" 2>&1
 echo done

@@ -1,14 +1,14 @@
 #!/bin/bash
 # PMC passes over the headline bench command (one counter group per rocprofv3
 # run, --kernel-trace only; no sys/runtime trace with --pmc), each pass under
-# its own time limit. The command renders exactly one 4-frame launch
-# (--steps 4 --warmup 0), so every rt_render_kernel dispatch is the same
-# launch the bench line reports. Output under gpurun_out/pmc_*;
+# its own time limit. The command renders exactly one 12-frame launch
+# (--steps 12 --warmup 0), the launch the default bench line reports. Output under gpurun_out/pmc_*;
 # tools/pmc_summary.py turns it into profiles/.
 set -uo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd /tmp && export TMPDIR=/tmp
-CMD="python3 $R/bench.py --steps 4 --warmup 0 --frames-per-launch 4 --no-cpu-baseline --reuse-steps 0"
+FPL=${FPL:-12}
+CMD="python3 $R/bench.py --steps $FPL --warmup 0 --frames-per-launch $FPL --no-cpu-baseline --reuse-steps 0"
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS" \
            "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \

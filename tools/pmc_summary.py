@@ -11,6 +11,7 @@ root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 out_dir = sys.argv[1] if len(sys.argv) > 1 else os.path.join(root, "gpurun_out")
 tag = sys.argv[2] if len(sys.argv) > 2 else "r01"
 wl = sys.argv[3] if len(sys.argv) > 3 else "rtiow1080"
+fpl = int(sys.argv[4]) if len(sys.argv) > 4 else 12
 
 vals = defaultdict(lambda: defaultdict(list))   # kernel -> counter -> per-dispatch values
 durs = defaultdict(list)
@@ -35,7 +36,7 @@ for f in glob.glob(os.path.join(out_dir, "pmc_*", "**", "*kernel_trace.csv"), re
 mean = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in vals.items()}
 rk = mean.get("rt_render_kernel", {})
 summary = {"command": "tools/pmc_round.sh: rocprofv3 --kernel-trace --pmc <group> -- python3 bench.py "
-                      "--steps 4 --warmup 0 --frames-per-launch 4 --no-cpu-baseline --reuse-steps 0",
+                      f"--steps {fpl} --warmup 0 --frames-per-launch {fpl} --no-cpu-baseline --reuse-steps 0",
            "per_dispatch_mean": mean,
            "render_kernel_ms_under_pmc": (sum(durs["rt_render_kernel"]) / len(durs["rt_render_kernel"])
                                           if durs["rt_render_kernel"] else None)}
@@ -51,10 +52,10 @@ if "FETCH_SIZE" in rk and "WRITE_SIZE" in rk:
     tp = os.path.join(root, "profiles", "pmc_traffic.json")
     d = json.load(open(tp)) if os.path.exists(tp) else {}
     d[wl] = {"hbm_bytes_per_launch": int(fetch + write), "fetch_bytes": int(fetch),
-             "write_bytes": int(write), "frames_per_launch": 4,
+             "write_bytes": int(write), "frames_per_launch": fpl,
              "source": f"profiles/{tag}_pmc_{wl}.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
                        "separate passes; FETCH_SIZE x2 per gfx950 correction, x1024 KB->B)",
-             "note": "per 4-frame render launch: block-sum / tail-sample writes dominate; "
+             "note": f"per {fpl}-frame render launch: block-sum / tail-sample writes dominate; "
                      "the sphere list is cache-resident"}
     json.dump(d, open(tp, "w"), indent=1)
 print(json.dumps({k: summary[k] for k in summary if k != "per_dispatch_mean"}, indent=1))

@@ -13,7 +13,8 @@ cam = default_camera_block()
 r = Renderer(0)
 r.set_scene(sc.objects_gpu(), sc.materials_gpu())
 W, H, S, D = wl.width, wl.height, wl.spp, wl.max_depth
-buf = torch.empty((8, H, W, 4), dtype=torch.float32, device="cuda:0")
+FS = [int(x) for x in os.environ.get("PROBE_F", "4,8").split(",")]
+buf = torch.empty((max(FS), H, W, 4), dtype=torch.float32, device="cuda:0")
 
 
 def per_frame(F, n=1, k=0, reps=2):
@@ -34,9 +35,9 @@ for rep in range(2):
         env = dict(p.split("=") for p in setting.split(";") if p)
         saved = {e: os.environ.get(e) for e in env}
         os.environ.update(env)
-        for F in (4, 8):
+        for F in FS:
             full = per_frame(F)
-            sh = [per_frame(F, 8, k) for k in (0, 3, 7)]
+            sh = [per_frame(F, 8, k) for k in range(8)]
             print(f"[{setting or 'default'}] F={F}: full {full:.3f} ms/frame | N=8 shards "
                   f"{' '.join('%.3f' % t for t in sh)} -> pred {full / max(sh):.2f}x, "
                   f"vs full@default-ish {23.5 / max(sh):.2f}x", flush=True)
