@@ -206,6 +206,14 @@ def main():
     if world > 1:
         dist.all_reduce(tot)
     segs_all, traced_all = float(tot[0].item()), float(tot[1].item())
+    per_rank = None
+    if world > 1:  # load balance of the row tiling: each rank's render-kernel time
+        mine = torch.tensor([float(sum(kms)), float(segs_local)], dtype=torch.float64,
+                            device=red_dev)
+        parts = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(parts, mine)
+        per_rank = {"kernel_ms": [round(float(p[0].item()), 3) for p in parts],
+                    "segments": [int(p[1].item()) for p in parts]}
 
     reuse = None
     if args.reuse_steps > 0:
@@ -265,6 +273,8 @@ def main():
         "traced_segments_per_frame": int(traced_all / args.steps),
         "primary_reuse": reuse,
     }
+    if per_rank is not None:
+        out["ranks"] = per_rank
 
     if args.check:
         import hashlib
