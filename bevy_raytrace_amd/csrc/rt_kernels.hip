@@ -500,6 +500,39 @@ __device__ __forceinline__ void filter8(const RayP& R, f2 cxa, f2 cxb, f2 cxc, f
 
 __device__ __forceinline__ uint32_t ge(float h, float t) { return h >= t ? 1u : 0u; }
 
+#if defined(RT_ASM_FILTER) && defined(__HIP_DEVICE_COMPILE__)
+// The lane's 8-bit candidate mask (bit j = H_j >= T, the same compares as
+// ge()): the 8 compares go to 8 SGPR lane masks, then m = 2m + c_j shifts
+// them in with v_addc (carry-in = the lane's bit of c_j), sphere 7 first --
+// 16 VALU instead of 8 compares + 8 v_cndmask + 4 ORs, and every mask is
+// read 7+ instructions after its compare wrote it (no VALU-SGPR wait states).
+__device__ __forceinline__ uint32_t cand_mask8(f2 g01, f2 g23, f2 g45, f2 g67, float T) {
+    uint32_t m;
+    uint64_t c0, c1, c2, c3, c4, c5, c6, c7;
+    asm("v_cmp_ge_f32_e64 %[c7], %[h7], %[T]\n"
+        "v_cmp_ge_f32_e64 %[c6], %[h6], %[T]\n"
+        "v_cmp_ge_f32_e64 %[c5], %[h5], %[T]\n"
+        "v_cmp_ge_f32_e64 %[c4], %[h4], %[T]\n"
+        "v_cmp_ge_f32_e64 %[c3], %[h3], %[T]\n"
+        "v_cmp_ge_f32_e64 %[c2], %[h2], %[T]\n"
+        "v_cmp_ge_f32_e64 %[c1], %[h1], %[T]\n"
+        "v_cmp_ge_f32_e64 %[c0], %[h0], %[T]\n"
+        "v_cndmask_b32_e64 %[m], 0, 1, %[c7]\n"
+        "v_addc_co_u32_e64 %[m], %[c7], %[m], %[m], %[c6]\n"
+        "v_addc_co_u32_e64 %[m], %[c6], %[m], %[m], %[c5]\n"
+        "v_addc_co_u32_e64 %[m], %[c5], %[m], %[m], %[c4]\n"
+        "v_addc_co_u32_e64 %[m], %[c4], %[m], %[m], %[c3]\n"
+        "v_addc_co_u32_e64 %[m], %[c3], %[m], %[m], %[c2]\n"
+        "v_addc_co_u32_e64 %[m], %[c2], %[m], %[m], %[c1]\n"
+        "v_addc_co_u32_e64 %[m], %[c1], %[m], %[m], %[c0]\n"
+        : [m] "=&v"(m), [c0] "=&s"(c0), [c1] "=&s"(c1), [c2] "=&s"(c2), [c3] "=&s"(c3),
+          [c4] "=&s"(c4), [c5] "=&s"(c5), [c6] "=&s"(c6), [c7] "=&s"(c7)
+        : [h0] "v"(g01.x), [h1] "v"(g01.y), [h2] "v"(g23.x), [h3] "v"(g23.y),
+          [h4] "v"(g45.x), [h5] "v"(g45.y), [h6] "v"(g67.x), [h7] "v"(g67.y), [T] "v"(T));
+    return m;
+}
+#endif
+
 template <bool FAST>
 __device__ __forceinline__ void drain_list(const uint32_t* cq, uint32_t cnt,
                                            const float4* __restrict__ sph, v3 o, v3 d, float a,
@@ -601,9 +634,13 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
                 cnt = 0;
             }
             const float T = RT_T;
+#if defined(RT_ASM_FILTER) && defined(__HIP_DEVICE_COMPILE__)
+            const uint32_t m = cand_mask8(g01, g23, g45, g67, T);
+#else
             const uint32_t m = ge(g01.x, T) | (ge(g01.y, T) << 1) | (ge(g23.x, T) << 2) |
                                (ge(g23.y, T) << 3) | (ge(g45.x, T) << 4) | (ge(g45.y, T) << 5) |
                                (ge(g67.x, T) << 6) | (ge(g67.y, T) << 7);
+#endif
             if (m) {
                 cq[cnt * 64 + lane] = (g << 8) | m;
                 ++cnt;
