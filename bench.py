@@ -8,7 +8,8 @@ through the persistent HIP kernel, depth 16, written to an HBM image. Inputs
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config rtiow1080]
 
 N > 1 is launched by torch.distributed.run (one process per GPU): the image
-is row-tiled in interleaved blocks, each rank renders its rows,
+is row-tiled in blocks dealt serpentine to the ranks, each rank
+renders its rows,
 then one RCCL gather over xGMI lands the shards on rank 0, which re-assembles
 the image on the device. Timing: barrier + synchronize around exactly K steps,
 max over ranks. value = algorithmic ray segments of the whole frame (all ranks)
