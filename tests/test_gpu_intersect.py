@@ -31,6 +31,8 @@ def mixed_scene(zero_radius=True):
 
 
 FAR = (1e4, -3e3, 2e4)
+EDGE_IN = (2.0 ** 30 - 2048.0, 0.0, 0.0)
+EDGE_OUT = (2.0 ** 31, 0.0, 0.0)
 SCENES = {  # name -> (spheres, translation applied to spheres and rays)
     "rtiow": lambda: (scene.rtiow_final_scene().objects_gpu(), None),
     "spheres10k": lambda: (scene.ten_thousand_scene().objects_gpu(), None),
@@ -38,6 +40,10 @@ SCENES = {  # name -> (spheres, translation applied to spheres and rays)
     "mixed": lambda: (mixed_scene().objects_gpu(), None),
     "mixed_short_math": lambda: (mixed_scene(zero_radius=False).objects_gpu(), None),
     "far_from_origin": lambda: (scene.rtiow_final_scene().objects_gpu(), FAR),
+    # centres just inside / outside the short-math scene domain |c| <= 2^30
+    # (rt_api.cpp scene_fast_ok): the same rays either way, fast vs IEEE path
+    "edge_of_short_domain": lambda: (scene.rtiow_final_scene().objects_gpu(), EDGE_IN),
+    "beyond_short_domain": lambda: (scene.rtiow_final_scene().objects_gpu(), EDGE_OUT),
 }
 
 
