@@ -1,4 +1,4 @@
-"""N>1 path on CPU: world_size-2 gloo run of the row tiling + gather +
+"""N>1 path on CPU: world_size-2/3/8 gloo runs of the row tiling + gather +
 re-assembly that bench.py drives over RCCL. Each rank's shard is rendered by
 the oracle (the checker; on the GPU box the same code path takes rt_render
 output), gathered to rank 0 with torch.distributed.gather, re-assembled and
@@ -37,7 +37,7 @@ def _worker(rank, world, port, B, q):
         cam = default_camera_block()
         lay = ShardLayout(H, B, world)
         part, segs = O.render(cam, sp, mt, W, H, S, D, row_block=B, shard_count=world,
-                              shard_index=rank, nthreads=2)
+                              shard_index=rank, nthreads=1)
         slab = torch.zeros((lay.max_rows, W, 4), dtype=torch.float32)
         slab[:part.shape[0]] = torch.from_numpy(part)
         g = gather_to_root(dist, slab, world, rank)
@@ -50,8 +50,10 @@ def _worker(rank, world, port, B, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("B", [1, 4])
-def test_gloo_world2_row_tiling(B):
+@pytest.mark.parametrize("world,B", [(2, 1), (2, 4), (3, 2), (8, 1)])
+def test_gloo_row_tiling(world, B):
+    """world 8 rehearses the driver's N=8 layout (21 rows: uneven shards,
+    padded slabs, serpentine deal over 3 groups)."""
     import torch.multiprocessing as mp
 
     from bevy_raytrace_amd import scene
@@ -61,7 +63,7 @@ def test_gloo_world2_row_tiling(B):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, B, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, B, q)) for r in range(world)]
     for p in procs:
         p.start()
     img, segs = q.get(timeout=120)
