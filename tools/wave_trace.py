@@ -16,7 +16,9 @@ r = Renderer(0, lib_path=LIB)
 r.lib.rt_debug_wave_trace.restype = ctypes.c_int
 r.set_scene(sc.objects_gpu(), sc.materials_gpu())
 W, H = wl.width, wl.height
-buf = torch.empty((8, H, W, 4), dtype=torch.float32, device="cuda:0")
+CASES = [tuple(int(v) for v in c.split(",")) for c in
+         os.environ.get("TRACE_CASES", "4,8,7;8,8,7;8,8,7;4,1,0").split(";")]
+buf = torch.empty((max(c[0] for c in CASES), H, W, 4), dtype=torch.float32, device="cuda:0")
 MAXW = 32768
 
 
@@ -58,5 +60,5 @@ def trace(S, n=1, k=0, rb=8, D=16, F=1):
     print("   ends histogram:", hist.tolist())
 
 
-for F, n, k in [(4, 8, 7), (8, 8, 7), (8, 8, 7), (4, 1, 0)]:
+for F, n, k in CASES:
     trace(64, n, k, configs.pick_row_block(H, n), F=F)
