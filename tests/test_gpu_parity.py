@@ -518,3 +518,29 @@ def test_short_math_and_ieee_identical(renderer, monkeypatch, name, mk):
     ref0, _ = O.render(cam, sp0, mt, 128, 72, 6, 10)
     check_exact(img, ref0)
     assert st["short_math"] == 0
+
+
+def stacked_scene():
+    """200 coincident spheres (every ray through them has 200 candidates: the
+    per-lane queue flushes every 8 groups, and equal roots are broken by list
+    order) around a glass and a metal sphere, over the ground."""
+    mats = scene.MaterialCache()
+    mats.insert("ground", scene.RayTraceMaterial((0.5, 0.5, 0.5, 1), scene.Reflectance.Lambertian, 1.0, 0))
+    mats.insert("a", scene.RayTraceMaterial((0.9, 0.2, 0.2, 1), scene.Reflectance.Lambertian, 1.0, 0))
+    mats.insert("b", scene.RayTraceMaterial((0.2, 0.9, 0.2, 1), scene.Reflectance.Metallic, 0.2, 0))
+    mats.insert("glass", scene.RayTraceMaterial((1, 1, 1, 1), scene.Reflectance.Dielectric, 0.0, 1.5))
+    sp = [scene.Sphere((0, -1000, -1), 1000, 0)]
+    sp += [scene.Sphere((0, 1, 0), 1, 1 + (i % 2)) for i in range(200)]  # ties: first wins
+    sp += [scene.Sphere((-2.2, 1, 0.5), 1, 3), scene.Sphere((2.2, 1, -0.5), 1, 2)]
+    return scene.Scene(sp, mats, "stacked")
+
+
+@pytest.mark.parametrize("flags", [0, NO_REUSE], ids=["reuse", "noreuse"])
+def test_coincident_spheres_queue_flushes(renderer, flags):
+    sp, mt = arrays(stacked_scene())
+    cam = default_camera_block()
+    renderer.set_scene(sp, mt)
+    img, st = renderer.render(cam, 96, 54, 5, 10, frame0=2, flags=flags)
+    ref, segs = O.render(cam, sp, mt, 96, 54, 5, 10, frame0=2)
+    check_exact(img, ref)
+    assert st["segments"] == segs
