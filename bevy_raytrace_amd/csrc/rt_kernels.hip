@@ -7,29 +7,33 @@
 // exchanged through HBM between stages: each lane keeps its whole path state
 // (ray, throughput, seed, sample-block sum) in VGPRs.
 //
-// Work decomposition: an *item* is (pixel, sample block of RT_SAMPLE_BLOCK
-// samples). Items are dealt to lanes from a global counter in chunks of 64 per
-// wave; a lane whose path ends starts the next sample of its block, and a lane
-// whose block ends writes the block sum and takes the next item (wave-ballot
-// refill), so lanes do not idle while the wave's longest path finishes.
+// Work decomposition: a launch covers F frames; its work
+// queue holds (frame, pixel, sample block of RT_SAMPLE_BLOCK samples) *block
+// items* followed by single-sample *tail items* (so no lane holds a long item
+// when the queue runs dry). Waves take chunks of items with one atomic
+// (prefetched a chunk ahead); a lane whose path ends starts the next sample of
+// its item, a lane whose item ends stores its block sum (or, for a tail item,
+// each sample's colour) and takes the next item (wave-ballot refill), so lanes
+// do not idle while the wave's longest path finishes. rt_collect_kernel folds
+// a pixel's slots in sample order -- the oracle's summation order.
 //
 // Intersection (the hot loop, intersect.wgsl:133-143): every sphere of the
-// list is tested for every live ray (brute force, list order). The sphere
-// records (cx, cy, cz, r^2) are wave-uniform, so they are read with scalar
-// loads (s_load_dwordx4 through the scalar cache) and fed to v_fma_f32 as SGPR
-// operands: no LDS or VGPR traffic per sphere. Each test is a conservative
-// FMA-form filter (11 VALU ops + 1 compare; see DESIGN.md "Exact filter"):
-//   G = (oc.dn)^2 + r^2 - (1 - 2^-16) |oc|^2,  dn = d/|d|
-// G < 0 proves the reference's discriminant (intersect.wgsl:102) is negative,
-// so the sphere cannot hit. Only the rare candidates (G >= 0) are re-evaluated
-// with the reference's exact op sequence (intersect.wgsl:97-115), in list
-// order, with the strict `<` tie-break (:137). The result is therefore
-// bit-identical to the brute-force reference loop.
+// list is tested for every live ray (brute force). The list is read as groups
+// of 8 spheres (SoA cx[8] cy[8] cz[8] S[8]) with scalar loads and fed to
+// hand-scheduled v_pk_fma_f32 as SGPR pairs (filter8: 28 packed FMAs + a
+// v_max3 chain + 1 compare per group):
+//   H - T = hb^2 + r^2 - (1 - m)|o - c|^2 + mu (|o|^2 + |c|^2),  hb = dn.(o - c)
+// H < T proves the reference's discriminant (intersect.wgsl:102) is negative.
+// Lanes queue their candidate groups (group, 8-bit mask) in LDS; after the
+// walk each lane runs the reference's exact op sequence (intersect.wgsl:
+// 97-115) on its own candidates in list order with the strict `<` tie-break
+// (:137), so the result is bit-identical to the brute-force reference loop.
 //
 // Floating point: compiled with -ffp-contract=off; every expression below
-// except the explicit __builtin_fmaf calls of the filter is one IEEE f32
-// round-to-nearest op, with correctly rounded div / sqrt (hipcc default), in
-// the same order as oracle/rt_oracle.c.
+// except the explicit FMAs of the filter is one IEEE f32 round-to-nearest op
+// in the same order as oracle/rt_oracle.c. Divides and square roots are
+// correctly rounded: the short forms of rt_math.h where their domain is
+// proved (exact test) or checked per lane (shading), IEEE otherwise.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
