@@ -70,7 +70,7 @@ struct rt_ctx {
     bool has_scene = false;
     bool scene_fast = false;  // scene_fast_ok(): the exact tests may take the short divide/sqrt
     uint32_t n = 0, ngroups = 0, m = 0;
-    float4* d_grp = nullptr;        // groups of 4 spheres, SoA (cx[4], cy[4], cz[4], r2[4])
+    float4* d_grp = nullptr;        // groups of RT_GROUP=8 spheres, SoA (cx[8], cy[8], cz[8], S[8])
     float4* d_sph = nullptr;        // (cx, cy, cz, r*r)
     float2* d_sph_rm = nullptr;     // (radius, material bits)
     rt_material* d_mats = nullptr;

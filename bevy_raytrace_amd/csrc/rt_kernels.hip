@@ -423,10 +423,10 @@ __device__ __forceinline__ RayF ray_filter_consts(v3 o, v3 d) {
     return r;
 }
 
-// Filter two spheres at once: 9 packed fp32 ops (v_pk_fma/mul/add_f32 -- the
-// only way to the 157.3 TF fp32 peak on gfx950, tools/ubench/fma_rate.hip).
-// Returns H = hb^2 + S + o2.c; G' = H + K, so "G' >= 0" is "H >= T" with the
-// per-ray threshold T = -K (an exact comparison). 7 packed ops per sphere pair.
+// Filter two spheres at once: 7 packed fp32 FMAs (v_pk_fma_f32: two f32 FMAs
+// per lane per issue, tools/ubench/fma_rate.hip). Returns H = hb^2 + S + o2.c;
+// the sphere is a candidate iff H >= T, the ray's threshold (an exact
+// comparison). The C++ form of filter8 (builds without RT_ASM_FILTER).
 __device__ __forceinline__ f2 filter2(f2 cx, f2 cy, f2 cz, f2 S, const RayF& r) {
     // every op has ONE SGPR-pair operand (sphere data) -- the constant-bus limit
     const f2 hb = pk_fma(r.dz, cz, pk_fma(r.dy, cy, pk_fma(r.dx, cx, r.k1)));  // k1 - dn.c
