@@ -295,7 +295,7 @@ static void pack_record(rt_ctx* ctx, uint32_t i, const rt_sphere& s) {
 // the ray side per segment (|origin_i| <= 2^32, |d|^2 in [2^-20, 2^20]); the
 // sphere side is checked here once per scene: |centre_i| <= 2^30 and
 // r^2 in [2^-40, 2^60]. Then |oc|^2 <= 2^68, |half_b| < 2^46, dis < 2^92 and
-// both root numerators < 2^47; and the lower ends need no guard (rt_kernels.hip
+// both root numerators < 2^47; and the lower ends need no guard (rt_dev_intersect.h
 // exact_body). Any other scene keeps the IEEE operations everywhere.
 static bool scene_fast_ok(const rt_ctx* ctx) {
     for (uint32_t i = 0; i < ctx->n; ++i) {

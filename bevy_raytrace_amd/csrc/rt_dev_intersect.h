@@ -1,0 +1,450 @@
+// rt_dev_intersect.h -- closest hit: the exact reference test, the packed
+// conservative filter (filter8), candidate queues, intersect_world / intersect_wide
+// (intersect.wgsl:94-143)
+// (included by rt_kernels.hip only: one translation unit, device code)
+#pragma once
+
+namespace {
+
+// ---- diagnostic build only (-DRT_PROFILE): per-wave phase clocks (s_memtime)
+// and wave-level event counts, summed into a debug buffer. Never compiled into
+// the product library.
+#ifdef RT_PROFILE
+struct Prof {
+    unsigned long long c[16];
+    unsigned long long last;
+};
+#define PROF_DECL Prof prof_ = {};
+#define PROF_START() (prof_.last = __builtin_amdgcn_s_memtime())
+#define PROF_MARK(i)                                            \
+    do {                                                        \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        prof_.c[i] += t_ - prof_.last;                          \
+        prof_.last = t_;                                        \
+    } while (0)
+#define PROF_ADD(i, v) (prof_.c[i] += (v))
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off));
+    return v;
+}
+#else
+#define PROF_DECL
+#define PROF_START()
+#define PROF_MARK(i)
+#define PROF_ADD(i, v)
+#endif
+
+// Exact reference test of one sphere (intersect.wgsl:97-115 + :137).
+// s.w = RN(radius*radius) = sqr(s.radius); r2p = s.w * (1 + 2^-20).
+#ifdef RT_PROFILE
+__device__ uint32_t g_prof_dummy;
+#define EXACT_COUNT(k) (ecnt[k]++)
+#define EXACT_ARGS , uint32_t* ecnt
+#define EXACT_PASS , ecnt
+#else
+#define EXACT_COUNT(k)
+#define EXACT_ARGS
+#define EXACT_PASS
+#endif
+// FAST (wave-uniform, ray_fast below): the short correctly-rounded forms of
+// rt_math.h, unguarded. Their domains hold without per-candidate checks:
+// the scene (rt_api.cpp scene_fast_ok) has |centre_i| <= 2^30 and
+// r^2 in [2^-40, 2^60], the ray |origin_i| <= 2^32 and a in [2^-20, 2^20], so
+// qq < 2^67, |half_b| < 2^44, dis < 2^88 and the numerators < 2^45. Low ends:
+//  - qq < 2^-100 (incl. 0): lo^2 < 2^-99 is below half an ulp of s.w >= 2^-40,
+//    so c = -s.w whichever lo (IEEE or short) the square root returned;
+//  - dis < 2^-100: the IEEE sqrtf (a rare branch; dis < 0 returns as before);
+//  - |numerator| < 2^-60 (incl. +-0): IEEE and short quotients both have
+//    |root| < 2^-40 < EPSILON and are rejected alike.
+// Otherwise the IEEE operations (sqrtf, '/'). ya = rt_recip_rn(a) when FAST.
+template <bool FAST>
+__device__ __forceinline__ void exact_body(float4 s, int idx, v3 o, v3 d, float a, float ya,
+                                           float& best_t, int& best_i EXACT_ARGS) {
+    EXACT_COUNT(0);
+    const v3 oc = mk(o.x - s.x, o.y - s.y, o.z - s.z);
+    const float half_b = dot(oc, d);
+    const float qq = dot(oc, oc);
+    // Cheap certain-miss: centre behind the origin (half_b >= 0) and origin
+    // outside (qq >= r^2 (1 + 2^-20) => c >= 0 after the sqrt/square round
+    // trip). Then dis <= half_b^2, sqrt(dis) <= half_b, and both roots are
+    // <= 0 < EPSILON, exactly as the full evaluation below would find.
+    if (half_b >= 0.0f && qq >= s.w * (1.0f + 0x1p-20f)) return;
+    EXACT_COUNT(1);
+    const float lo = FAST ? rt_sqrt_rn(qq) : sqrtf(qq);
+    const float c = lo * lo - s.w;
+    const float dis = half_b * half_b - a * c;
+    float sqrtd;
+    if (FAST) {
+        if (dis < 0x1p-100f) {
+            if (dis < 0.0f) return;
+            sqrtd = sqrtf(rt_cold(dis));
+        } else {
+            sqrtd = rt_sqrt_rn(dis);
+        }
+    } else {
+        if (dis < 0.0f) return;
+        sqrtd = sqrtf(dis);
+    }
+    float root = FAST ? rt_div_rn(-half_b - sqrtd, a, ya) : (-half_b - sqrtd) / a;
+    if (root < EPSILON || VERY_FAR < root) {
+        root = FAST ? rt_div_rn(-half_b + sqrtd, a, ya) : (-half_b + sqrtd) / a;
+        if (root < EPSILON || VERY_FAR < root) return;
+    }
+    if (root < best_t) {
+        best_t = root;
+        best_i = idx;
+    }
+}
+
+__device__ __forceinline__ void exact_test(float4 s, int idx, v3 o, v3 d, float a, float ya,
+                                           bool fast, float& best_t, int& best_i EXACT_ARGS) {
+    if (fast)
+        exact_body<true>(s, idx, o, d, a, ya, best_t, best_i EXACT_PASS);
+    else
+        exact_body<false>(s, idx, o, d, a, ya, best_t, best_i EXACT_PASS);
+}
+
+// The ray side of the short-math domain (exact_body), for the whole wave.
+__device__ __forceinline__ bool ray_fast(uint32_t scene_fast, v3 o, float a) {
+#ifdef RT_NO_FAST_MATH
+    return false;
+#else
+    // (a NaN origin component makes every exact test of the lane NaN in both
+    // forms: no hit either way)
+    const float om = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+    return scene_fast != 0 && (rt_ballot(!(om <= 0x1p32f)) | rt_ballot(!(a >= 0x1p-20f)) |
+                               rt_ballot(!(a <= 0x1p20f))) == 0;
+#endif
+}
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(4))) const float4 cfloat4;  // scalar-cache reads
+
+__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 bc(float x) { return f2{x, x}; }
+
+// Per-ray constants of the expanded-form filter (see file header / DESIGN.md):
+//   G' = (k1 - dn.c)^2 + S + K + o2.c
+//      = hb^2 + r^2 - (1 - m) |o - c|^2 + mu (|o|^2 + |c|^2)
+// with hb = dn.(o - c), dn ~ d/|d|, S = r^2 - (1 - m - mu)|c|^2 (per sphere,
+// host), k1 = dn.o, K = -(1 - m - mu)|o|^2, o2 = 2(1 - m) o (per ray).
+// m = 2^-16 bounds the exact path's rounding relative to |o - c|^2 + r^2,
+// mu = 2^-17 the expanded form's cancellation relative to |o|^2 + |c|^2.
+struct RayF {
+    f2 dx, dy, dz, o2x, o2y, o2z, k1;  // dx,dy,dz hold -dn
+    float T;                           // candidate threshold -K
+};
+
+__device__ __forceinline__ RayF ray_filter_consts(v3 o, v3 d) {
+    const float rs = __builtin_amdgcn_rsqf(dot(d, d));  // approximate 1/|d| (covered by m)
+    const float dnx = d.x * rs, dny = d.y * rs, dnz = d.z * rs;
+    const float m = 0x1p-16f, mu = 0x1p-17f;
+    const float oo = __builtin_fmaf(o.z, o.z, __builtin_fmaf(o.y, o.y, o.x * o.x));
+    const float k1 = __builtin_fmaf(dnz, o.z, __builtin_fmaf(dny, o.y, dnx * o.x));
+    const float two = 2.0f * (1.0f - m);
+    RayF r;
+    r.dx = bc(-dnx); r.dy = bc(-dny); r.dz = bc(-dnz);  // negated: hb = k1 + (-dn).c
+    r.o2x = bc(two * o.x); r.o2y = bc(two * o.y); r.o2z = bc(two * o.z);
+    r.k1 = bc(k1);
+    r.T = (1.0f - m - mu) * oo;
+    return r;
+}
+
+// Filter two spheres at once: 7 packed fp32 FMAs (v_pk_fma_f32: two f32 FMAs
+// per lane per issue, tools/ubench/fma_rate.hip). Returns H = hb^2 + S + o2.c;
+// the sphere is a candidate iff H >= T, the ray's threshold (an exact
+// comparison). The C++ form of filter8 (builds without RT_ASM_FILTER).
+__device__ __forceinline__ f2 filter2(f2 cx, f2 cy, f2 cz, f2 S, const RayF& r) {
+    // every op has ONE SGPR-pair operand (sphere data) -- the constant-bus limit
+    const f2 hb = pk_fma(r.dz, cz, pk_fma(r.dy, cy, pk_fma(r.dx, cx, r.k1)));  // k1 - dn.c
+    return pk_fma(r.o2x, cx, pk_fma(r.o2y, cy, pk_fma(r.o2z, cz, pk_fma(hb, hb, S))));
+}
+
+// The same filter for a whole group of 8 spheres in hand-scheduled VOP3P:
+// the ray constants live ONCE in 4 VGPR pairs (r0 = (-dnx, -dny),
+// r1 = (-dnz, k1), r2 = (o2x, o2y), r3 = (o2z, T)) and op_sel / op_sel_hi
+// broadcast one half to both packed lanes -- the compiler's form needs every
+// constant duplicated in a pair (7 VGPRs more at the 80-VGPR occupancy limit).
+// The four pair chains are interleaved, so dependent ops are 4 apart (no
+// wait states, and a lone wave in the queue tail issues back to back). Op
+// order per pair is exactly filter2's.
+struct RayP {
+    f2 r0, r1, r2, r3;
+};
+
+__device__ __forceinline__ RayP ray_pack(const RayF& r) {
+    RayP p;
+    p.r0 = f2{r.dx.x, r.dy.x};
+    p.r1 = f2{r.dz.x, r.k1.x};
+    p.r2 = f2{r.o2x.x, r.o2y.x};
+    p.r3 = f2{r.o2z.x, r.T};
+    return p;
+}
+
+__device__ __forceinline__ void filter8(const RayP& R, f2 cxa, f2 cxb, f2 cxc, f2 cxd, f2 cya,
+                                        f2 cyb, f2 cyc, f2 cyd, f2 cza, f2 czb, f2 czc, f2 czd,
+                                        f2 sa, f2 sb, f2 sc, f2 sd, f2& ha, f2& hb, f2& hc,
+                                        f2& hd, float& hmax) {
+    asm volatile(
+        // hb = k1 + (-dnx) cx + (-dny) cy + (-dnz) cz
+        "v_pk_fma_f32 %[ha], %[r0], %[cxa], %[r1] op_sel:[0,0,1] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[hb], %[r0], %[cxb], %[r1] op_sel:[0,0,1] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[hc], %[r0], %[cxc], %[r1] op_sel:[0,0,1] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[hd], %[r0], %[cxd], %[r1] op_sel:[0,0,1] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[ha], %[r0], %[cya], %[ha] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[hb], %[r0], %[cyb], %[hb] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[hc], %[r0], %[cyc], %[hc] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[hd], %[r0], %[cyd], %[hd] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[ha], %[r1], %[cza], %[ha] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[hb], %[r1], %[czb], %[hb] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[hc], %[r1], %[czc], %[hc] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[hd], %[r1], %[czd], %[hd] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        // H = hb^2 + S + o2z cz + o2y cy + o2x cx
+        "v_pk_fma_f32 %[ha], %[ha], %[ha], %[sa]\n\t"
+        "v_pk_fma_f32 %[hb], %[hb], %[hb], %[sb]\n\t"
+        "v_pk_fma_f32 %[hc], %[hc], %[hc], %[sc]\n\t"
+        "v_pk_fma_f32 %[hd], %[hd], %[hd], %[sd]\n\t"
+        "v_pk_fma_f32 %[ha], %[r3], %[cza], %[ha] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[hb], %[r3], %[czb], %[hb] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[hc], %[r3], %[czc], %[hc] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[hd], %[r3], %[czd], %[hd] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[ha], %[r2], %[cya], %[ha] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[hb], %[r2], %[cyb], %[hb] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[hc], %[r2], %[cyc], %[hc] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[hd], %[r2], %[cyd], %[hd] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[ha], %[r2], %[cxa], %[ha] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[hb], %[r2], %[cxb], %[hb] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[hc], %[r2], %[cxc], %[hc] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[hd], %[r2], %[cxd], %[hd] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        // group max of the 8 H (v_max3 drops a quiet-NaN operand, as fmaxf)
+        "v_max3_f32 %[hm], v40, v41, v42\n\t"
+        "v_max3_f32 %[hm], %[hm], v43, v44\n\t"
+        "v_max3_f32 %[hm], %[hm], v45, v46\n\t"
+        "v_max_f32 %[hm], %[hm], v47"
+        : [ha] "={v[40:41]}"(ha), [hb] "={v[42:43]}"(hb), [hc] "={v[44:45]}"(hc),
+          [hd] "={v[46:47]}"(hd), [hm] "=&v"(hmax)
+        : [r0] "v"(R.r0), [r1] "v"(R.r1), [r2] "v"(R.r2), [r3] "v"(R.r3), [cxa] "s"(cxa),
+          [cxb] "s"(cxb), [cxc] "s"(cxc), [cxd] "s"(cxd), [cya] "s"(cya), [cyb] "s"(cyb),
+          [cyc] "s"(cyc), [cyd] "s"(cyd), [cza] "s"(cza), [czb] "s"(czb), [czc] "s"(czc),
+          [czd] "s"(czd), [sa] "s"(sa), [sb] "s"(sb), [sc] "s"(sc), [sd] "s"(sd));
+}
+
+__device__ __forceinline__ uint32_t ge(float h, float t) { return h >= t ? 1u : 0u; }
+
+#if defined(RT_ASM_FILTER) && defined(__HIP_DEVICE_COMPILE__)
+// The lane's 8-bit candidate mask (bit j = H_j >= T, the same compares as
+// ge()): the 8 compares go to 8 SGPR lane masks, then m = 2m + c_j shifts
+// them in with v_addc (carry-in = the lane's bit of c_j), sphere 7 first --
+// 16 VALU instead of 8 compares + 8 v_cndmask + 4 ORs, and every mask is
+// read 7+ instructions after its compare wrote it (no VALU-SGPR wait states).
+__device__ __forceinline__ uint32_t cand_mask8(f2 g01, f2 g23, f2 g45, f2 g67, float T) {
+    uint32_t m;
+    uint64_t c0, c1, c2, c3, c4, c5, c6, c7;
+    asm("v_cmp_ge_f32_e64 %[c7], %[h7], %[T]\n"
+        "v_cmp_ge_f32_e64 %[c6], %[h6], %[T]\n"
+        "v_cmp_ge_f32_e64 %[c5], %[h5], %[T]\n"
+        "v_cmp_ge_f32_e64 %[c4], %[h4], %[T]\n"
+        "v_cmp_ge_f32_e64 %[c3], %[h3], %[T]\n"
+        "v_cmp_ge_f32_e64 %[c2], %[h2], %[T]\n"
+        "v_cmp_ge_f32_e64 %[c1], %[h1], %[T]\n"
+        "v_cmp_ge_f32_e64 %[c0], %[h0], %[T]\n"
+        "v_cndmask_b32_e64 %[m], 0, 1, %[c7]\n"
+        "v_addc_co_u32_e64 %[m], %[c7], %[m], %[m], %[c6]\n"
+        "v_addc_co_u32_e64 %[m], %[c6], %[m], %[m], %[c5]\n"
+        "v_addc_co_u32_e64 %[m], %[c5], %[m], %[m], %[c4]\n"
+        "v_addc_co_u32_e64 %[m], %[c4], %[m], %[m], %[c3]\n"
+        "v_addc_co_u32_e64 %[m], %[c3], %[m], %[m], %[c2]\n"
+        "v_addc_co_u32_e64 %[m], %[c2], %[m], %[m], %[c1]\n"
+        "v_addc_co_u32_e64 %[m], %[c1], %[m], %[m], %[c0]\n"
+        : [m] "=&v"(m), [c0] "=&s"(c0), [c1] "=&s"(c1), [c2] "=&s"(c2), [c3] "=&s"(c3),
+          [c4] "=&s"(c4), [c5] "=&s"(c5), [c6] "=&s"(c6), [c7] "=&s"(c7)
+        : [h0] "v"(g01.x), [h1] "v"(g01.y), [h2] "v"(g23.x), [h3] "v"(g23.y),
+          [h4] "v"(g45.x), [h5] "v"(g45.y), [h6] "v"(g67.x), [h7] "v"(g67.y), [T] "v"(T));
+    return m;
+}
+#endif
+
+template <bool FAST>
+__device__ __forceinline__ void drain_list(const uint32_t* cq, uint32_t cnt,
+                                           const float4* __restrict__ sph, v3 o, v3 d, float a,
+                                           float ya, float& best_t, int& best_i EXACT_ARGS) {
+    const uint32_t lane = __lane_id();
+    for (uint32_t k = 0; k < cnt; ++k) {
+        const uint32_t e = cq[k * 64 + lane];
+        uint32_t m = e & 0xFFu;
+        const uint32_t base = (e >> 8) * RT_GROUP;
+        while (m) {
+            const uint32_t j = __builtin_ctz(m);
+            m &= m - 1;
+            exact_body<FAST>(sph[base + j], (int)(base + j), o, d, a, ya, best_t, best_i EXACT_PASS);
+        }
+    }
+}
+
+// Run the exact test for every queued candidate of this lane, in list order.
+// Queue entries are (group << 8 | 8-bit candidate mask), one column per lane.
+__device__ __forceinline__ void drain_candidates(const uint32_t* cq, uint32_t cnt,
+                                                 const float4* __restrict__ sph, v3 o, v3 d,
+                                                 float a, bool fast, float& best_t,
+                                                 int& best_i EXACT_ARGS) {
+    if (fast)
+        drain_list<true>(cq, cnt, sph, o, d, a, rt_recip_rn(a), best_t, best_i EXACT_PASS);
+    else
+        drain_list<false>(cq, cnt, sph, o, d, a, a, best_t, best_i EXACT_PASS);
+}
+
+// Closest hit over the whole list (intersect.wgsl:133-143).
+// grp: the sphere list as groups of RT_GROUP=8, SoA (cx[8], cy[8], cz[8], S[8]),
+// padded to whole groups with pad records of S = -inf (never candidates).
+// Wave-uniform: read with s_load_dwordx16 and fed to the packed ops as SGPR
+// pairs. sph: the padded records AoS (cx, cy, cz, r2), gathered per lane by
+// the exact tests. Pass 1 filters every sphere and queues candidates per lane
+// (LDS, cq); the group test is max(H) >= T over the 8 spheres. Pass 2 (drain)
+// runs the exact reference test on the queued candidates in list order, so the
+// wave pays for max-over-lanes candidates, not for their union.
+// Returns the best index (-1 = miss) and t.
+__device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
+                                               const float4* __restrict__ sph, uint32_t ngroups,
+                                               uint32_t scene_fast, v3 o, v3 d, float& t_out,
+                                               uint32_t* cq
+#ifdef RT_PROFILE
+                                               , Prof& prof_
+#endif
+                                               ) {
+    const float l = sqrt_x(dot(d, d));
+    const float a = l * l;  // sqr(length(r.dir)), intersect.wgsl:98
+    const bool fast = ray_fast(scene_fast, o, a);
+#if defined(RT_ASM_FILTER) && defined(__HIP_DEVICE_COMPILE__)
+    const RayP RP = ray_pack(ray_filter_consts(o, d));
+    const float RT_T = RP.r3.y;
+#else
+    const RayF R = ray_filter_consts(o, d);
+    const float RT_T = R.T;
+#endif
+    const uint32_t lane = __lane_id();
+    float best_t = VERY_FAR;
+    int best_i = -1;
+    uint32_t cnt = 0;
+#ifdef RT_PROFILE
+    uint32_t ecnt[2] = {0, 0};
+#endif
+    // constant address space: the groups are read with s_load into SGPRs
+    // whatever the alias analysis concludes about other stores
+#if defined(__HIP_DEVICE_COMPILE__)
+    const cfloat4* gp = (const cfloat4*)(uintptr_t)grp;
+#else
+    const float4* gp = grp;  // host pass: never executed
+#endif
+    for (uint32_t g = 0; g < ngroups; ++g) {
+        const auto* p = gp + (size_t)g * 8;
+        const float4 X0 = p[0], X1 = p[1], Y0 = p[2], Y1 = p[3];
+        const float4 Z0 = p[4], Z1 = p[5], S0 = p[6], S1 = p[7];
+#if defined(RT_ASM_FILTER) && defined(__HIP_DEVICE_COMPILE__)
+        f2 g01, g23, g45, g67;
+        float hmax;
+        filter8(RP, f2{X0.x, X0.y}, f2{X0.z, X0.w}, f2{X1.x, X1.y}, f2{X1.z, X1.w},
+                f2{Y0.x, Y0.y}, f2{Y0.z, Y0.w}, f2{Y1.x, Y1.y}, f2{Y1.z, Y1.w},
+                f2{Z0.x, Z0.y}, f2{Z0.z, Z0.w}, f2{Z1.x, Z1.y}, f2{Z1.z, Z1.w},
+                f2{S0.x, S0.y}, f2{S0.z, S0.w}, f2{S1.x, S1.y}, f2{S1.z, S1.w}, g01, g23, g45, g67,
+                hmax);
+#else
+        // group test below: max of the 8 H (v_max3 chain; a NaN H is dropped
+        // by max -- a NaN H never hits) against the ray's threshold
+        const f2 g01 = filter2(f2{X0.x, X0.y}, f2{Y0.x, Y0.y}, f2{Z0.x, Z0.y}, f2{S0.x, S0.y}, R);
+        const f2 g23 = filter2(f2{X0.z, X0.w}, f2{Y0.z, Y0.w}, f2{Z0.z, Z0.w}, f2{S0.z, S0.w}, R);
+        const f2 g45 = filter2(f2{X1.x, X1.y}, f2{Y1.x, Y1.y}, f2{Z1.x, Z1.y}, f2{S1.x, S1.y}, R);
+        const f2 g67 = filter2(f2{X1.z, X1.w}, f2{Y1.z, Y1.w}, f2{Z1.z, Z1.w}, f2{S1.z, S1.w}, R);
+        const float hmax = fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(g01.x, g01.y), g23.x), g23.y),
+                                                   g45.x), g45.y), g67.x), g67.y);
+#endif
+        if (rt_ballot(hmax >= RT_T) != 0) {
+            PROF_ADD(5, 1);
+            if (rt_ballot(cnt >= RT_CQ_CAP) != 0) {  // a lane's queue is full: drain all
+                PROF_ADD(11, 1);
+                drain_candidates(cq, cnt, sph, o, d, a, fast, best_t, best_i EXACT_PASS);
+                cnt = 0;
+            }
+            const float T = RT_T;
+#if defined(RT_ASM_FILTER) && defined(__HIP_DEVICE_COMPILE__)
+            const uint32_t m = cand_mask8(g01, g23, g45, g67, T);
+#else
+            const uint32_t m = ge(g01.x, T) | (ge(g01.y, T) << 1) | (ge(g23.x, T) << 2) |
+                               (ge(g23.y, T) << 3) | (ge(g45.x, T) << 4) | (ge(g45.y, T) << 5) |
+                               (ge(g67.x, T) << 6) | (ge(g67.y, T) << 7);
+#endif
+            if (m) {
+                cq[cnt * 64 + lane] = (g << 8) | m;
+                ++cnt;
+            }
+        }
+    }
+    PROF_MARK(1);
+#ifdef RT_PROFILE
+    PROF_ADD(6, wave_max_u32(cnt));
+#endif
+    drain_candidates(cq, cnt, sph, o, d, a, fast, best_t, best_i EXACT_PASS);
+    PROF_MARK(2);
+#ifdef RT_PROFILE
+    PROF_ADD(13, wave_max_u32(ecnt[0]));
+    PROF_ADD(14, wave_max_u32(ecnt[1]));
+    {
+        uint32_t sum0 = ecnt[0];
+        for (int off = 32; off > 0; off >>= 1) sum0 += __shfl_xor(sum0, off);
+        PROF_ADD(15, sum0);
+    }
+#endif
+    t_out = best_t;
+    return best_i;
+}
+
+// Sphere-parallel closest hit for the few live rays of a nearly empty wave
+// (the end of the work queue, where a wave's remaining paths would otherwise
+// each pay the whole ray-parallel list walk): one ray at a time, the 64 lanes
+// split the list and run the exact reference test (intersect.wgsl:97-115) on
+// their spheres in list order with the strict `<`; the wave reduction then
+// takes the smallest t, ties to the smallest index -- exactly the answer of
+// the sequential strict-`<` scan (intersect.wgsl:133-143).
+__device__ __forceinline__ void intersect_wide(const float4* __restrict__ sph, uint32_t n,
+                                               uint32_t scene_fast, uint64_t active, v3 o, v3 d,
+                                               int& hi, float& t) {
+    const uint32_t lane = __lane_id();
+    while (active) {
+        const int src = (int)__builtin_ctzll(active);
+        active &= active - 1;
+        const v3 ro = mk(__shfl(o.x, src), __shfl(o.y, src), __shfl(o.z, src));
+        const v3 rd = mk(__shfl(d.x, src), __shfl(d.y, src), __shfl(d.z, src));
+        const float l = sqrt_x(dot(rd, rd));
+        const float a = l * l;  // sqr(length(r.dir)), intersect.wgsl:98
+        const bool fast = ray_fast(scene_fast, ro, a);
+        const float ya = fast ? rt_recip_rn(a) : a;
+        float bt = VERY_FAR;
+        int bi = -1;
+        for (uint32_t i = lane; i < n; i += 64) {
+#ifdef RT_PROFILE
+            uint32_t ecnt[2];
+            exact_test(sph[i], (int)i, ro, rd, a, ya, fast, bt, bi, ecnt);
+#else
+            exact_test(sph[i], (int)i, ro, rd, a, ya, fast, bt, bi);
+#endif
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            const float ot = __shfl_xor(bt, off);
+            const int oi = __shfl_xor(bi, off);
+            if (ot < bt || (ot == bt && (uint32_t)oi < (uint32_t)bi)) {
+                bt = ot;
+                bi = oi;
+            }
+        }
+        if ((int)lane == src) {
+            hi = bi;
+            t = bt;
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t lanemask_lt_count(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+
+}  // namespace

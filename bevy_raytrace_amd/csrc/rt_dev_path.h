@@ -1,0 +1,226 @@
+// rt_dev_path.h -- lane path state, work items and shading (shade.wgsl:105-258)
+// (included by rt_kernels.hip only: one translation unit, device code)
+#pragma once
+
+// Lane state of one in-flight path.
+struct PathState {
+    v3 o, d;            // current ray
+    v3 pd;              // primary direction of this pixel (generate.wgsl: pixel-only)
+    v3 color;           // throughput (intersection.color, clear.wgsl:86)
+    v3 bsum;            // sum of finished samples of the current block
+    v3 nseed;           // normalize(seed)
+    float seedx;        // seed.x (dielectric Schlick test)
+    uint32_t x, y;      // global pixel
+    uint32_t item;      // work item = (block - block_begin) * npix + pixel
+    uint32_t s, s_end;  // current sample, end of the block
+    uint32_t bounce;
+};
+
+// New sample s of the lane's pixel: seed (shade.wgsl:216-218), primary ray
+// (generate.wgsl:109-129; origin = camera translation, direction cached per
+// item since it depends on the pixel only), throughput 1 (clear.wgsl:86).
+__device__ __forceinline__ void start_sample(const KParams& P, PathState& st) {
+    const uint32_t frame = P.frame0 + st.s;
+    const uint32_t idx = st.x + P.width * st.y + (P.width * P.height) * frame;
+    const v3 seed = hash3(idx);
+    st.seedx = seed.x;
+    st.nseed = normalize_seed(seed);
+    // (with the opt-in camera sampling the main loop replaces this primary
+    // ray before tracing it: one call site for sampled_primary_ray)
+    st.o = mk(0.0f + P.T[12], 0.0f + P.T[13], 0.0f + P.T[14]);
+    st.d = st.pd;
+    st.color = mk(1.0f, 1.0f, 1.0f);
+    st.bounce = 0;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+    const uint32_t t = __umulhi(f.m, n);
+    return (t + ((n - t) >> f.sh1)) >> f.sh2;
+}
+
+// Shard pixel p -> global (x, y): rows are blocks of row_block dealt
+// serpentine to the shards (rt_block_owner).
+__device__ __forceinline__ void pixel_xy(const KParams& P, uint32_t p, uint32_t& x, uint32_t& y) {
+    const uint32_t r = fdiv(p, P.div_width);
+    x = p - r * P.width;
+    const uint32_t rb = fdiv(r, P.div_row_block);
+    y = rt_shard_block(rb, P.shard_count, P.shard_index) * P.row_block + (r - rb * P.row_block);
+}
+
+// k-th pixel of a block in processing order -> shard-local pixel index
+// (row-major). Order: 8x8 tiles, so the 64 lanes of a wave trace a compact
+// patch of the image (coherent rays: fewer sphere groups with a candidate in
+// the wave); tile rows run bottom-up so the queue ends on the cheap sky rows.
+__device__ __forceinline__ uint32_t order_to_pixel(const KParams& P, uint32_t k) {
+    k = P.npix - 1 - k;
+    const uint32_t W = P.width;
+    const uint32_t tiled = P.tile_full_rows * 8 * W;
+    uint32_t x, r;
+    if (k < tiled) {
+        const uint32_t tr = fdiv(k, P.div_8w);
+        const uint32_t rem = k - tr * 8 * W;
+        const uint32_t tx = rem >> 6;
+        if (tx < P.tile_full_cols) {
+            x = tx * 8 + (rem & 7);
+            r = tr * 8 + ((rem >> 3) & 7);
+        } else {  // the narrow last tile of the tile row
+            const uint32_t j = rem - P.tile_full_cols * 64;
+            const uint32_t jr = fdiv(j, P.div_wrem);
+            x = P.tile_full_cols * 8 + (j - jr * P.tile_wrem);
+            r = tr * 8 + jr;
+        }
+    } else {
+        const uint32_t j = k - tiled;
+        const uint32_t jr = fdiv(j, P.div_width);
+        x = j - jr * W;
+        r = P.tile_full_rows * 8 + jr;
+    }
+    return r * W + x;
+}
+
+// Work item -> (sample block, pixel). block_sums is indexed by (block, pixel)
+// for the collect pass.
+// pixel table entry (rt_primary_kernel): k-th pixel of the processing order
+// -> its primary direction and (shard pixel index, x | y << 16).
+struct PixelEntry {
+    float4 d;       // xyz: primary direction, w: unused
+    uint32_t p, xy;
+    uint32_t pad0, pad1;
+};
+
+__device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint32_t item,
+                                           const PixelEntry* __restrict__ tab) {
+    uint32_t k, s0, s1;  // pixel in processing order; the item's samples [s0, s1)
+    if (item < P.main_all) {  // block item of pair q = (frame f, block b)
+        const uint32_t q = fdiv(item, P.div_npix);
+        k = item - q * P.npix;
+        const uint32_t f = fdiv(q, P.div_nblocks);
+        const uint32_t sl = (P.block_begin + (q - f * P.nblocks)) * RT_SAMPLE_BLOCK;
+        s0 = P.sample_base + f * P.spp + sl;
+        s1 = P.sample_base + f * P.spp + min(P.spp, sl + RT_SAMPLE_BLOCK);
+    } else {  // tail item: z = 4, 2 or 1 consecutive samples, each stored on its own
+        uint32_t j = item - P.main_all, z, gb, ge;
+        if (j < P.ti1) {
+            z = 4; gb = P.g0; ge = P.g1;
+        } else if (j < P.ti2) {
+            j -= P.ti1; z = 2; gb = P.g1; ge = P.g2;
+        } else {
+            j -= P.ti2; z = 1; gb = P.g2; ge = P.g_end;
+        }
+        const uint32_t g = fdiv(j, P.div_npix);
+        k = j - g * P.npix;
+        s0 = P.sample_base + gb + g * z;
+        s1 = P.sample_base + min(gb + g * z + z, ge);
+    }
+    const PixelEntry& e = tab[k];
+    const uint4 pxy = *reinterpret_cast<const uint4*>(&e.p);
+    const float4 q4 = e.d;
+    // block item: its output slot (= queue index); tail item: RT_TAIL_ITEM | k
+    st.item = item < P.main_all ? item : (RT_TAIL_ITEM | k);
+    st.x = pxy.y & 0xFFFFu;
+    st.y = pxy.y >> 16;
+    st.s = s0;
+    st.s_end = s1;
+    st.bsum = mk(0.0f, 0.0f, 0.0f);
+    st.pd = mk(q4.x, q4.y, q4.z);
+    start_sample(P, st);
+}
+
+// One path step after an intersection: shade.wgsl:199-258 for hit `hi` at t.
+// Returns true when the path has finished (miss, or hit at bounce D-1).
+// Written as converged stages so that each normalize (correctly rounded sqrt
+// + 3 divides) is issued once per wave, not once per material branch:
+//   record  : hit point + normal (intersect.wgsl:117-127)
+//   pre     : normalize(reflect(d,n)) for metal, normalize(d) for dielectric
+//   select  : per-material arithmetic producing the vector to normalize
+//   post    : normalize(d) for the sky, the new direction otherwise
+// Every lane performs exactly the reference's op sequence for its case.
+__device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, float t,
+                                      const float4* __restrict__ sph,
+                                      const float2* __restrict__ sph_rm,
+                                      const rt_material* __restrict__ mats) {
+    const bool miss = hi < 0;
+    if (!miss && st.bounce == P.max_depth - 1) {  // shade.wgsl:236-238
+        st.color = mk(0.0f, 0.0f, 0.0f);
+        return true;
+    }
+    // ---- record (hit lanes)
+    v3 pos = mk(0.0f, 0.0f, 0.0f), nrm = mk(0.0f, 0.0f, 0.0f);
+    bool front = true;
+    int refl = -1;
+    float4 mc = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+    float fuzz = 0.0f, ior = 1.0f;
+    if (!miss) {
+        const float4 s = sph[hi];
+        const float2 rm = sph_rm[hi];
+        const float radius = rm.x;
+        const uint32_t mi = __float_as_uint(rm.y);
+        pos = add(st.o, scale(st.d, t));
+        const v3 q = sub(pos, mk(s.x, s.y, s.z));
+        nrm = normalize_x(div3_x(q, radius));
+        if (dot(st.d, nrm) > 0.0f) {
+            nrm = neg(nrm);
+            front = false;
+        }
+        const rt_material& m = mats[mi];
+        refl = m.reflectance;
+        mc = *reinterpret_cast<const float4*>(m.color);
+        fuzz = m.fuzziness;
+        ior = m.index_of_refraction;
+    }
+    // ---- pre-normalize: metal normalize(reflect(d, n)) (shade.wgsl:140),
+    //      dielectric unit_dir = normalize(d) (shade.wgsl:169)
+    v3 un = mk(0.0f, 0.0f, 0.0f);
+    if (refl == RT_METALLIC || refl == RT_DIELECTRIC)
+        un = normalize_x(refl == RT_METALLIC ? reflect(st.d, nrm) : st.d);
+    // ---- select
+    v3 v = st.d;           // vector to normalize (sky: d, shade.wgsl:190)
+    bool post = true;      // false: dielectric reflection keeps reflect(d, n) unnormalized
+    v3 e_dir_raw = mk(0.0f, 0.0f, 0.0f);
+    if (refl == RT_LAMBERTIAN) {  // shade.wgsl:121-124
+        const v3 dest = add(add(pos, nrm), st.nseed);
+        v = sub(dest, pos);
+    } else if (refl == RT_METALLIC) {  // shade.wgsl:141-142
+        v = add(un, scale(st.nseed, fuzz));
+    } else if (refl == RT_DIELECTRIC) {  // shade.wgsl:164-180
+        float ratio = ior;
+        if (front) ratio = 1.0f / ior;
+        const float cos_theta = fminf(dot(neg(un), nrm), 1.0f);
+        const float sin_theta = sqrt_x(1.0f - cos_theta * cos_theta);
+        const bool cannot_refract = ratio * sin_theta > 1.0f;
+        float r0 = (1.0f - ratio) / (1.0f + ratio);  // reflectance(), shade.wgsl:156-161
+        r0 = r0 * r0;
+        const float xr = 1.0f - cos_theta;
+        const float x2 = xr * xr;
+        const float refl_p = r0 + (1.0f - r0) * ((x2 * x2) * xr);
+        if (cannot_refract || refl_p > st.seedx) {
+            e_dir_raw = reflect(st.d, nrm);
+            post = false;
+        } else {  // refract(unit_dir, n, ratio), shade.wgsl:148-153
+            const v3 perp = scale(add(un, scale(nrm, cos_theta)), ratio);
+            const float lp = length_x(perp);
+            const float par = -sqrt_x(fabsf(1.0f - (lp * lp)));
+            v = add(perp, scale(nrm, par));
+        }
+    }
+    // ---- post-normalize
+    v3 vn = mk(0.0f, 0.0f, 0.0f);
+    if (post) vn = normalize_x(v);
+    if (miss) {  // miss(), shade.wgsl:189-197, color *= sky
+        const float tt = 0.5f * vn.y + 1.0f;
+        const float omt = (1.0f - tt) * 1.0f;
+        st.color = mul(st.color, mk(omt + tt * 0.5f, omt + tt * 0.7f, omt + tt * 1.0f));
+        return true;
+    }
+    if (refl == RT_LAMBERTIAN) {
+        st.o = pos;  // no offset (shade.wgsl:123)
+        st.d = vn;
+        st.color = mul(st.color, mk(mc.x, mc.y, mc.z));
+    } else {
+        st.o = add(pos, scale(nrm, EPSILON));  // shade.wgsl:139, 182
+        st.d = post ? vn : e_dir_raw;
+        if (refl == RT_METALLIC) st.color = mul(st.color, mk(mc.x, mc.y, mc.z));
+    }
+    ++st.bounce;
+    return false;
+}

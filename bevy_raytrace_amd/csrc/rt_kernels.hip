@@ -29,6 +29,11 @@
 // 97-115) on its own candidates in list order with the strict `<` tie-break
 // (:137), so the result is bit-identical to the brute-force reference loop.
 //
+// Sources: rt_dev_math.h (vector ops, correctly rounded short forms, camera
+// rays), rt_dev_intersect.h (exact test, filter8, candidate queues,
+// intersect_world / intersect_wide), rt_dev_path.h (lane state, work items,
+// shading); this file holds the kernels and their launchers.
+//
 // Floating point: compiled with -ffp-contract=off; every expression below
 // except the explicit FMAs of the filter is one IEEE f32 round-to-nearest op
 // in the same order as oracle/rt_oracle.c. Divides and square roots are
@@ -58,891 +63,10 @@ __device__ __forceinline__ float rt_cold(float x) {
 #define VERY_FAR 1e20f
 #define EPSILON 0.001f
 
-namespace {
+#include "rt_dev_math.h"
+#include "rt_dev_intersect.h"
+#include "rt_dev_path.h"
 
-struct v3 {
-    float x, y, z;
-};
-
-__device__ __forceinline__ v3 mk(float x, float y, float z) { return v3{x, y, z}; }
-__device__ __forceinline__ v3 add(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
-__device__ __forceinline__ v3 sub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
-__device__ __forceinline__ v3 mul(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
-__device__ __forceinline__ v3 scale(v3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
-__device__ __forceinline__ v3 neg(v3 a) { return mk(-a.x, -a.y, -a.z); }
-__device__ __forceinline__ float dot(v3 a, v3 b) {
-    float r = a.x * b.x;
-    r = r + a.y * b.y;
-    r = r + a.z * b.z;
-    return r;
-}
-__device__ __forceinline__ float length(v3 a) { return sqrtf(dot(a, a)); }
-__device__ __forceinline__ v3 normalize(v3 a) {
-    float l = length(a);
-    return mk(a.x / l, a.y / l, a.z / l);
-}
-
-// ---- the hot path's correctly rounded ops (rt_math.h): the short forms on
-// their checked domain; lanes outside it recompute with the plain IEEE op in
-// a branch the wave skips when no lane needs it. The result is the IEEE one
-// in every case (GPU parity tests; rt_debug_math + tests/test_gpu_math.py on
-// zeros, denormals, huge, inf and NaN operands).
-#ifdef RT_FAST_NOGUARD  // measurement only (NOT exact): no IEEE fallback lanes
-#define RT_GUARD_ON 0
-#else
-#define RT_GUARD_ON 1
-#endif
-#if defined(RT_NO_FAST_MATH) || defined(RT_SHADE_IEEE)  // A/B: plain IEEE operations
-__device__ __forceinline__ float sqrt_x(float x) { return sqrtf(x); }
-__device__ __forceinline__ float length_x(v3 a) { return sqrtf(dot(a, a)); }
-__device__ __forceinline__ float div_x(float n, float b, float) { return n / b; }
-__device__ __forceinline__ float recip_or_nan(float b) { return b; }
-__device__ __forceinline__ v3 div3_x(v3 v, float b) { return mk(v.x / b, v.y / b, v.z / b); }
-__device__ __forceinline__ v3 normalize_x(v3 v) { return normalize(v); }
-__device__ __forceinline__ v3 normalize_seed(v3 v) { return normalize(v); }
-#else
-// Each guard's ballot takes a single compare (no && / ||): the compare's lane
-// mask is then the ballot, with no round trip through a VGPR.
-__device__ __forceinline__ float sqrt_x(float x) {
-    float r = rt_sqrt_rn(x);
-    // x outside [2^-100, 2^100] (0, NaN, inf, < 0: IEEE) as one unsigned compare
-    const bool bad = __float_as_uint(x) - 0x0D800000u > 0x71800000u - 0x0D800000u;
-    if (RT_GUARD_ON && rt_ballot(bad) != 0) {
-        if (bad) r = sqrtf(rt_cold(x));
-    }
-    return r;
-}
-__device__ __forceinline__ float length_x(v3 a) { return sqrt_x(dot(a, a)); }
-
-// n / b for a denominator b > 0 with yb = rt_recip_rn(b), or yb = NaN when b
-// is outside rt_recip_rn's domain (every lane then takes the IEEE divide).
-__device__ __forceinline__ float div_x(float n, float b, float yb) {
-    float r = rt_div_rn(n, b, yb);
-    const bool ok = yb == yb && rt_num_ok(n);
-    if (RT_GUARD_ON && rt_ballot(!ok) != 0) {
-        if (!ok) r = n / b;
-    }
-    return r;
-}
-__device__ __forceinline__ float recip_or_nan(float b) {
-    return b > 0.0f && rt_den_ok(b) ? rt_recip_rn(b) : __builtin_nanf("");
-}
-
-// v / b componentwise, any sign of b: short form when b and every component
-// lie within [2^-40, 2^40] in magnitude (no zeros, so the sign rule of
-// rt_div_rn does not arise). The range test runs on the magnitudes' bit
-// patterns (integer min/max: same order as the floats, NaN above inf), so no
-// canonicalising float min/max is needed.
-__device__ __forceinline__ v3 div3_x(v3 v, float b) {
-    const float y = rt_recip_rn(b);
-    v3 r = mk(rt_div_rn(v.x, b, y), rt_div_rn(v.y, b, y), rt_div_rn(v.z, b, y));
-    const uint32_t ax = __float_as_uint(v.x) & 0x7FFFFFFFu, ay = __float_as_uint(v.y) & 0x7FFFFFFFu;
-    const uint32_t az = __float_as_uint(v.z) & 0x7FFFFFFFu, ab = __float_as_uint(b) & 0x7FFFFFFFu;
-    const uint32_t lo = min(min(min(ax, ay), az), ab), hi = max(max(max(ax, ay), az), ab);
-    const bool small = lo < 0x2B800000u /* 2^-40 */, big = hi > 0x53800000u /* 2^40 */;
-    if (RT_GUARD_ON && (rt_ballot(small) | rt_ballot(big)) != 0) {
-        if (small || big) {
-            const float bb = rt_cold(b);
-            r = mk(v.x / bb, v.y / bb, v.z / bb);
-        }
-    }
-    return r;
-}
-
-// normalize(v) = v / sqrt(dot(v, v)): short form when every squared component
-// is at least 2^-80 and dot(v, v) <= 2^80 (false for NaN / inf): then every
-// |v_i| >= 2^-40 (1 - 2^-24), dot(v, v) lies in rt_sqrt_rn's domain, the
-// length l in [2^-40, 2^40] > 0 and every numerator in rt_div_rn's. The
-// squares are dot's own products, so the guard costs a v_min3 and 2 compares.
-__device__ __forceinline__ v3 normalize_x(v3 v) {
-    const float px = v.x * v.x, py = v.y * v.y, pz = v.z * v.z;
-    const float d2 = (px + py) + pz;  // = dot(v, v), same op order
-    const float l = rt_sqrt_rn(d2);
-    const float y = rt_recip_rn(l);
-    v3 r = mk(rt_div_rn(v.x, l, y), rt_div_rn(v.y, l, y), rt_div_rn(v.z, l, y));
-    const bool small = !(fminf(fminf(px, py), pz) >= 0x1p-80f), big = !(d2 <= 0x1p80f);
-    if (RT_GUARD_ON && (rt_ballot(small) | rt_ballot(big)) != 0) {
-        if (small || big) r = normalize(mk(rt_cold(v.x), v.y, v.z));
-    }
-    return r;
-}
-
-// normalize(hash3(n)) needs no guard: hash3's components are k / 2^31 with k
-// odd (shade.wgsl:105-116: n is odd after the first step), so each lies in
-// [2^-31, 1], dot in [3*2^-62, 3] and the length in [2^-31, 2].
-__device__ __forceinline__ v3 normalize_seed(v3 v) {
-    const float l = rt_sqrt_rn(dot(v, v));
-    const float y = rt_recip_rn(l);
-    return mk(rt_div_rn(v.x, l, y), rt_div_rn(v.y, l, y), rt_div_rn(v.z, l, y));
-}
-#endif  // RT_NO_FAST_MATH
-
-// shade.wgsl:105-116
-__device__ __forceinline__ v3 hash3(uint32_t n) {
-    n = (n << 13) ^ n;
-    n = n * (n * n * 15731u + 789221u) + 1376312589u;
-    uint32_t kx = n * n;
-    uint32_t ky = n * (n * 16807u);
-    uint32_t kz = n * (n * 48271u);
-    const float den = 2147483648.0f;
-    return mk((float)(kx & 0x7fffffffu) / den, (float)(ky & 0x7fffffffu) / den,
-              (float)(kz & 0x7fffffffu) / den);
-}
-
-// generate.wgsl:66-129 (lens offset 0: origin = camera translation).
-__device__ __forceinline__ void primary_ray(const KParams& P, uint32_t x, uint32_t y, v3& o,
-                                            v3& d) {
-    float px = (float)x, py = (float)y;
-    v3 dir = mk(((px - P.half_w) * P.tan_half) / P.aspect,
-                ((-py + P.half_h) * P.tan_half) / P.aspect, -1.0f);
-    dir = normalize(dir);
-    float denom = dot(dir, mk(0.0f, 0.0f, -1.0f));
-    v3 fpnt = scale(dir, P.focus_plane / denom);
-    v3 origin = mk(0.0f, 0.0f, 0.0f);
-    dir = normalize(sub(fpnt, origin));
-    const float* T = P.T;
-    o = add(origin, mk(T[12], T[13], T[14]));
-    d.x = ((T[0] * dir.x + T[4] * dir.y) + T[8] * dir.z) + T[12] * 0.0f;
-    d.y = ((T[1] * dir.x + T[5] * dir.y) + T[9] * dir.z) + T[13] * 0.0f;
-    d.z = ((T[2] * dir.x + T[6] * dir.y) + T[10] * dir.z) + T[14] * 0.0f;
-}
-
-// rt_sincos of the opt-in thin-lens sampling (include/rt_hip.h): Cody-Waite
-// reduction by pi/2, Taylor polynomials, quadrant swap; plain f32 ops in the
-// oracle's order (oracle/rt_oracle.c rto_sincos).
-__device__ __forceinline__ void rt_sincos(float theta, float& s, float& c) {
-    const float q = rintf(theta * 0x1.45f306p-1f);
-    float r = theta - q * 0x1.92p+0f;
-    r = r - q * 0x1.fb5444p-12f;
-    r = r - q * 0x1.68cp-39f;
-    const float r2 = r * r;
-    const float sr = r + r * (r2 * (-0x1.555556p-3f +
-                                    r2 * (0x1.111112p-7f +
-                                          r2 * (-0x1.a01a02p-13f + r2 * 0x1.71de3ap-19f))));
-    const float cr = 1.0f + r2 * (-0x1p-1f +
-                                  r2 * (0x1.555556p-5f +
-                                        r2 * (-0x1.6c16c2p-10f +
-                                              r2 * (0x1.a01a02p-16f + r2 * -0x1.27e4fcp-22f))));
-    switch ((int)q & 3) {
-        case 0: s = sr; c = cr; break;
-        case 1: s = cr; c = -sr; break;
-        case 2: s = -sr; c = -cr; break;
-        default: s = -cr; c = sr; break;
-    }
-}
-
-// Opt-in camera sampling (RT_FLAG_JITTER / RT_FLAG_THIN_LENS, rt_hip.h):
-// generate.wgsl:66-129 with a jittered pixel position and/or a lens sample
-// fed to thin_lens_ray (generate.wgsl:85-107) verbatim. idx = the seed index.
-__device__ __forceinline__ void sampled_primary_ray(const KParams& P, uint32_t x, uint32_t y,
-                                                 uint32_t idx, v3& o, v3& d) {
-    float px = (float)x, py = (float)y;
-    if (P.flags & RT_FLAG_JITTER) {
-        const v3 j = hash3(idx * RT_JITTER_HASH_MUL);
-        px = px + (j.x - 0.5f);
-        py = py + (j.y - 0.5f);
-    }
-    v3 dir = mk(((px - P.half_w) * P.tan_half) / P.aspect,
-                ((-py + P.half_h) * P.tan_half) / P.aspect, -1.0f);
-    dir = normalize(dir);
-    const float denom = dot(dir, mk(0.0f, 0.0f, -1.0f));
-    const v3 fpnt = scale(dir, P.focus_plane / denom);
-    v3 origin = mk(0.0f, 0.0f, 0.0f);
-    if (P.flags & RT_FLAG_THIN_LENS) {
-        const v3 l = hash3(idx * RT_LENS_HASH_MUL);
-        const float pi2 = 2.0f * 3.14159265358979f;
-        const float theta = pi2 * l.x + pi2;
-        const float sr = sqrtf(l.y);
-        float sn, cs;
-        rt_sincos(theta, sn, cs);
-        const float a = (cs * sr) * P.coc, b = (sn * sr) * P.coc;
-        origin = add(mk(1.0f * a, 0.0f * a, 0.0f * a), mk(0.0f * b, 1.0f * b, 0.0f * b));
-    }
-    dir = normalize(sub(fpnt, origin));
-    const float* T = P.T;
-    o = add(origin, mk(T[12], T[13], T[14]));
-    d.x = ((T[0] * dir.x + T[4] * dir.y) + T[8] * dir.z) + T[12] * 0.0f;
-    d.y = ((T[1] * dir.x + T[5] * dir.y) + T[9] * dir.z) + T[13] * 0.0f;
-    d.z = ((T[2] * dir.x + T[6] * dir.y) + T[10] * dir.z) + T[14] * 0.0f;
-}
-
-// shade.wgsl:189-197
-__device__ __forceinline__ v3 sky(v3 d) {
-    v3 unit = normalize(d);
-    float t = 0.5f * unit.y + 1.0f;
-    float omt = (1.0f - t) * 1.0f;
-    return mk(omt + t * 0.5f, omt + t * 0.7f, omt + t * 1.0f);
-}
-
-__device__ __forceinline__ v3 reflect(v3 v, v3 n) {  // shade.wgsl:132-134
-    float k = 2.0f * dot(v, n);
-    return sub(v, scale(n, k));
-}
-
-// ---- diagnostic build only (-DRT_PROFILE): per-wave phase clocks (s_memtime)
-// and wave-level event counts, summed into a debug buffer. Never compiled into
-// the product library.
-#ifdef RT_PROFILE
-struct Prof {
-    unsigned long long c[16];
-    unsigned long long last;
-};
-#define PROF_DECL Prof prof_ = {};
-#define PROF_START() (prof_.last = __builtin_amdgcn_s_memtime())
-#define PROF_MARK(i)                                            \
-    do {                                                        \
-        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-        prof_.c[i] += t_ - prof_.last;                          \
-        prof_.last = t_;                                        \
-    } while (0)
-#define PROF_ADD(i, v) (prof_.c[i] += (v))
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-    for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off));
-    return v;
-}
-#else
-#define PROF_DECL
-#define PROF_START()
-#define PROF_MARK(i)
-#define PROF_ADD(i, v)
-#endif
-
-// Exact reference test of one sphere (intersect.wgsl:97-115 + :137).
-// s.w = RN(radius*radius) = sqr(s.radius); r2p = s.w * (1 + 2^-20).
-#ifdef RT_PROFILE
-__device__ uint32_t g_prof_dummy;
-#define EXACT_COUNT(k) (ecnt[k]++)
-#define EXACT_ARGS , uint32_t* ecnt
-#define EXACT_PASS , ecnt
-#else
-#define EXACT_COUNT(k)
-#define EXACT_ARGS
-#define EXACT_PASS
-#endif
-// FAST (wave-uniform, ray_fast below): the short correctly-rounded forms of
-// rt_math.h, unguarded. Their domains hold without per-candidate checks:
-// the scene (rt_api.cpp scene_fast_ok) has |centre_i| <= 2^30 and
-// r^2 in [2^-40, 2^60], the ray |origin_i| <= 2^32 and a in [2^-20, 2^20], so
-// qq < 2^67, |half_b| < 2^44, dis < 2^88 and the numerators < 2^45. Low ends:
-//  - qq < 2^-100 (incl. 0): lo^2 < 2^-99 is below half an ulp of s.w >= 2^-40,
-//    so c = -s.w whichever lo (IEEE or short) the square root returned;
-//  - dis < 2^-100: the IEEE sqrtf (a rare branch; dis < 0 returns as before);
-//  - |numerator| < 2^-60 (incl. +-0): IEEE and short quotients both have
-//    |root| < 2^-40 < EPSILON and are rejected alike.
-// Otherwise the IEEE operations (sqrtf, '/'). ya = rt_recip_rn(a) when FAST.
-template <bool FAST>
-__device__ __forceinline__ void exact_body(float4 s, int idx, v3 o, v3 d, float a, float ya,
-                                           float& best_t, int& best_i EXACT_ARGS) {
-    EXACT_COUNT(0);
-    const v3 oc = mk(o.x - s.x, o.y - s.y, o.z - s.z);
-    const float half_b = dot(oc, d);
-    const float qq = dot(oc, oc);
-    // Cheap certain-miss: centre behind the origin (half_b >= 0) and origin
-    // outside (qq >= r^2 (1 + 2^-20) => c >= 0 after the sqrt/square round
-    // trip). Then dis <= half_b^2, sqrt(dis) <= half_b, and both roots are
-    // <= 0 < EPSILON, exactly as the full evaluation below would find.
-    if (half_b >= 0.0f && qq >= s.w * (1.0f + 0x1p-20f)) return;
-    EXACT_COUNT(1);
-    const float lo = FAST ? rt_sqrt_rn(qq) : sqrtf(qq);
-    const float c = lo * lo - s.w;
-    const float dis = half_b * half_b - a * c;
-    float sqrtd;
-    if (FAST) {
-        if (dis < 0x1p-100f) {
-            if (dis < 0.0f) return;
-            sqrtd = sqrtf(rt_cold(dis));
-        } else {
-            sqrtd = rt_sqrt_rn(dis);
-        }
-    } else {
-        if (dis < 0.0f) return;
-        sqrtd = sqrtf(dis);
-    }
-    float root = FAST ? rt_div_rn(-half_b - sqrtd, a, ya) : (-half_b - sqrtd) / a;
-    if (root < EPSILON || VERY_FAR < root) {
-        root = FAST ? rt_div_rn(-half_b + sqrtd, a, ya) : (-half_b + sqrtd) / a;
-        if (root < EPSILON || VERY_FAR < root) return;
-    }
-    if (root < best_t) {
-        best_t = root;
-        best_i = idx;
-    }
-}
-
-__device__ __forceinline__ void exact_test(float4 s, int idx, v3 o, v3 d, float a, float ya,
-                                           bool fast, float& best_t, int& best_i EXACT_ARGS) {
-    if (fast)
-        exact_body<true>(s, idx, o, d, a, ya, best_t, best_i EXACT_PASS);
-    else
-        exact_body<false>(s, idx, o, d, a, ya, best_t, best_i EXACT_PASS);
-}
-
-// The ray side of the short-math domain (exact_body), for the whole wave.
-__device__ __forceinline__ bool ray_fast(uint32_t scene_fast, v3 o, float a) {
-#ifdef RT_NO_FAST_MATH
-    return false;
-#else
-    // (a NaN origin component makes every exact test of the lane NaN in both
-    // forms: no hit either way)
-    const float om = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
-    return scene_fast != 0 && (rt_ballot(!(om <= 0x1p32f)) | rt_ballot(!(a >= 0x1p-20f)) |
-                               rt_ballot(!(a <= 0x1p20f))) == 0;
-#endif
-}
-
-typedef float f2 __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(4))) const float4 cfloat4;  // scalar-cache reads
-
-__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ f2 bc(float x) { return f2{x, x}; }
-
-// Per-ray constants of the expanded-form filter (see file header / DESIGN.md):
-//   G' = (k1 - dn.c)^2 + S + K + o2.c
-//      = hb^2 + r^2 - (1 - m) |o - c|^2 + mu (|o|^2 + |c|^2)
-// with hb = dn.(o - c), dn ~ d/|d|, S = r^2 - (1 - m - mu)|c|^2 (per sphere,
-// host), k1 = dn.o, K = -(1 - m - mu)|o|^2, o2 = 2(1 - m) o (per ray).
-// m = 2^-16 bounds the exact path's rounding relative to |o - c|^2 + r^2,
-// mu = 2^-17 the expanded form's cancellation relative to |o|^2 + |c|^2.
-struct RayF {
-    f2 dx, dy, dz, o2x, o2y, o2z, k1;  // dx,dy,dz hold -dn
-    float T;                           // candidate threshold -K
-};
-
-__device__ __forceinline__ RayF ray_filter_consts(v3 o, v3 d) {
-    const float rs = __builtin_amdgcn_rsqf(dot(d, d));  // approximate 1/|d| (covered by m)
-    const float dnx = d.x * rs, dny = d.y * rs, dnz = d.z * rs;
-    const float m = 0x1p-16f, mu = 0x1p-17f;
-    const float oo = __builtin_fmaf(o.z, o.z, __builtin_fmaf(o.y, o.y, o.x * o.x));
-    const float k1 = __builtin_fmaf(dnz, o.z, __builtin_fmaf(dny, o.y, dnx * o.x));
-    const float two = 2.0f * (1.0f - m);
-    RayF r;
-    r.dx = bc(-dnx); r.dy = bc(-dny); r.dz = bc(-dnz);  // negated: hb = k1 + (-dn).c
-    r.o2x = bc(two * o.x); r.o2y = bc(two * o.y); r.o2z = bc(two * o.z);
-    r.k1 = bc(k1);
-    r.T = (1.0f - m - mu) * oo;
-    return r;
-}
-
-// Filter two spheres at once: 7 packed fp32 FMAs (v_pk_fma_f32: two f32 FMAs
-// per lane per issue, tools/ubench/fma_rate.hip). Returns H = hb^2 + S + o2.c;
-// the sphere is a candidate iff H >= T, the ray's threshold (an exact
-// comparison). The C++ form of filter8 (builds without RT_ASM_FILTER).
-__device__ __forceinline__ f2 filter2(f2 cx, f2 cy, f2 cz, f2 S, const RayF& r) {
-    // every op has ONE SGPR-pair operand (sphere data) -- the constant-bus limit
-    const f2 hb = pk_fma(r.dz, cz, pk_fma(r.dy, cy, pk_fma(r.dx, cx, r.k1)));  // k1 - dn.c
-    return pk_fma(r.o2x, cx, pk_fma(r.o2y, cy, pk_fma(r.o2z, cz, pk_fma(hb, hb, S))));
-}
-
-// The same filter for a whole group of 8 spheres in hand-scheduled VOP3P:
-// the ray constants live ONCE in 4 VGPR pairs (r0 = (-dnx, -dny),
-// r1 = (-dnz, k1), r2 = (o2x, o2y), r3 = (o2z, T)) and op_sel / op_sel_hi
-// broadcast one half to both packed lanes -- the compiler's form needs every
-// constant duplicated in a pair (7 VGPRs more at the 80-VGPR occupancy limit).
-// The four pair chains are interleaved, so dependent ops are 4 apart (no
-// wait states, and a lone wave in the queue tail issues back to back). Op
-// order per pair is exactly filter2's.
-struct RayP {
-    f2 r0, r1, r2, r3;
-};
-
-__device__ __forceinline__ RayP ray_pack(const RayF& r) {
-    RayP p;
-    p.r0 = f2{r.dx.x, r.dy.x};
-    p.r1 = f2{r.dz.x, r.k1.x};
-    p.r2 = f2{r.o2x.x, r.o2y.x};
-    p.r3 = f2{r.o2z.x, r.T};
-    return p;
-}
-
-__device__ __forceinline__ void filter8(const RayP& R, f2 cxa, f2 cxb, f2 cxc, f2 cxd, f2 cya,
-                                        f2 cyb, f2 cyc, f2 cyd, f2 cza, f2 czb, f2 czc, f2 czd,
-                                        f2 sa, f2 sb, f2 sc, f2 sd, f2& ha, f2& hb, f2& hc,
-                                        f2& hd, float& hmax) {
-    asm volatile(
-        // hb = k1 + (-dnx) cx + (-dny) cy + (-dnz) cz
-        "v_pk_fma_f32 %[ha], %[r0], %[cxa], %[r1] op_sel:[0,0,1] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[hb], %[r0], %[cxb], %[r1] op_sel:[0,0,1] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[hc], %[r0], %[cxc], %[r1] op_sel:[0,0,1] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[hd], %[r0], %[cxd], %[r1] op_sel:[0,0,1] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[ha], %[r0], %[cya], %[ha] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
-        "v_pk_fma_f32 %[hb], %[r0], %[cyb], %[hb] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
-        "v_pk_fma_f32 %[hc], %[r0], %[cyc], %[hc] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
-        "v_pk_fma_f32 %[hd], %[r0], %[cyd], %[hd] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
-        "v_pk_fma_f32 %[ha], %[r1], %[cza], %[ha] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[hb], %[r1], %[czb], %[hb] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[hc], %[r1], %[czc], %[hc] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[hd], %[r1], %[czd], %[hd] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
-        // H = hb^2 + S + o2z cz + o2y cy + o2x cx
-        "v_pk_fma_f32 %[ha], %[ha], %[ha], %[sa]\n\t"
-        "v_pk_fma_f32 %[hb], %[hb], %[hb], %[sb]\n\t"
-        "v_pk_fma_f32 %[hc], %[hc], %[hc], %[sc]\n\t"
-        "v_pk_fma_f32 %[hd], %[hd], %[hd], %[sd]\n\t"
-        "v_pk_fma_f32 %[ha], %[r3], %[cza], %[ha] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[hb], %[r3], %[czb], %[hb] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[hc], %[r3], %[czc], %[hc] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[hd], %[r3], %[czd], %[hd] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[ha], %[r2], %[cya], %[ha] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
-        "v_pk_fma_f32 %[hb], %[r2], %[cyb], %[hb] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
-        "v_pk_fma_f32 %[hc], %[r2], %[cyc], %[hc] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
-        "v_pk_fma_f32 %[hd], %[r2], %[cyd], %[hd] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
-        "v_pk_fma_f32 %[ha], %[r2], %[cxa], %[ha] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[hb], %[r2], %[cxb], %[hb] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[hc], %[r2], %[cxc], %[hc] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[hd], %[r2], %[cxd], %[hd] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
-        // group max of the 8 H (v_max3 drops a quiet-NaN operand, as fmaxf)
-        "v_max3_f32 %[hm], v40, v41, v42\n\t"
-        "v_max3_f32 %[hm], %[hm], v43, v44\n\t"
-        "v_max3_f32 %[hm], %[hm], v45, v46\n\t"
-        "v_max_f32 %[hm], %[hm], v47"
-        : [ha] "={v[40:41]}"(ha), [hb] "={v[42:43]}"(hb), [hc] "={v[44:45]}"(hc),
-          [hd] "={v[46:47]}"(hd), [hm] "=&v"(hmax)
-        : [r0] "v"(R.r0), [r1] "v"(R.r1), [r2] "v"(R.r2), [r3] "v"(R.r3), [cxa] "s"(cxa),
-          [cxb] "s"(cxb), [cxc] "s"(cxc), [cxd] "s"(cxd), [cya] "s"(cya), [cyb] "s"(cyb),
-          [cyc] "s"(cyc), [cyd] "s"(cyd), [cza] "s"(cza), [czb] "s"(czb), [czc] "s"(czc),
-          [czd] "s"(czd), [sa] "s"(sa), [sb] "s"(sb), [sc] "s"(sc), [sd] "s"(sd));
-}
-
-__device__ __forceinline__ uint32_t ge(float h, float t) { return h >= t ? 1u : 0u; }
-
-#if defined(RT_ASM_FILTER) && defined(__HIP_DEVICE_COMPILE__)
-// The lane's 8-bit candidate mask (bit j = H_j >= T, the same compares as
-// ge()): the 8 compares go to 8 SGPR lane masks, then m = 2m + c_j shifts
-// them in with v_addc (carry-in = the lane's bit of c_j), sphere 7 first --
-// 16 VALU instead of 8 compares + 8 v_cndmask + 4 ORs, and every mask is
-// read 7+ instructions after its compare wrote it (no VALU-SGPR wait states).
-__device__ __forceinline__ uint32_t cand_mask8(f2 g01, f2 g23, f2 g45, f2 g67, float T) {
-    uint32_t m;
-    uint64_t c0, c1, c2, c3, c4, c5, c6, c7;
-    asm("v_cmp_ge_f32_e64 %[c7], %[h7], %[T]\n"
-        "v_cmp_ge_f32_e64 %[c6], %[h6], %[T]\n"
-        "v_cmp_ge_f32_e64 %[c5], %[h5], %[T]\n"
-        "v_cmp_ge_f32_e64 %[c4], %[h4], %[T]\n"
-        "v_cmp_ge_f32_e64 %[c3], %[h3], %[T]\n"
-        "v_cmp_ge_f32_e64 %[c2], %[h2], %[T]\n"
-        "v_cmp_ge_f32_e64 %[c1], %[h1], %[T]\n"
-        "v_cmp_ge_f32_e64 %[c0], %[h0], %[T]\n"
-        "v_cndmask_b32_e64 %[m], 0, 1, %[c7]\n"
-        "v_addc_co_u32_e64 %[m], %[c7], %[m], %[m], %[c6]\n"
-        "v_addc_co_u32_e64 %[m], %[c6], %[m], %[m], %[c5]\n"
-        "v_addc_co_u32_e64 %[m], %[c5], %[m], %[m], %[c4]\n"
-        "v_addc_co_u32_e64 %[m], %[c4], %[m], %[m], %[c3]\n"
-        "v_addc_co_u32_e64 %[m], %[c3], %[m], %[m], %[c2]\n"
-        "v_addc_co_u32_e64 %[m], %[c2], %[m], %[m], %[c1]\n"
-        "v_addc_co_u32_e64 %[m], %[c1], %[m], %[m], %[c0]\n"
-        : [m] "=&v"(m), [c0] "=&s"(c0), [c1] "=&s"(c1), [c2] "=&s"(c2), [c3] "=&s"(c3),
-          [c4] "=&s"(c4), [c5] "=&s"(c5), [c6] "=&s"(c6), [c7] "=&s"(c7)
-        : [h0] "v"(g01.x), [h1] "v"(g01.y), [h2] "v"(g23.x), [h3] "v"(g23.y),
-          [h4] "v"(g45.x), [h5] "v"(g45.y), [h6] "v"(g67.x), [h7] "v"(g67.y), [T] "v"(T));
-    return m;
-}
-#endif
-
-template <bool FAST>
-__device__ __forceinline__ void drain_list(const uint32_t* cq, uint32_t cnt,
-                                           const float4* __restrict__ sph, v3 o, v3 d, float a,
-                                           float ya, float& best_t, int& best_i EXACT_ARGS) {
-    const uint32_t lane = __lane_id();
-    for (uint32_t k = 0; k < cnt; ++k) {
-        const uint32_t e = cq[k * 64 + lane];
-        uint32_t m = e & 0xFFu;
-        const uint32_t base = (e >> 8) * RT_GROUP;
-        while (m) {
-            const uint32_t j = __builtin_ctz(m);
-            m &= m - 1;
-            exact_body<FAST>(sph[base + j], (int)(base + j), o, d, a, ya, best_t, best_i EXACT_PASS);
-        }
-    }
-}
-
-// Run the exact test for every queued candidate of this lane, in list order.
-// Queue entries are (group << 8 | 8-bit candidate mask), one column per lane.
-__device__ __forceinline__ void drain_candidates(const uint32_t* cq, uint32_t cnt,
-                                                 const float4* __restrict__ sph, v3 o, v3 d,
-                                                 float a, bool fast, float& best_t,
-                                                 int& best_i EXACT_ARGS) {
-    if (fast)
-        drain_list<true>(cq, cnt, sph, o, d, a, rt_recip_rn(a), best_t, best_i EXACT_PASS);
-    else
-        drain_list<false>(cq, cnt, sph, o, d, a, a, best_t, best_i EXACT_PASS);
-}
-
-// Closest hit over the whole list (intersect.wgsl:133-143).
-// grp: the sphere list as groups of RT_GROUP=8, SoA (cx[8], cy[8], cz[8], S[8]),
-// padded to whole groups with pad records of S = -inf (never candidates).
-// Wave-uniform: read with s_load_dwordx16 and fed to the packed ops as SGPR
-// pairs. sph: the padded records AoS (cx, cy, cz, r2), gathered per lane by
-// the exact tests. Pass 1 filters every sphere and queues candidates per lane
-// (LDS, cq); the group test is max(H) >= T over the 8 spheres. Pass 2 (drain)
-// runs the exact reference test on the queued candidates in list order, so the
-// wave pays for max-over-lanes candidates, not for their union.
-// Returns the best index (-1 = miss) and t.
-__device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
-                                               const float4* __restrict__ sph, uint32_t ngroups,
-                                               uint32_t scene_fast, v3 o, v3 d, float& t_out,
-                                               uint32_t* cq
-#ifdef RT_PROFILE
-                                               , Prof& prof_
-#endif
-                                               ) {
-    const float l = sqrt_x(dot(d, d));
-    const float a = l * l;  // sqr(length(r.dir)), intersect.wgsl:98
-    const bool fast = ray_fast(scene_fast, o, a);
-#if defined(RT_ASM_FILTER) && defined(__HIP_DEVICE_COMPILE__)
-    const RayP RP = ray_pack(ray_filter_consts(o, d));
-    const float RT_T = RP.r3.y;
-#else
-    const RayF R = ray_filter_consts(o, d);
-    const float RT_T = R.T;
-#endif
-    const uint32_t lane = __lane_id();
-    float best_t = VERY_FAR;
-    int best_i = -1;
-    uint32_t cnt = 0;
-#ifdef RT_PROFILE
-    uint32_t ecnt[2] = {0, 0};
-#endif
-    // constant address space: the groups are read with s_load into SGPRs
-    // whatever the alias analysis concludes about other stores
-#if defined(__HIP_DEVICE_COMPILE__)
-    const cfloat4* gp = (const cfloat4*)(uintptr_t)grp;
-#else
-    const float4* gp = grp;  // host pass: never executed
-#endif
-    for (uint32_t g = 0; g < ngroups; ++g) {
-        const auto* p = gp + (size_t)g * 8;
-        const float4 X0 = p[0], X1 = p[1], Y0 = p[2], Y1 = p[3];
-        const float4 Z0 = p[4], Z1 = p[5], S0 = p[6], S1 = p[7];
-#if defined(RT_ASM_FILTER) && defined(__HIP_DEVICE_COMPILE__)
-        f2 g01, g23, g45, g67;
-        float hmax;
-        filter8(RP, f2{X0.x, X0.y}, f2{X0.z, X0.w}, f2{X1.x, X1.y}, f2{X1.z, X1.w},
-                f2{Y0.x, Y0.y}, f2{Y0.z, Y0.w}, f2{Y1.x, Y1.y}, f2{Y1.z, Y1.w},
-                f2{Z0.x, Z0.y}, f2{Z0.z, Z0.w}, f2{Z1.x, Z1.y}, f2{Z1.z, Z1.w},
-                f2{S0.x, S0.y}, f2{S0.z, S0.w}, f2{S1.x, S1.y}, f2{S1.z, S1.w}, g01, g23, g45, g67,
-                hmax);
-#else
-        // group test below: max of the 8 H (v_max3 chain; a NaN H is dropped
-        // by max -- a NaN H never hits) against the ray's threshold
-        const f2 g01 = filter2(f2{X0.x, X0.y}, f2{Y0.x, Y0.y}, f2{Z0.x, Z0.y}, f2{S0.x, S0.y}, R);
-        const f2 g23 = filter2(f2{X0.z, X0.w}, f2{Y0.z, Y0.w}, f2{Z0.z, Z0.w}, f2{S0.z, S0.w}, R);
-        const f2 g45 = filter2(f2{X1.x, X1.y}, f2{Y1.x, Y1.y}, f2{Z1.x, Z1.y}, f2{S1.x, S1.y}, R);
-        const f2 g67 = filter2(f2{X1.z, X1.w}, f2{Y1.z, Y1.w}, f2{Z1.z, Z1.w}, f2{S1.z, S1.w}, R);
-        const float hmax = fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(g01.x, g01.y), g23.x), g23.y),
-                                                   g45.x), g45.y), g67.x), g67.y);
-#endif
-        if (rt_ballot(hmax >= RT_T) != 0) {
-            PROF_ADD(5, 1);
-            if (rt_ballot(cnt >= RT_CQ_CAP) != 0) {  // a lane's queue is full: drain all
-                PROF_ADD(11, 1);
-                drain_candidates(cq, cnt, sph, o, d, a, fast, best_t, best_i EXACT_PASS);
-                cnt = 0;
-            }
-            const float T = RT_T;
-#if defined(RT_ASM_FILTER) && defined(__HIP_DEVICE_COMPILE__)
-            const uint32_t m = cand_mask8(g01, g23, g45, g67, T);
-#else
-            const uint32_t m = ge(g01.x, T) | (ge(g01.y, T) << 1) | (ge(g23.x, T) << 2) |
-                               (ge(g23.y, T) << 3) | (ge(g45.x, T) << 4) | (ge(g45.y, T) << 5) |
-                               (ge(g67.x, T) << 6) | (ge(g67.y, T) << 7);
-#endif
-            if (m) {
-                cq[cnt * 64 + lane] = (g << 8) | m;
-                ++cnt;
-            }
-        }
-    }
-    PROF_MARK(1);
-#ifdef RT_PROFILE
-    PROF_ADD(6, wave_max_u32(cnt));
-#endif
-    drain_candidates(cq, cnt, sph, o, d, a, fast, best_t, best_i EXACT_PASS);
-    PROF_MARK(2);
-#ifdef RT_PROFILE
-    PROF_ADD(13, wave_max_u32(ecnt[0]));
-    PROF_ADD(14, wave_max_u32(ecnt[1]));
-    {
-        uint32_t sum0 = ecnt[0];
-        for (int off = 32; off > 0; off >>= 1) sum0 += __shfl_xor(sum0, off);
-        PROF_ADD(15, sum0);
-    }
-#endif
-    t_out = best_t;
-    return best_i;
-}
-
-// Sphere-parallel closest hit for the few live rays of a nearly empty wave
-// (the end of the work queue, where a wave's remaining paths would otherwise
-// each pay the whole ray-parallel list walk): one ray at a time, the 64 lanes
-// split the list and run the exact reference test (intersect.wgsl:97-115) on
-// their spheres in list order with the strict `<`; the wave reduction then
-// takes the smallest t, ties to the smallest index -- exactly the answer of
-// the sequential strict-`<` scan (intersect.wgsl:133-143).
-__device__ __forceinline__ void intersect_wide(const float4* __restrict__ sph, uint32_t n,
-                                               uint32_t scene_fast, uint64_t active, v3 o, v3 d,
-                                               int& hi, float& t) {
-    const uint32_t lane = __lane_id();
-    while (active) {
-        const int src = (int)__builtin_ctzll(active);
-        active &= active - 1;
-        const v3 ro = mk(__shfl(o.x, src), __shfl(o.y, src), __shfl(o.z, src));
-        const v3 rd = mk(__shfl(d.x, src), __shfl(d.y, src), __shfl(d.z, src));
-        const float l = sqrt_x(dot(rd, rd));
-        const float a = l * l;  // sqr(length(r.dir)), intersect.wgsl:98
-        const bool fast = ray_fast(scene_fast, ro, a);
-        const float ya = fast ? rt_recip_rn(a) : a;
-        float bt = VERY_FAR;
-        int bi = -1;
-        for (uint32_t i = lane; i < n; i += 64) {
-#ifdef RT_PROFILE
-            uint32_t ecnt[2];
-            exact_test(sph[i], (int)i, ro, rd, a, ya, fast, bt, bi, ecnt);
-#else
-            exact_test(sph[i], (int)i, ro, rd, a, ya, fast, bt, bi);
-#endif
-        }
-        for (int off = 32; off > 0; off >>= 1) {
-            const float ot = __shfl_xor(bt, off);
-            const int oi = __shfl_xor(bi, off);
-            if (ot < bt || (ot == bt && (uint32_t)oi < (uint32_t)bi)) {
-                bt = ot;
-                bi = oi;
-            }
-        }
-        if ((int)lane == src) {
-            hi = bi;
-            t = bt;
-        }
-    }
-}
-
-__device__ __forceinline__ uint32_t lanemask_lt_count(uint64_t m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-}  // namespace
-
-// Lane state of one in-flight path.
-struct PathState {
-    v3 o, d;            // current ray
-    v3 pd;              // primary direction of this pixel (generate.wgsl: pixel-only)
-    v3 color;           // throughput (intersection.color, clear.wgsl:86)
-    v3 bsum;            // sum of finished samples of the current block
-    v3 nseed;           // normalize(seed)
-    float seedx;        // seed.x (dielectric Schlick test)
-    uint32_t x, y;      // global pixel
-    uint32_t item;      // work item = (block - block_begin) * npix + pixel
-    uint32_t s, s_end;  // current sample, end of the block
-    uint32_t bounce;
-};
-
-// New sample s of the lane's pixel: seed (shade.wgsl:216-218), primary ray
-// (generate.wgsl:109-129; origin = camera translation, direction cached per
-// item since it depends on the pixel only), throughput 1 (clear.wgsl:86).
-__device__ __forceinline__ void start_sample(const KParams& P, PathState& st) {
-    const uint32_t frame = P.frame0 + st.s;
-    const uint32_t idx = st.x + P.width * st.y + (P.width * P.height) * frame;
-    const v3 seed = hash3(idx);
-    st.seedx = seed.x;
-    st.nseed = normalize_seed(seed);
-    // (with the opt-in camera sampling the main loop replaces this primary
-    // ray before tracing it: one call site for sampled_primary_ray)
-    st.o = mk(0.0f + P.T[12], 0.0f + P.T[13], 0.0f + P.T[14]);
-    st.d = st.pd;
-    st.color = mk(1.0f, 1.0f, 1.0f);
-    st.bounce = 0;
-}
-
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
-    const uint32_t t = __umulhi(f.m, n);
-    return (t + ((n - t) >> f.sh1)) >> f.sh2;
-}
-
-// Shard pixel p -> global (x, y): rows are blocks of row_block dealt
-// serpentine to the shards (rt_block_owner).
-__device__ __forceinline__ void pixel_xy(const KParams& P, uint32_t p, uint32_t& x, uint32_t& y) {
-    const uint32_t r = fdiv(p, P.div_width);
-    x = p - r * P.width;
-    const uint32_t rb = fdiv(r, P.div_row_block);
-    y = rt_shard_block(rb, P.shard_count, P.shard_index) * P.row_block + (r - rb * P.row_block);
-}
-
-// k-th pixel of a block in processing order -> shard-local pixel index
-// (row-major). Order: 8x8 tiles, so the 64 lanes of a wave trace a compact
-// patch of the image (coherent rays: fewer sphere groups with a candidate in
-// the wave); tile rows run bottom-up so the queue ends on the cheap sky rows.
-__device__ __forceinline__ uint32_t order_to_pixel(const KParams& P, uint32_t k) {
-    k = P.npix - 1 - k;
-    const uint32_t W = P.width;
-    const uint32_t tiled = P.tile_full_rows * 8 * W;
-    uint32_t x, r;
-    if (k < tiled) {
-        const uint32_t tr = fdiv(k, P.div_8w);
-        const uint32_t rem = k - tr * 8 * W;
-        const uint32_t tx = rem >> 6;
-        if (tx < P.tile_full_cols) {
-            x = tx * 8 + (rem & 7);
-            r = tr * 8 + ((rem >> 3) & 7);
-        } else {  // the narrow last tile of the tile row
-            const uint32_t j = rem - P.tile_full_cols * 64;
-            const uint32_t jr = fdiv(j, P.div_wrem);
-            x = P.tile_full_cols * 8 + (j - jr * P.tile_wrem);
-            r = tr * 8 + jr;
-        }
-    } else {
-        const uint32_t j = k - tiled;
-        const uint32_t jr = fdiv(j, P.div_width);
-        x = j - jr * W;
-        r = P.tile_full_rows * 8 + jr;
-    }
-    return r * W + x;
-}
-
-// Work item -> (sample block, pixel). block_sums is indexed by (block, pixel)
-// for the collect pass.
-// pixel table entry (rt_primary_kernel): k-th pixel of the processing order
-// -> its primary direction and (shard pixel index, x | y << 16).
-struct PixelEntry {
-    float4 d;       // xyz: primary direction, w: unused
-    uint32_t p, xy;
-    uint32_t pad0, pad1;
-};
-
-__device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint32_t item,
-                                           const PixelEntry* __restrict__ tab) {
-    uint32_t k, s0, s1;  // pixel in processing order; the item's samples [s0, s1)
-    if (item < P.main_all) {  // block item of pair q = (frame f, block b)
-        const uint32_t q = fdiv(item, P.div_npix);
-        k = item - q * P.npix;
-        const uint32_t f = fdiv(q, P.div_nblocks);
-        const uint32_t sl = (P.block_begin + (q - f * P.nblocks)) * RT_SAMPLE_BLOCK;
-        s0 = P.sample_base + f * P.spp + sl;
-        s1 = P.sample_base + f * P.spp + min(P.spp, sl + RT_SAMPLE_BLOCK);
-    } else {  // tail item: z = 4, 2 or 1 consecutive samples, each stored on its own
-        uint32_t j = item - P.main_all, z, gb, ge;
-        if (j < P.ti1) {
-            z = 4; gb = P.g0; ge = P.g1;
-        } else if (j < P.ti2) {
-            j -= P.ti1; z = 2; gb = P.g1; ge = P.g2;
-        } else {
-            j -= P.ti2; z = 1; gb = P.g2; ge = P.g_end;
-        }
-        const uint32_t g = fdiv(j, P.div_npix);
-        k = j - g * P.npix;
-        s0 = P.sample_base + gb + g * z;
-        s1 = P.sample_base + min(gb + g * z + z, ge);
-    }
-    const PixelEntry& e = tab[k];
-    const uint4 pxy = *reinterpret_cast<const uint4*>(&e.p);
-    const float4 q4 = e.d;
-    // block item: its output slot (= queue index); tail item: RT_TAIL_ITEM | k
-    st.item = item < P.main_all ? item : (RT_TAIL_ITEM | k);
-    st.x = pxy.y & 0xFFFFu;
-    st.y = pxy.y >> 16;
-    st.s = s0;
-    st.s_end = s1;
-    st.bsum = mk(0.0f, 0.0f, 0.0f);
-    st.pd = mk(q4.x, q4.y, q4.z);
-    start_sample(P, st);
-}
-
-// One path step after an intersection: shade.wgsl:199-258 for hit `hi` at t.
-// Returns true when the path has finished (miss, or hit at bounce D-1).
-// Written as converged stages so that each normalize (correctly rounded sqrt
-// + 3 divides) is issued once per wave, not once per material branch:
-//   record  : hit point + normal (intersect.wgsl:117-127)
-//   pre     : normalize(reflect(d,n)) for metal, normalize(d) for dielectric
-//   select  : per-material arithmetic producing the vector to normalize
-//   post    : normalize(d) for the sky, the new direction otherwise
-// Every lane performs exactly the reference's op sequence for its case.
-__device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, float t,
-                                      const float4* __restrict__ sph,
-                                      const float2* __restrict__ sph_rm,
-                                      const rt_material* __restrict__ mats) {
-    const bool miss = hi < 0;
-    if (!miss && st.bounce == P.max_depth - 1) {  // shade.wgsl:236-238
-        st.color = mk(0.0f, 0.0f, 0.0f);
-        return true;
-    }
-    // ---- record (hit lanes)
-    v3 pos = mk(0.0f, 0.0f, 0.0f), nrm = mk(0.0f, 0.0f, 0.0f);
-    bool front = true;
-    int refl = -1;
-    float4 mc = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
-    float fuzz = 0.0f, ior = 1.0f;
-    if (!miss) {
-        const float4 s = sph[hi];
-        const float2 rm = sph_rm[hi];
-        const float radius = rm.x;
-        const uint32_t mi = __float_as_uint(rm.y);
-        pos = add(st.o, scale(st.d, t));
-        const v3 q = sub(pos, mk(s.x, s.y, s.z));
-        nrm = normalize_x(div3_x(q, radius));
-        if (dot(st.d, nrm) > 0.0f) {
-            nrm = neg(nrm);
-            front = false;
-        }
-        const rt_material& m = mats[mi];
-        refl = m.reflectance;
-        mc = *reinterpret_cast<const float4*>(m.color);
-        fuzz = m.fuzziness;
-        ior = m.index_of_refraction;
-    }
-    // ---- pre-normalize: metal normalize(reflect(d, n)) (shade.wgsl:140),
-    //      dielectric unit_dir = normalize(d) (shade.wgsl:169)
-    v3 un = mk(0.0f, 0.0f, 0.0f);
-    if (refl == RT_METALLIC || refl == RT_DIELECTRIC)
-        un = normalize_x(refl == RT_METALLIC ? reflect(st.d, nrm) : st.d);
-    // ---- select
-    v3 v = st.d;           // vector to normalize (sky: d, shade.wgsl:190)
-    bool post = true;      // false: dielectric reflection keeps reflect(d, n) unnormalized
-    v3 e_dir_raw = mk(0.0f, 0.0f, 0.0f);
-    if (refl == RT_LAMBERTIAN) {  // shade.wgsl:121-124
-        const v3 dest = add(add(pos, nrm), st.nseed);
-        v = sub(dest, pos);
-    } else if (refl == RT_METALLIC) {  // shade.wgsl:141-142
-        v = add(un, scale(st.nseed, fuzz));
-    } else if (refl == RT_DIELECTRIC) {  // shade.wgsl:164-180
-        float ratio = ior;
-        if (front) ratio = 1.0f / ior;
-        const float cos_theta = fminf(dot(neg(un), nrm), 1.0f);
-        const float sin_theta = sqrt_x(1.0f - cos_theta * cos_theta);
-        const bool cannot_refract = ratio * sin_theta > 1.0f;
-        float r0 = (1.0f - ratio) / (1.0f + ratio);  // reflectance(), shade.wgsl:156-161
-        r0 = r0 * r0;
-        const float xr = 1.0f - cos_theta;
-        const float x2 = xr * xr;
-        const float refl_p = r0 + (1.0f - r0) * ((x2 * x2) * xr);
-        if (cannot_refract || refl_p > st.seedx) {
-            e_dir_raw = reflect(st.d, nrm);
-            post = false;
-        } else {  // refract(unit_dir, n, ratio), shade.wgsl:148-153
-            const v3 perp = scale(add(un, scale(nrm, cos_theta)), ratio);
-            const float lp = length_x(perp);
-            const float par = -sqrt_x(fabsf(1.0f - (lp * lp)));
-            v = add(perp, scale(nrm, par));
-        }
-    }
-    // ---- post-normalize
-    v3 vn = mk(0.0f, 0.0f, 0.0f);
-    if (post) vn = normalize_x(v);
-    if (miss) {  // miss(), shade.wgsl:189-197, color *= sky
-        const float tt = 0.5f * vn.y + 1.0f;
-        const float omt = (1.0f - tt) * 1.0f;
-        st.color = mul(st.color, mk(omt + tt * 0.5f, omt + tt * 0.7f, omt + tt * 1.0f));
-        return true;
-    }
-    if (refl == RT_LAMBERTIAN) {
-        st.o = pos;  // no offset (shade.wgsl:123)
-        st.d = vn;
-        st.color = mul(st.color, mk(mc.x, mc.y, mc.z));
-    } else {
-        st.o = add(pos, scale(nrm, EPSILON));  // shade.wgsl:139, 182
-        st.d = post ? vn : e_dir_raw;
-        if (refl == RT_METALLIC) st.color = mul(st.color, mk(mc.x, mc.y, mc.z));
-    }
-    ++st.bounce;
-    return false;
-}
 
 #ifdef RT_CHUNK_TRACE
 #define RT_CHUNK_TRACE_MAX (1u << 22)

@@ -14,7 +14,7 @@
 // (both signs, 5 exponents), division on 2^33 random pairs over the domain
 // incl. signed zeros, sqrt on every significand at both exponent parities.
 // Callers keep IEEE results everywhere: operands outside the domain take the
-// plain IEEE operation (rt_kernels.hip guards).
+// plain IEEE operation (rt_dev_math.h guards).
 #pragma once
 
 #include <hip/hip_runtime.h>

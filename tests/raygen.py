@@ -52,7 +52,7 @@ def adversarial_rays(spheres: np.ndarray, n: int, seed: int = 0) -> np.ndarray:
     d = _unit(t + nrm * rng.uniform(-1e-3, 1e-3, k)[:, None])
     out.append(np.hstack([o, d]))
     # 5 far origins looking at the scene
-    # (1e10 > 2^32: those lanes' waves take the IEEE exact test, rt_kernels.hip ray_fast)
+    # (1e10 > 2^32: those lanes' waves take the IEEE exact test, rt_dev_intersect.h ray_fast)
     o = rng.normal(size=(k, 3)) * rng.choice([1e3, 1e4, 1e5, 1e10], k)[:, None]
     tgt = rng.uniform(lo, hi, (k, 3))
     d = _unit(tgt - o)

@@ -1,5 +1,5 @@
 """The kernel's short correctly rounded forms (bevy_raytrace_amd/csrc/rt_math.h,
-guarded in rt_kernels.hip) against the IEEE operations, on the operands their
+guarded in rt_dev_math.h) against the IEEE operations, on the operands their
 guards exist for: signed zeros, denormals, tiny / huge values, inf, NaN, and a
 random bulk. numpy's float32 sqrt and division are IEEE correctly rounded, so
 the bar is bit equality (NaN == NaN)."""
