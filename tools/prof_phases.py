@@ -1,7 +1,7 @@
 """Phase breakdown of rt_render_kernel from the -DRT_PROFILE diagnostic build
 (tools/librt_hip_prof.so), per launch shape / item policy. Shares (not
 absolute times) are meaningful: the stamps perturb the kernel.
-usage: python tools/prof_phases.py [F,n,k,ENV=VAL;...] ..."""
+usage: python tools/prof_phases.py [F,n,k[,ENV=VAL;ENV=VAL]] ..."""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -21,9 +21,9 @@ nsp = len(sc.objects_gpu())
 buf = torch.empty((8, H, W, 4), dtype=torch.float32, device="cuda:0")
 cases = sys.argv[1:] or ["4,1,0", "4,1,0,RT_SPLIT_ALL=1", "4,8,7", "8,8,7"]
 for case in cases:
-    parts = case.split(",")
+    parts = case.split(",", 3)  # F,n,k[,ENV=VAL;ENV=VAL...] (values may hold commas)
     F, n, k = int(parts[0]), int(parts[1]), int(parts[2])
-    env = dict(p.split("=") for p in parts[3:])
+    env = dict(p.split("=", 1) for p in parts[3].split(";")) if len(parts) > 3 else {}
     old = {e: os.environ.get(e) for e in env}
     os.environ.update(env)
     rb = configs.pick_row_block(H, n)
