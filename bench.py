@@ -67,6 +67,8 @@ def parse():
                     help="frames per persistent launch (rt_render_frames_device)")
     ap.add_argument("--reuse-steps", type=int, default=4,
                     help="extra frames timed with primary-hit reuse on (0 = skip)")
+    ap.add_argument("--cull-steps", type=int, default=12,
+                    help="extra frames timed with the culled list, RT_FLAG_CULL (0 = skip)")
     return ap.parse_args()
 
 
@@ -228,6 +230,25 @@ def main():
                  "note": "RT_FLAG_NO_PRIMARY_CACHE off: the pixel-only primary hit is reused "
                          "across a sample block (bit-identical image)"}
 
+    culled = None
+    if args.cull_steps > 0:
+        CULLF = NO_REUSE | abi.RT_FLAG_CULL
+        run(min(args.cull_steps, FPL), CULLF)  # warm-up launch of the timed size
+        cdt, cstats, csizes = timed(args.cull_steps, CULLF)
+        csegs = torch.tensor([float(sum(s["segments"] for s in cstats))], dtype=torch.float64,
+                             device=red_dev)
+        if world > 1:
+            dist.all_reduce(csegs)
+        cval = float(csegs[0].item()) / cdt / 1e6
+        culled = {"value": round(cval, 2), "unit": "Mrays/s",
+                  "frame_ms": round(cdt / args.cull_steps * 1e3, 3),
+                  "kernel_ms_per_launch": round(sum(s["kernel_ms"] for s in cstats)
+                                                / max(1, sum(s["kernel_launches"] for s in cstats)), 3),
+                  "launch_sizes": csizes,
+                  "note": "RT_FLAG_CULL: spatially grouped list with conservative group bounds; "
+                          "identical frames and segment counts, less filter work (no roofline: "
+                          "the brute-force 18*N flops per segment are no longer all executed)"}
+
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -273,7 +294,10 @@ def main():
         "segments_per_frame": int(segs_all / args.steps),
         "traced_segments_per_frame": int(traced_all / args.steps),
         "primary_reuse": reuse,
+        "culled": culled,
     }
+    if culled is not None:
+        culled["speedup"] = round(culled["value"] / value, 3)
     if per_rank is not None:
         out["ranks"] = per_rank
 

@@ -36,6 +36,7 @@ RT_SAMPLE_BLOCK = 8
 RT_FLAG_NO_PRIMARY_CACHE = 0x1
 RT_FLAG_JITTER = 0x2             # opt-in sub-pixel jitter (include/rt_hip.h)
 RT_FLAG_THIN_LENS = 0x4          # opt-in thin-lens sample (generate.wgsl:85-107)
+RT_FLAG_CULL = 0x8               # culled list: group bounds, identical hits (include/rt_hip.h)
 RT_MAX_PENDING = 2          # frames in flight per ctx (rt_render_device / rt_render_async)
 
 SPHERE_DTYPE = np.dtype(
@@ -125,6 +126,7 @@ _PROTOS = {
     "rt_wait": (ctypes.c_int, [_VP, ctypes.POINTER(RtStats)]),
     "rt_assemble_shards": (ctypes.c_int, [_VP, _VP, _U32, _VP, _U32, _U32, _U32, _U32, _VP]),
     "rt_intersect": (ctypes.c_int, [_VP, _VP, _U32, _VP, _VP]),
+    "rt_intersect_ex": (ctypes.c_int, [_VP, _VP, _U32, _U32, _VP, _VP]),
     "rt_update_spheres": (ctypes.c_int, [_VP, _U32, _VP, _U32]),
     "rt_render_progressive": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(RtParams), ctypes.c_int, _VP,
                                              ctypes.POINTER(ctypes.c_uint64)]),
@@ -171,7 +173,9 @@ def load(path=None):
     _share_torch_hip_runtime()
     lib = ctypes.CDLL(path)
     for name, (res, args) in _PROTOS.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:  # an older diagnostic build (tools/); the product exports all
+            continue
         fn.restype = res
         fn.argtypes = args
     if hasattr(lib, "rt_debug_math"):  # internal diagnostic symbol (tests/test_gpu_math.py)
@@ -180,8 +184,34 @@ def load(path=None):
     if hasattr(lib, "rt_debug_counters"):  # internal diagnostic symbol
         lib.rt_debug_counters.restype = ctypes.c_int
         lib.rt_debug_counters.argtypes = [_VP, ctypes.POINTER(ctypes.c_uint64)]
+    if hasattr(lib, "rt_debug_cull_layout"):  # internal, host only (tests/test_cull.py)
+        lib.rt_debug_cull_layout.restype = ctypes.c_int
+        lib.rt_debug_cull_layout.argtypes = [_VP, _U32, _VP, _VP, _U32, _VP, _U32]
     _libs[path] = lib
     return lib
+
+
+def cull_layout(spheres, lib=None):
+    """The culled list the library builds for RT_FLAG_CULL (host only, no
+    device): (perm, bounds, ngroups, nclusters). perm[p] = original index of
+    permuted position p (-1 = pad); bounds (nclusters*8, 4) = (Cx, Cy, Cz, S_B)
+    per group."""
+    import numpy as np
+    lib = lib or load()
+    sp = np.ascontiguousarray(spheres)
+    n = len(sp)
+    counts = (ctypes.c_uint32 * 3)()
+    ptr = sp.ctypes.data_as(_VP) if n else None
+    if lib.rt_debug_cull_layout(ptr, n, counts, None, 0, None, 0) != 0:
+        raise RuntimeError("rt_debug_cull_layout failed")
+    ng, nc, nrec = counts[0], counts[1], counts[2]
+    perm = np.empty(nrec, dtype=np.uint32)
+    bnd = np.empty(nc * 32, dtype=np.float32)
+    if lib.rt_debug_cull_layout(ptr, n, counts, perm.ctypes.data_as(_VP), nrec,
+                                bnd.ctypes.data_as(_VP), nc * 32) != 0:
+        raise RuntimeError("rt_debug_cull_layout failed")
+    b = bnd.reshape(nc, 4, 8).transpose(0, 2, 1).reshape(nc * 8, 4)
+    return perm.astype(np.int64) - (perm == 0xFFFFFFFF) * (1 << 32), b, ng, nc
 
 
 def check(lib, ctx, status):

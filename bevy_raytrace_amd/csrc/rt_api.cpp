@@ -79,6 +79,15 @@ struct rt_ctx {
     std::vector<float> h_S;
     std::vector<float2> h_rm;
     std::vector<rt_material> h_mats;
+    // culled list (RT_FLAG_CULL, build_cull): the records permuted into spatial
+    // groups, clusters of 8 groups, the group bounds and the permutation
+    uint32_t n_c = 0, ngroups_c = 0, nclusters_c = 0;
+    float4* d_grp_c = nullptr;
+    float4* d_sph_c = nullptr;
+    float2* d_rm_c = nullptr;
+    float4* d_bnd_c = nullptr;
+    uint32_t* d_perm_c = nullptr;
+    size_t grp_c_cap = 0, sph_c_cap = 0, rm_c_cap = 0, bnd_c_cap = 0, perm_c_cap = 0;
 
     // frames in flight: RT_MAX_PENDING slots of per-frame work buffers, each
     // with its own stream, so frame i+1 can start while frame i drains
@@ -256,6 +265,11 @@ void rt_destroy(rt_ctx* ctx) {
     hipFree(ctx->d_sph_rm);
     hipFree(ctx->d_mats);
     hipFree(ctx->d_prog);
+    hipFree(ctx->d_grp_c);
+    hipFree(ctx->d_sph_c);
+    hipFree(ctx->d_rm_c);
+    hipFree(ctx->d_bnd_c);
+    hipFree(ctx->d_perm_c);
     for (Frame& f : ctx->fr) {
         hipFree(f.d_block_sums);
         hipFree(f.d_acc);
@@ -278,16 +292,20 @@ void rt_destroy(rt_ctx* ctx) {
 // double (DESIGN.md "Exact filter"). Padded to whole groups plus one; pad
 // records have r^2 = S = -inf, which the filter never passes. Host mirrors
 // are kept so rt_update_* re-packs and uploads only the touched groups.
-static void pack_record(rt_ctx* ctx, uint32_t i, const rt_sphere& s) {
+static void pack_record_to(const rt_sphere& s, float4& q, float& S, float2& rm) {
     const float r = s.radius;
     const float r2 = r * r;  // sqr(s.radius): the f32 value the exact test uses
-    ctx->h_sph[i] = make_float4(s.center[0], s.center[1], s.center[2], r2);
+    q = make_float4(s.center[0], s.center[1], s.center[2], r2);
     const double kS = 1.0 - 0x1p-16 - 0x1p-17;
     const double cx = s.center[0], cy = s.center[1], cz = s.center[2];
-    ctx->h_S[i] = (float)((double)r2 - kS * (cx * cx + cy * cy + cz * cz));
+    S = (float)((double)r2 - kS * (cx * cx + cy * cy + cz * cz));
     float mbits;
     std::memcpy(&mbits, &s.material, 4);
-    ctx->h_rm[i] = make_float2(r, mbits);
+    rm = make_float2(r, mbits);
+}
+
+static void pack_record(rt_ctx* ctx, uint32_t i, const rt_sphere& s) {
+    pack_record_to(s, ctx->h_sph[i], ctx->h_S[i], ctx->h_rm[i]);
 }
 
 // The exact sphere test's short correctly-rounded sqrt/divide forms (rt_math.h)
@@ -307,10 +325,61 @@ static bool scene_fast_ok(const rt_ctx* ctx) {
     return true;
 }
 
+static void pack_group_soa(const float4* q, const float* sg, float4* o);
 static void pack_group(rt_ctx* ctx, size_t g) {
-    const float4* q = &ctx->h_sph[RT_GROUP * g];
-    const float* sg = &ctx->h_S[RT_GROUP * g];
-    float4* o = &ctx->h_grp[RT_GROUP * g];
+    pack_group_soa(&ctx->h_sph[RT_GROUP * g], &ctx->h_S[RT_GROUP * g], &ctx->h_grp[RT_GROUP * g]);
+}
+
+// ---- culled list (RT_FLAG_CULL) ---------------------------------------------
+// The spheres permuted into spatial groups of RT_GROUP (large spheres first, in
+// groups of their own; the rest in Morton order of their centres), clusters of
+// 8 consecutive groups, and per group a bounding sphere (C, R) stored in the
+// group layout -- SoA (Cx[8], Cy[8], Cz[8], S_B[8]) per cluster -- so the
+// kernel runs the same packed filter over a cluster's 8 bounds
+// (rt_dev_intersect.h intersect_world<true>) and walks only the groups some lane
+// passes, against TB = (1 - m - muB)|o|^2, m = 2^-16, muB = 2^-7.
+//
+// Why a skipped group holds no candidate (all quantities of one lane; exact
+// arithmetic unless marked ~). Filter of sphere (c, r): F = hb~^2 + r^2 -
+// (1-m)|o-c|^2 + mu(|o|^2+|c|^2), hb~ = dn~.(o-c), dn~ = (1+eta) d/|d| with
+// |eta| <= 2^-21 (rsq + products); the computed H~ - T~ is F within
+// E = 2^-17 (|o|^2 + |c|^2 + r^2) (the expanded form's rounding, generous;
+// operands finite with |o|, |c|, r <= 2^30, so no overflow). A candidate has
+// H~ >= T~, so with dist = the true distance of c from the ray's line:
+//   dist_i^2 <= r_i^2 (1 + 2^-17) + delta_i,
+//   delta_i = 2^-15 (|o - c_i|^2 + |o|^2 + |c_i|^2)      (m + 2^-19, mu + 2^-17 <= 2^-15)
+// so dist_i <= r_i (1 + 2^-18) + sqrt(delta_i). The line distance is
+// 1-Lipschitz in the point: dist_C <= dist_i + |C - c_i| <= L + sqrt(delta_i)
+// with L = max_i (|C - c_i| + r_i (1 + 2^-18)). Then, with 2ab <= a^2/16 + 16 b^2
+// and |o - c_i|^2 + |o|^2 + |c_i|^2 <= 6 (|o|^2 + |C|^2) + 4 L^2:
+//   dist_C^2 <= (1 + 2^-4) L^2 + 17 delta_i <= (1 + 2^-4 + 2^-8) L^2 + 2^-8 (|o|^2 + |C|^2).
+// The bound's filter with R^2 = (1 + 2^-3) L^2 + 2^-60 and S_B = R^2 - (1 - m - muB)|C|^2:
+//   F_B = hb~_C^2 + R^2 - (1-m)|o-C|^2 + muB (|o|^2 + |C|^2)
+//      >= R^2 - dist_C^2 + (muB - 2^-18)(|o|^2 + |C|^2)
+//      >= (2^-4 - 2^-8) L^2 + 2^-60 + (2^-7 - 2^-8 - 2^-18)(|o|^2 + |C|^2),
+// which exceeds the bound's own rounding 2^-17 (|o|^2 + |C|^2 + R^2): H~_B >= TB~.
+// S_B is rounded up to f32 (a larger S_B only passes more). Groups with a
+// non-finite member, a centre component or radius above 2^30 get C = 0,
+// S_B = +inf (always pass); empty groups S_B = -inf (never); the kernel walks
+// every group for a wave with a lane outside |o_i| <= 2^30, |d|^2 in
+// [2^-100, 2^100].
+struct CullLayout {
+    uint32_t ngroups = 0, nclusters = 0, nrec = 0;
+    std::vector<uint32_t> perm;  // position -> original index (0xFFFFFFFF = pad)
+    std::vector<float4> sph, grp, bnd;
+    std::vector<float2> rm;
+};
+
+static uint32_t morton_spread10(uint32_t v) {
+    v &= 0x3FFu;
+    v = (v | (v << 16)) & 0x030000FFu;
+    v = (v | (v << 8)) & 0x0300F00Fu;
+    v = (v | (v << 4)) & 0x030C30C3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+
+static void pack_group_soa(const float4* q, const float* sg, float4* o) {
     o[0] = make_float4(q[0].x, q[1].x, q[2].x, q[3].x);
     o[1] = make_float4(q[4].x, q[5].x, q[6].x, q[7].x);
     o[2] = make_float4(q[0].y, q[1].y, q[2].y, q[3].y);
@@ -319,6 +388,163 @@ static void pack_group(rt_ctx* ctx, size_t g) {
     o[5] = make_float4(q[4].z, q[5].z, q[6].z, q[7].z);
     o[6] = make_float4(sg[0], sg[1], sg[2], sg[3]);
     o[7] = make_float4(sg[4], sg[5], sg[6], sg[7]);
+}
+
+static float round_up_f32(double v) {
+    if (std::isnan(v)) return INFINITY;
+    float f = (float)v;
+    if ((double)f < v) f = std::nextafter(f, INFINITY);
+    return f;
+}
+
+// sph: (cx, cy, cz, r*r) f32 records, S: their filter constants, rm: (radius,
+// material bits), all in the original order, n records.
+static void cull_layout(const float4* sph, const float* S, const float2* rm, uint32_t n,
+                        CullLayout& L) {
+    auto finite_rec = [&](uint32_t i) {
+        const float4 q = sph[i];
+        return std::isfinite(q.x) && std::isfinite(q.y) && std::isfinite(q.z) && std::isfinite(q.w) &&
+               std::isfinite(S[i]);
+    };
+    // large (or non-finite) spheres go first, in groups of their own
+    std::vector<double> radii;
+    for (uint32_t i = 0; i < n; ++i)
+        if (finite_rec(i)) radii.push_back(std::sqrt((double)sph[i].w));
+    double thr = INFINITY;
+    if (!radii.empty()) {
+        std::nth_element(radii.begin(), radii.begin() + radii.size() / 2, radii.end());
+        thr = 4.0 * radii[radii.size() / 2];
+    }
+    std::vector<uint32_t> big, rest;
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (uint32_t i = 0; i < n; ++i) {
+        if (!finite_rec(i) || std::sqrt((double)sph[i].w) > thr) {
+            big.push_back(i);
+            continue;
+        }
+        rest.push_back(i);
+        const double c[3] = {sph[i].x, sph[i].y, sph[i].z};
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = std::min(lo[k], c[k]);
+            hi[k] = std::max(hi[k], c[k]);
+        }
+    }
+    std::vector<std::pair<uint32_t, uint32_t>> key;  // (Morton code, index)
+    key.reserve(rest.size());
+    for (uint32_t i : rest) {
+        const double c[3] = {sph[i].x, sph[i].y, sph[i].z};
+        uint32_t code = 0;
+        for (int k = 0; k < 3; ++k) {
+            const double ext = hi[k] - lo[k];
+            uint32_t qk = 0;
+            if (ext > 0) {
+                const double t = (c[k] - lo[k]) / ext * 1024.0;
+                qk = t >= 1023.0 ? 1023u : (t <= 0 ? 0u : (uint32_t)t);
+            }
+            code |= morton_spread10(qk) << k;
+        }
+        key.emplace_back(code, i);
+    }
+    std::sort(key.begin(), key.end());
+    std::vector<uint32_t> order = big;
+    while (order.size() % RT_GROUP) order.push_back(0xFFFFFFFFu);
+    for (const auto& kv : key) order.push_back(kv.second);
+    while (order.size() % RT_GROUP) order.push_back(0xFFFFFFFFu);
+    L.ngroups = (uint32_t)(order.size() / RT_GROUP);
+    L.nclusters = (L.ngroups + 7) / 8;
+    const uint32_t slots = L.nclusters * 8;  // groups the walk may visit
+    L.nrec = (slots + 1) * RT_GROUP;         // + one pad group, as the plain list
+    L.perm.assign(L.nrec, 0xFFFFFFFFu);
+    L.sph.assign(L.nrec, make_float4(0.0f, 0.0f, 0.0f, -INFINITY));
+    L.rm.assign(L.nrec, make_float2(0.0f, 0.0f));
+    std::vector<float> Sp(L.nrec, -INFINITY);
+    for (size_t p = 0; p < order.size(); ++p) {
+        const uint32_t i = order[p];
+        if (i == 0xFFFFFFFFu) continue;
+        L.perm[p] = i;
+        L.sph[p] = sph[i];
+        L.rm[p] = rm[i];
+        Sp[p] = S[i];
+    }
+    L.grp.assign(L.nrec, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    for (uint32_t g = 0; g < L.nrec / RT_GROUP; ++g)
+        pack_group_soa(&L.sph[RT_GROUP * g], &Sp[RT_GROUP * g], &L.grp[RT_GROUP * g]);
+    // group bounds, SoA per cluster
+    const double kB = 1.0 - 0x1p-16 - 0x1p-7;
+    std::vector<float4> bc(slots * 8, make_float4(0.0f, 0.0f, 0.0f, -INFINITY));  // (C, S_B) per group
+    std::vector<float> bs(slots * 8, -INFINITY);
+    for (uint32_t g = 0; g < slots; ++g) {
+        double blo[3] = {INFINITY, INFINITY, INFINITY}, bhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        bool any = false, wild = false;
+        for (uint32_t j = 0; j < RT_GROUP; ++j) {
+            const uint32_t i = L.perm[RT_GROUP * g + j];
+            if (i == 0xFFFFFFFFu) continue;
+            any = true;
+            const float4 q = sph[i];
+            if (!finite_rec(i) || std::fabs(q.x) > 0x1p30f || std::fabs(q.y) > 0x1p30f ||
+                std::fabs(q.z) > 0x1p30f || q.w > 0x1p60f) {
+                wild = true;
+                continue;
+            }
+            const double c[3] = {q.x, q.y, q.z};
+            for (int k = 0; k < 3; ++k) {
+                blo[k] = std::min(blo[k], c[k]);
+                bhi[k] = std::max(bhi[k], c[k]);
+            }
+        }
+        float4 C = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        float SB = -INFINITY;  // empty: never passes
+        if (any && wild) {
+            SB = INFINITY;  // always passes
+        } else if (any) {
+            C = make_float4((float)((blo[0] + bhi[0]) * 0.5), (float)((blo[1] + bhi[1]) * 0.5),
+                            (float)((blo[2] + bhi[2]) * 0.5), 0.0f);
+            double Lm = 0.0;
+            for (uint32_t j = 0; j < RT_GROUP; ++j) {
+                const uint32_t i = L.perm[RT_GROUP * g + j];
+                if (i == 0xFFFFFFFFu) continue;
+                const float4 q = sph[i];
+                const double dx = (double)q.x - C.x, dy = (double)q.y - C.y, dz = (double)q.z - C.z;
+                const double rho = std::sqrt(dx * dx + dy * dy + dz * dz) * (1.0 + 0x1p-40);
+                Lm = std::max(Lm, rho + std::sqrt((double)q.w) * (1.0 + 0x1p-18));
+            }
+            const double R2 = (1.0 + 0x1p-3) * Lm * Lm * (1.0 + 0x1p-40) + 0x1p-60;
+            const double CC = (double)C.x * C.x + (double)C.y * C.y + (double)C.z * C.z;
+            SB = round_up_f32((R2 - kB * CC) * (1.0 + 0x1p-40) + 0x1p-60);
+        }
+        bc[g] = C;
+        bs[g] = SB;
+    }
+    L.bnd.assign((size_t)L.nclusters * 8, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    for (uint32_t k = 0; k < L.nclusters; ++k) {
+        float4 q[8];
+        for (int j = 0; j < 8; ++j) q[j] = bc[k * 8 + j];
+        pack_group_soa(q, &bs[k * 8], &L.bnd[(size_t)k * 8]);
+    }
+}
+
+// Rebuild and upload the culled list from the host mirrors (set_scene / update).
+static int build_cull(rt_ctx* ctx) {
+    CullLayout L;
+    cull_layout(ctx->h_sph.data(), ctx->h_S.data(), ctx->h_rm.data(), ctx->n, L);
+    int rc = ensure(ctx, &ctx->d_grp_c, &ctx->grp_c_cap, sizeof(float4) * L.nrec);
+    if (!rc) rc = ensure(ctx, &ctx->d_sph_c, &ctx->sph_c_cap, sizeof(float4) * L.nrec);
+    if (!rc) rc = ensure(ctx, &ctx->d_rm_c, &ctx->rm_c_cap, sizeof(float2) * L.nrec);
+    if (!rc) rc = ensure(ctx, &ctx->d_bnd_c, &ctx->bnd_c_cap, sizeof(float4) * L.bnd.size());
+    if (!rc) rc = ensure(ctx, &ctx->d_perm_c, &ctx->perm_c_cap, sizeof(uint32_t) * L.nrec);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpy(ctx->d_grp_c, L.grp.data(), sizeof(float4) * L.nrec, hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(ctx->d_sph_c, L.sph.data(), sizeof(float4) * L.nrec, hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(ctx->d_rm_c, L.rm.data(), sizeof(float2) * L.nrec, hipMemcpyHostToDevice));
+    if (!L.bnd.empty())
+        HIP_TRY(ctx, hipMemcpy(ctx->d_bnd_c, L.bnd.data(), sizeof(float4) * L.bnd.size(),
+                               hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(ctx->d_perm_c, L.perm.data(), sizeof(uint32_t) * L.nrec,
+                           hipMemcpyHostToDevice));
+    ctx->n_c = L.ngroups * RT_GROUP;
+    ctx->ngroups_c = L.ngroups;
+    ctx->nclusters_c = L.nclusters;
+    return RT_OK;
 }
 
 static int check_materials(rt_ctx* ctx, const rt_material* mats, uint32_t first, uint32_t count) {
@@ -388,6 +614,8 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n, const rt_mat
     ctx->ngroups = ngroups;
     ctx->m = m;
     ctx->scene_fast = scene_fast_ok(ctx);
+    rc = build_cull(ctx);
+    if (rc) return rc;
     ctx->has_scene = true;
     return RT_OK;
 }
@@ -414,7 +642,7 @@ int rt_update_spheres(rt_ctx* ctx, uint32_t first, const rt_sphere* spheres, uin
     HIP_TRY(ctx, hipMemcpy(ctx->d_grp + RT_GROUP * g0, &ctx->h_grp[RT_GROUP * g0],
                            sizeof(float4) * RT_GROUP * (g1 - g0), hipMemcpyHostToDevice));
     ctx->scene_fast = scene_fast_ok(ctx);
-    return RT_OK;
+    return build_cull(ctx);
 }
 
 int rt_update_materials(rt_ctx* ctx, uint32_t first, const rt_material* materials,
@@ -568,8 +796,14 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     K_.shard_count = K;
     K_.shard_index = p.shard_index;
     K_.npix = npix;
-    K_.nspheres = ctx->n;
-    K_.ngroups = ctx->ngroups;
+    const bool cull = (p.flags & RT_FLAG_CULL) != 0;
+    K_.nspheres = cull ? ctx->n_c : ctx->n;
+    K_.ngroups = cull ? ctx->ngroups_c : ctx->ngroups;
+    if (cull) {
+        K_.bnd = ctx->d_bnd_c;
+        K_.perm = ctx->d_perm_c;
+        K_.nclusters = ctx->nclusters_c;
+    }
     K_.scene_fast = ctx->scene_fast && env_flag("RT_FAST_EXACT", true) ? 1u : 0u;
     K_.flags = p.flags;
     std::memcpy(K_.T, cam->transform, sizeof(K_.T));
@@ -596,8 +830,11 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     // the drain: switch while k rays cost less sphere-parallel. RT_WIDE_MAX
     // overrides (0 = never).
     {
-        const uint64_t per_ray = (uint64_t)((ctx->n + 63) / 64) * 32 + 48;
-        uint64_t k = ((uint64_t)ctx->ngroups * 34 + 300) / per_ray;
+        const uint64_t per_ray = (uint64_t)((K_.nspheres + 63) / 64) * 32 + 48;
+        // culled walk: the cluster bounds plus, measured on the RTIOW scene,
+        // about a quarter of the groups
+        uint64_t k = ((cull ? (uint64_t)K_.nclusters * 40 + (uint64_t)K_.ngroups * 34 / 4
+                            : (uint64_t)K_.ngroups * 34) + 300) / per_ray;
         if (k > 16) k = 16;
         const char* e = getenv("RT_WIDE_MAX");
         if (e && *e) k = strtoul(e, nullptr, 10);
@@ -642,7 +879,9 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         const uint64_t tail_items = 2ull * RT_WAVE_CHUNK * grid * (RT_BLOCK_THREADS / 64);
         K_.tail_start = (uint32_t)(items > tail_items ? items - tail_items : 0);
         HIP_TRY(ctx, hipEventRecord(f.ev[2 * i], stream));
-        HIP_TRY(ctx, rt_launch_render(&K_, ctx->d_grp, ctx->d_sph, ctx->d_sph_rm, ctx->d_mats, f.d_pd,
+        HIP_TRY(ctx, rt_launch_render(&K_, cull ? ctx->d_grp_c : ctx->d_grp,
+                                      cull ? ctx->d_sph_c : ctx->d_sph,
+                                      cull ? ctx->d_rm_c : ctx->d_sph_rm, ctx->d_mats, f.d_pd,
                                       f.d_block_sums,
                                       f.d_counters + RT_CNT_WORK_OFFSET + i,
                                       reinterpret_cast<unsigned long long*>(f.d_counters),
@@ -844,6 +1083,11 @@ int rt_assemble_shards(rt_ctx* ctx, const float* gathered_device, uint32_t max_r
 }
 
 int rt_intersect(rt_ctx* ctx, const float* rays, uint32_t n, int32_t* hit_index, float* hit_t) {
+    return rt_intersect_ex(ctx, rays, n, 0u, hit_index, hit_t);
+}
+
+int rt_intersect_ex(rt_ctx* ctx, const float* rays, uint32_t n, uint32_t flags, int32_t* hit_index,
+                    float* hit_t) {
     if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_intersect: ctx is NULL");
     if (!ctx->has_scene) return fail(ctx, RT_ERR_NO_SCENE, "rt_intersect before rt_set_scene");
     if (n == 0) return RT_OK;
@@ -858,10 +1102,15 @@ int rt_intersect(rt_ctx* ctx, const float* rays, uint32_t n, int32_t* hit_index,
     char* b = (char*)buf;
     hipError_t e = hipMemcpyAsync(b, rays, rb, hipMemcpyHostToDevice, ctx->stream);
     if (e == hipSuccess)
-        e = rt_launch_intersect(ctx->d_grp, ctx->d_sph, ctx->ngroups,
+    {
+        const bool cull = (flags & RT_FLAG_CULL) != 0 && ctx->d_bnd_c;
+        e = rt_launch_intersect(cull ? ctx->d_grp_c : ctx->d_grp, cull ? ctx->d_sph_c : ctx->d_sph,
+                                cull ? ctx->ngroups_c : ctx->ngroups,
                                 ctx->scene_fast && env_flag("RT_FAST_EXACT", true) ? 1u : 0u,
-                                (const float*)b, n,
-                                (int*)(b + rb), (float*)(b + rb + ob), ctx->stream);
+                                (const float*)b, n, (int*)(b + rb), (float*)(b + rb + ob),
+                                cull ? ctx->d_bnd_c : nullptr, cull ? ctx->d_perm_c : nullptr,
+                                cull ? ctx->nclusters_c : 0u, ctx->stream);
+    }
     if (e == hipSuccess)
         e = hipMemcpyAsync(hit_index, b + rb, ob, hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess)
@@ -871,6 +1120,28 @@ int rt_intersect(rt_ctx* ctx, const float* rays, uint32_t n, int32_t* hit_index,
     if (e != hipSuccess)
         return fail(ctx, RT_ERR_DEVICE, "rt_intersect: %s", hipGetErrorString(e));
     return RT_OK;
+}
+
+// Internal (not in include/rt_hip.h; tests/test_cull.py, CPU): the culled
+// layout of a sphere list as build_cull makes it, without a device.
+// counts[0..2] = (groups, clusters, records); perm (records entries) and bnd
+// (clusters * 32 floats: per cluster Cx[8] Cy[8] Cz[8] S_B[8]) are filled when
+// their capacities suffice. Returns 0, or -1 on a NULL argument.
+int rt_debug_cull_layout(const rt_sphere* spheres, uint32_t n, uint32_t* counts, uint32_t* perm,
+                         uint32_t perm_cap, float* bnd, uint32_t bnd_cap) {
+    if (!counts || (n && !spheres)) return -1;
+    std::vector<float4> q(n);
+    std::vector<float> S(n);
+    std::vector<float2> rm(n);
+    for (uint32_t i = 0; i < n; ++i) pack_record_to(spheres[i], q[i], S[i], rm[i]);
+    CullLayout L;
+    cull_layout(q.data(), S.data(), rm.data(), n, L);
+    counts[0] = L.ngroups;
+    counts[1] = L.nclusters;
+    counts[2] = L.nrec;
+    if (perm && perm_cap >= L.nrec) std::copy(L.perm.begin(), L.perm.end(), perm);
+    if (bnd && bnd_cap >= L.bnd.size() * 4) std::memcpy(bnd, L.bnd.data(), L.bnd.size() * sizeof(float4));
+    return 0;
 }
 
 // Internal (not in include/rt_hip.h): the 16 diagnostic counters of the last

@@ -57,9 +57,16 @@ __device__ uint32_t g_prof_dummy;
 //  - |numerator| < 2^-60 (incl. +-0): IEEE and short quotients both have
 //    |root| < 2^-40 < EPSILON and are rejected alike.
 // Otherwise the IEEE operations (sqrtf, '/'). ya = rt_recip_rn(a) when FAST.
-template <bool FAST>
+//
+// CULL (the culled list of rt_render_cull_kernel, rt_api.cpp build_cull): the
+// list is spatially permuted, so the winner is the lexicographic minimum of
+// (t, original index perm[idx]) -- the sequential strict-`<` scan's answer in
+// the original order (intersect.wgsl:137) whatever order the candidates come
+// in. perm is read only on an exact tie.
+template <bool FAST, bool CULL>
 __device__ __forceinline__ void exact_body(float4 s, int idx, v3 o, v3 d, float a, float ya,
-                                           float& best_t, int& best_i EXACT_ARGS) {
+                                           float& best_t, int& best_i,
+                                           const uint32_t* perm EXACT_ARGS) {
     EXACT_COUNT(0);
     const v3 oc = mk(o.x - s.x, o.y - s.y, o.z - s.z);
     const float half_b = dot(oc, d);
@@ -90,18 +97,26 @@ __device__ __forceinline__ void exact_body(float4 s, int idx, v3 o, v3 d, float 
         root = FAST ? rt_div_rn(-half_b + sqrtd, a, ya) : (-half_b + sqrtd) / a;
         if (root < EPSILON || VERY_FAR < root) return;
     }
-    if (root < best_t) {
+    if (CULL) {
+        if (root <= best_t &&
+            (root < best_t || (best_i >= 0 && perm[idx] < perm[best_i]))) {
+            best_t = root;
+            best_i = idx;
+        }
+    } else if (root < best_t) {
         best_t = root;
         best_i = idx;
     }
 }
 
+template <bool CULL>
 __device__ __forceinline__ void exact_test(float4 s, int idx, v3 o, v3 d, float a, float ya,
-                                           bool fast, float& best_t, int& best_i EXACT_ARGS) {
+                                           bool fast, float& best_t, int& best_i,
+                                           const uint32_t* perm EXACT_ARGS) {
     if (fast)
-        exact_body<true>(s, idx, o, d, a, ya, best_t, best_i EXACT_PASS);
+        exact_body<true, CULL>(s, idx, o, d, a, ya, best_t, best_i, perm EXACT_PASS);
     else
-        exact_body<false>(s, idx, o, d, a, ya, best_t, best_i EXACT_PASS);
+        exact_body<false, CULL>(s, idx, o, d, a, ya, best_t, best_i, perm EXACT_PASS);
 }
 
 // The ray side of the short-math domain (exact_body), for the whole wave.
@@ -264,10 +279,11 @@ __device__ __forceinline__ uint32_t cand_mask8(f2 g01, f2 g23, f2 g45, f2 g67, f
 }
 #endif
 
-template <bool FAST>
+template <bool FAST, bool CULL>
 __device__ __forceinline__ void drain_list(const uint32_t* cq, uint32_t cnt,
                                            const float4* __restrict__ sph, v3 o, v3 d, float a,
-                                           float ya, float& best_t, int& best_i EXACT_ARGS) {
+                                           float ya, float& best_t, int& best_i,
+                                           const uint32_t* perm EXACT_ARGS) {
     const uint32_t lane = __lane_id();
     for (uint32_t k = 0; k < cnt; ++k) {
         const uint32_t e = cq[k * 64 + lane];
@@ -276,21 +292,24 @@ __device__ __forceinline__ void drain_list(const uint32_t* cq, uint32_t cnt,
         while (m) {
             const uint32_t j = __builtin_ctz(m);
             m &= m - 1;
-            exact_body<FAST>(sph[base + j], (int)(base + j), o, d, a, ya, best_t, best_i EXACT_PASS);
+            exact_body<FAST, CULL>(sph[base + j], (int)(base + j), o, d, a, ya, best_t, best_i,
+                                   perm EXACT_PASS);
         }
     }
 }
 
 // Run the exact test for every queued candidate of this lane, in list order.
 // Queue entries are (group << 8 | 8-bit candidate mask), one column per lane.
+template <bool CULL>
 __device__ __forceinline__ void drain_candidates(const uint32_t* cq, uint32_t cnt,
                                                  const float4* __restrict__ sph, v3 o, v3 d,
                                                  float a, bool fast, float& best_t,
-                                                 int& best_i EXACT_ARGS) {
+                                                 int& best_i, const uint32_t* perm EXACT_ARGS) {
     if (fast)
-        drain_list<true>(cq, cnt, sph, o, d, a, rt_recip_rn(a), best_t, best_i EXACT_PASS);
+        drain_list<true, CULL>(cq, cnt, sph, o, d, a, rt_recip_rn(a), best_t, best_i,
+                               perm EXACT_PASS);
     else
-        drain_list<false>(cq, cnt, sph, o, d, a, a, best_t, best_i EXACT_PASS);
+        drain_list<false, CULL>(cq, cnt, sph, o, d, a, a, best_t, best_i, perm EXACT_PASS);
 }
 
 // Closest hit over the whole list (intersect.wgsl:133-143).
@@ -303,14 +322,30 @@ __device__ __forceinline__ void drain_candidates(const uint32_t* cq, uint32_t cn
 // runs the exact reference test on the queued candidates in list order, so the
 // wave pays for max-over-lanes candidates, not for their union.
 // Returns the best index (-1 = miss) and t.
+//
+// CULL (rt_render_cull_kernel; the list permuted into spatial groups and
+// clusters of 8 groups by rt_api.cpp build_cull): before its 8 groups, a
+// cluster's 8 group BOUNDS -- spheres (C_j, R_j) stored exactly like a group
+// of spheres, S_j = R_j^2 - (1 - m - muB)|C_j|^2 -- go through the same packed
+// filter against the threshold TB = (1 - m - muB)|o|^2, and only the groups
+// some lane of the wave passes are filtered. Each bound dominates its members'
+// filter values (proof in rt_api.cpp build_cull: R_j^2 = (1 + 2^-3) L^2 with
+// L = max(|C_j - c_i| + r_i (1 + 2^-18)), muB = 2^-7): a lane with a candidate
+// in group j passes bound j, so a skipped group held no candidate of any lane
+// and the candidate lists -- hence the hits -- are those of the full walk.
+// The proof needs finite, moderate operands: a wave with a lane outside
+// |o_i| <= 2^30, |d|^2 in [2^-100, 2^100] walks every group (bounds of groups
+// with huge or non-finite members are "always pass" on the host side).
+template <bool CULL>
 __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
                                                const float4* __restrict__ sph, uint32_t ngroups,
                                                uint32_t scene_fast, v3 o, v3 d, float& t_out,
-                                               uint32_t* cq
+                                               uint32_t* cq,
 #ifdef RT_PROFILE
-                                               , Prof& prof_
+                                               Prof& prof_,
 #endif
-                                               ) {
+                                               const float4* bnd, const uint32_t* perm,
+                                               uint32_t nclusters) {
     const float l = sqrt_x(dot(d, d));
     const float a = l * l;  // sqr(length(r.dir)), intersect.wgsl:98
     const bool fast = ray_fast(scene_fast, o, a);
@@ -332,10 +367,13 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
     // whatever the alias analysis concludes about other stores
 #if defined(__HIP_DEVICE_COMPILE__)
     const cfloat4* gp = (const cfloat4*)(uintptr_t)grp;
+    const cfloat4* bp = (const cfloat4*)(uintptr_t)bnd;
 #else
     const float4* gp = grp;  // host pass: never executed
+    const float4* bp = bnd;
 #endif
-    for (uint32_t g = 0; g < ngroups; ++g) {
+    // The filter of one group of 8 (pass 1 of the walk).
+    auto group = [&](uint32_t g) __attribute__((always_inline)) {
         const auto* p = gp + (size_t)g * 8;
         const float4 X0 = p[0], X1 = p[1], Y0 = p[2], Y1 = p[3];
         const float4 Z0 = p[4], Z1 = p[5], S0 = p[6], S1 = p[7];
@@ -361,7 +399,7 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
             PROF_ADD(5, 1);
             if (rt_ballot(cnt >= RT_CQ_CAP) != 0) {  // a lane's queue is full: drain all
                 PROF_ADD(11, 1);
-                drain_candidates(cq, cnt, sph, o, d, a, fast, best_t, best_i EXACT_PASS);
+                drain_candidates<CULL>(cq, cnt, sph, o, d, a, fast, best_t, best_i, perm EXACT_PASS);
                 cnt = 0;
             }
             const float T = RT_T;
@@ -377,12 +415,63 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
                 ++cnt;
             }
         }
+    };
+    if constexpr (CULL) {
+        const float oo = __builtin_fmaf(o.z, o.z, __builtin_fmaf(o.y, o.y, o.x * o.x));
+        const float TB = (1.0f - 0x1p-16f - 0x1p-7f) * oo;  // bound threshold, muB = 2^-7
+        const float om = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+        const bool cull_ok = (rt_ballot(!(om <= 0x1p30f)) | rt_ballot(!(a >= 0x1p-100f)) |
+                              rt_ballot(!(a <= 0x1p100f))) == 0;
+        for (uint32_t k = 0; k < nclusters; ++k) {
+            uint32_t gm = 0xFFu;  // groups of cluster k to filter
+            if (cull_ok) {
+                const auto* p = bp + (size_t)k * 8;
+                const float4 X0 = p[0], X1 = p[1], Y0 = p[2], Y1 = p[3];
+                const float4 Z0 = p[4], Z1 = p[5], S0 = p[6], S1 = p[7];
+#if defined(RT_ASM_FILTER) && defined(__HIP_DEVICE_COMPILE__)
+                f2 b01, b23, b45, b67;
+                float bmax;
+                filter8(RP, f2{X0.x, X0.y}, f2{X0.z, X0.w}, f2{X1.x, X1.y}, f2{X1.z, X1.w},
+                        f2{Y0.x, Y0.y}, f2{Y0.z, Y0.w}, f2{Y1.x, Y1.y}, f2{Y1.z, Y1.w},
+                        f2{Z0.x, Z0.y}, f2{Z0.z, Z0.w}, f2{Z1.x, Z1.y}, f2{Z1.z, Z1.w},
+                        f2{S0.x, S0.y}, f2{S0.z, S0.w}, f2{S1.x, S1.y}, f2{S1.z, S1.w}, b01, b23,
+                        b45, b67, bmax);
+#else
+                const f2 b01 = filter2(f2{X0.x, X0.y}, f2{Y0.x, Y0.y}, f2{Z0.x, Z0.y}, f2{S0.x, S0.y}, R);
+                const f2 b23 = filter2(f2{X0.z, X0.w}, f2{Y0.z, Y0.w}, f2{Z0.z, Z0.w}, f2{S0.z, S0.w}, R);
+                const f2 b45 = filter2(f2{X1.x, X1.y}, f2{Y1.x, Y1.y}, f2{Z1.x, Z1.y}, f2{S1.x, S1.y}, R);
+                const f2 b67 = filter2(f2{X1.z, X1.w}, f2{Y1.z, Y1.w}, f2{Z1.z, Z1.w}, f2{S1.z, S1.w}, R);
+                const float bmax = fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(b01.x, b01.y), b23.x),
+                                                             b23.y), b45.x), b45.y), b67.x), b67.y);
+#endif
+                gm = 0u;
+                if (rt_ballot(bmax >= TB) != 0) {
+                    gm = (rt_ballot(b01.x >= TB) != 0 ? 0x01u : 0u) |
+                         (rt_ballot(b01.y >= TB) != 0 ? 0x02u : 0u) |
+                         (rt_ballot(b23.x >= TB) != 0 ? 0x04u : 0u) |
+                         (rt_ballot(b23.y >= TB) != 0 ? 0x08u : 0u) |
+                         (rt_ballot(b45.x >= TB) != 0 ? 0x10u : 0u) |
+                         (rt_ballot(b45.y >= TB) != 0 ? 0x20u : 0u) |
+                         (rt_ballot(b67.x >= TB) != 0 ? 0x40u : 0u) |
+                         (rt_ballot(b67.y >= TB) != 0 ? 0x80u : 0u);
+                }
+            }
+            while (gm) {
+                const uint32_t j = __builtin_ctz(gm);
+                gm &= gm - 1u;
+                group(k * 8u + j);
+            }
+        }
+    } else {
+        (void)bp;
+        (void)nclusters;
+        for (uint32_t g = 0; g < ngroups; ++g) group(g);
     }
     PROF_MARK(1);
 #ifdef RT_PROFILE
     PROF_ADD(6, wave_max_u32(cnt));
 #endif
-    drain_candidates(cq, cnt, sph, o, d, a, fast, best_t, best_i EXACT_PASS);
+    drain_candidates<CULL>(cq, cnt, sph, o, d, a, fast, best_t, best_i, perm EXACT_PASS);
     PROF_MARK(2);
 #ifdef RT_PROFILE
     PROF_ADD(13, wave_max_u32(ecnt[0]));
@@ -404,9 +493,11 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
 // their spheres in list order with the strict `<`; the wave reduction then
 // takes the smallest t, ties to the smallest index -- exactly the answer of
 // the sequential strict-`<` scan (intersect.wgsl:133-143).
+// CULL: the permuted list; ties go to the smaller original index perm[i].
+template <bool CULL>
 __device__ __forceinline__ void intersect_wide(const float4* __restrict__ sph, uint32_t n,
                                                uint32_t scene_fast, uint64_t active, v3 o, v3 d,
-                                               int& hi, float& t) {
+                                               int& hi, float& t, const uint32_t* perm) {
     const uint32_t lane = __lane_id();
     while (active) {
         const int src = (int)__builtin_ctzll(active);
@@ -422,15 +513,21 @@ __device__ __forceinline__ void intersect_wide(const float4* __restrict__ sph, u
         for (uint32_t i = lane; i < n; i += 64) {
 #ifdef RT_PROFILE
             uint32_t ecnt[2];
-            exact_test(sph[i], (int)i, ro, rd, a, ya, fast, bt, bi, ecnt);
+            exact_test<CULL>(sph[i], (int)i, ro, rd, a, ya, fast, bt, bi, perm, ecnt);
 #else
-            exact_test(sph[i], (int)i, ro, rd, a, ya, fast, bt, bi);
+            exact_test<CULL>(sph[i], (int)i, ro, rd, a, ya, fast, bt, bi, perm);
 #endif
         }
         for (int off = 32; off > 0; off >>= 1) {
             const float ot = __shfl_xor(bt, off);
             const int oi = __shfl_xor(bi, off);
-            if (ot < bt || (ot == bt && (uint32_t)oi < (uint32_t)bi)) {
+            bool take;
+            if (CULL)  // key: original index, a miss (-1) last
+                take = ot < bt || (ot == bt && (oi < 0 ? 0xFFFFFFFFu : perm[oi]) <
+                                                   (bi < 0 ? 0xFFFFFFFFu : perm[bi]));
+            else
+                take = ot < bt || (ot == bt && (uint32_t)oi < (uint32_t)bi);
+            if (take) {
                 bt = ot;
                 bi = oi;
             }

@@ -73,6 +73,11 @@ struct KParams {
     uint32_t prefetch;  // 1: waves prefetch their next work chunk (RT_PREFETCH=0 off)
     uint32_t prio_mode;   // s_setprio rotation (RT_PRIO): 0 off, 1 by iteration, 3 by wall time
     uint32_t prio_shift;  // mode 3: one step per 2^prio_shift ticks of 10 ns (RT_PRIO_SHIFT)
+    // culled list (RT_FLAG_CULL; rt_render_cull_kernel): grp / sph / sph_rm
+    // are then the permuted arrays, nspheres / ngroups their padded sizes
+    const float4* bnd;      // per cluster of 8 groups: the 8 group bounds, SoA like a group; null = brute force
+    const uint32_t* perm;   // permuted position -> original sphere index (ties)
+    uint32_t nclusters;
 };
 
 // Row block b of the image -> owning shard (rt_params: serpentine deal).
@@ -100,6 +105,7 @@ hipError_t rt_launch_assemble(const float4* gathered, uint32_t max_rows, float4*
                               uint32_t shard_count, hipStream_t stream);
 hipError_t rt_launch_intersect(const float4* grp, const float4* sph, uint32_t ngroups,
                                uint32_t scene_fast, const float* rays, uint32_t n, int* out_i, float* out_t,
+                               const float4* bnd, const uint32_t* perm, uint32_t nclusters,
                                hipStream_t stream);
 hipError_t rt_render_occupancy(int* blocks_per_cu);
 hipError_t rt_launch_primary(const KParams* P, float4* pd, hipStream_t stream);

@@ -96,8 +96,12 @@ __device__ __forceinline__ const KParams& fresh_params() {
 }
 #endif
 
-__global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_render_kernel(
-    KParams P, const float4* grp, const float4* __restrict__ sph,
+// The persistent render loop; CULL = false is rt_render_kernel (the brute-force
+// walk of the headline), CULL = true rt_render_cull_kernel (the permuted list
+// with group bounds, P.bnd / P.perm / P.nclusters; identical results).
+template <bool CULL>
+__device__ __forceinline__ void render_body(
+    const KParams& P, const float4* grp, const float4* __restrict__ sph,
     const float2* __restrict__ sph_rm, const rt_material* __restrict__ mats,
     const PixelEntry* __restrict__ tab, float4* __restrict__ block_sums,
     uint32_t* __restrict__ work_counter,
@@ -259,13 +263,13 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
         float t = VERY_FAR;
         const uint64_t live = rt_ballot(has_item);
         if ((uint32_t)__popcll(live) <= P.wide_max) {  // nearly empty wave: sphere-parallel
-            intersect_wide(sph, P.nspheres, P.scene_fast, live, st.o, st.d, hi, t);
+            intersect_wide<CULL>(sph, P.nspheres, P.scene_fast, live, st.o, st.d, hi, t, P.perm);
         } else if (has_item) {
-            hi = intersect_world(grp, sph, P.ngroups, P.scene_fast, st.o, st.d, t, cq
+            hi = intersect_world<CULL>(grp, sph, P.ngroups, P.scene_fast, st.o, st.d, t, cq,
 #ifdef RT_PROFILE
-                                 , prof_
+                                       prof_,
 #endif
-                                 );
+                                       P.bnd, P.perm, P.nclusters);
         }
         traced += (uint32_t)__popcll(live);
         if (has_item) {
@@ -358,6 +362,24 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
     }
 }
 
+__global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_render_kernel(
+    KParams P, const float4* grp, const float4* __restrict__ sph,
+    const float2* __restrict__ sph_rm, const rt_material* __restrict__ mats,
+    const PixelEntry* __restrict__ tab, float4* __restrict__ block_sums,
+    uint32_t* __restrict__ work_counter,
+    unsigned long long* __restrict__ seg_counter, unsigned long long* __restrict__ dbg) {
+    render_body<false>(P, grp, sph, sph_rm, mats, tab, block_sums, work_counter, seg_counter, dbg);
+}
+
+__global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_render_cull_kernel(
+    KParams P, const float4* grp, const float4* __restrict__ sph,
+    const float2* __restrict__ sph_rm, const rt_material* __restrict__ mats,
+    const PixelEntry* __restrict__ tab, float4* __restrict__ block_sums,
+    uint32_t* __restrict__ work_counter,
+    unsigned long long* __restrict__ seg_counter, unsigned long long* __restrict__ dbg) {
+    render_body<true>(P, grp, sph, sph_rm, mats, tab, block_sums, work_counter, seg_counter, dbg);
+}
+
 // Pixel table, once per frame: for the k-th pixel of the processing order
 // its shard pixel index, global (x, y) and primary ray direction
 // (generate.wgsl:66-126; the direction depends on the pixel only: lens
@@ -379,10 +401,12 @@ __global__ void rt_primary_kernel(KParams P, PixelEntry* __restrict__ tab) {
 }
 
 // Batch closest-hit query (rt_intersect): one ray per lane, same intersect_world.
-__global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_kernel(
+// CULL: the permuted list with its bounds; the index returned is the original.
+template <bool CULL>
+__device__ __forceinline__ void intersect_body(
     const float4* __restrict__ grp, const float4* __restrict__ sph, uint32_t ngroups,
     uint32_t scene_fast, const float* __restrict__ rays, uint32_t n, int* __restrict__ out_i,
-    float* __restrict__ out_t) {
+    float* __restrict__ out_t, const float4* bnd, const uint32_t* perm, uint32_t nclusters) {
     __shared__ uint32_t s_cq[RT_BLOCK_THREADS * RT_CQ_CAP];
     uint32_t* cq = s_cq + (threadIdx.x / 64u) * (64u * RT_CQ_CAP);
 #ifdef RT_PROFILE
@@ -393,15 +417,28 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_kernel(
     if (i >= n) return;
     const float* r = rays + (size_t)i * 6;
     float t;
-    const int hi = intersect_world(grp, sph, ngroups, scene_fast, mk(r[0], r[1], r[2]),
-                                   mk(r[3], r[4], r[5]),
-                                   t, cq
+    const int hi = intersect_world<CULL>(grp, sph, ngroups, scene_fast, mk(r[0], r[1], r[2]),
+                                         mk(r[3], r[4], r[5]), t, cq,
 #ifdef RT_PROFILE
-                                   , prof_
+                                         prof_,
 #endif
-                                   );
-    out_i[i] = hi;
+                                         bnd, perm, nclusters);
+    out_i[i] = (CULL && hi >= 0) ? (int)perm[hi] : hi;
     out_t[i] = t;
+}
+
+__global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_kernel(
+    const float4* __restrict__ grp, const float4* __restrict__ sph, uint32_t ngroups,
+    uint32_t scene_fast, const float* __restrict__ rays, uint32_t n, int* __restrict__ out_i,
+    float* __restrict__ out_t) {
+    intersect_body<false>(grp, sph, ngroups, scene_fast, rays, n, out_i, out_t, nullptr, nullptr, 0);
+}
+
+__global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_cull_kernel(
+    const float4* __restrict__ grp, const float4* __restrict__ sph, uint32_t ngroups,
+    uint32_t scene_fast, const float* __restrict__ rays, uint32_t n, int* __restrict__ out_i,
+    float* __restrict__ out_t, const float4* bnd, const uint32_t* perm, uint32_t nclusters) {
+    intersect_body<true>(grp, sph, ngroups, scene_fast, rays, n, out_i, out_t, bnd, perm, nclusters);
 }
 
 // Fold one frame's block sums (launch frame f = blockIdx.y) into acc (block
@@ -509,9 +546,14 @@ hipError_t rt_launch_render(const KParams* P, const float4* grp, const float4* s
 #else
     const size_t dyn = 0;
 #endif
-    hipLaunchKernelGGL(rt_render_kernel, dim3(grid), dim3(RT_BLOCK_THREADS), dyn, stream, *P, grp,
-                       sph, sph_rm, mats, reinterpret_cast<const PixelEntry*>(pd), block_sums,
-                       work_counter, seg_counter, seg_counter + 2);
+    if (P->bnd)
+        hipLaunchKernelGGL(rt_render_cull_kernel, dim3(grid), dim3(RT_BLOCK_THREADS), dyn, stream,
+                           *P, grp, sph, sph_rm, mats, reinterpret_cast<const PixelEntry*>(pd),
+                           block_sums, work_counter, seg_counter, seg_counter + 2);
+    else
+        hipLaunchKernelGGL(rt_render_kernel, dim3(grid), dim3(RT_BLOCK_THREADS), dyn, stream, *P,
+                           grp, sph, sph_rm, mats, reinterpret_cast<const PixelEntry*>(pd),
+                           block_sums, work_counter, seg_counter, seg_counter + 2);
     return hipGetLastError();
 }
 
@@ -551,10 +593,15 @@ hipError_t rt_launch_assemble(const float4* gathered, uint32_t max_rows, float4*
 
 hipError_t rt_launch_intersect(const float4* grp, const float4* sph, uint32_t ngroups,
                                uint32_t scene_fast, const float* rays, uint32_t n, int* out_i,
-                               float* out_t, hipStream_t stream) {
+                               float* out_t, const float4* bnd, const uint32_t* perm,
+                               uint32_t nclusters, hipStream_t stream) {
     const uint32_t T = RT_BLOCK_THREADS;
-    hipLaunchKernelGGL(rt_intersect_kernel, dim3((n + T - 1) / T), dim3(T), 0, stream, grp, sph,
-                       ngroups, scene_fast, rays, n, out_i, out_t);
+    if (bnd)
+        hipLaunchKernelGGL(rt_intersect_cull_kernel, dim3((n + T - 1) / T), dim3(T), 0, stream, grp,
+                           sph, ngroups, scene_fast, rays, n, out_i, out_t, bnd, perm, nclusters);
+    else
+        hipLaunchKernelGGL(rt_intersect_kernel, dim3((n + T - 1) / T), dim3(T), 0, stream, grp, sph,
+                           ngroups, scene_fast, rays, n, out_i, out_t);
     return hipGetLastError();
 }
 

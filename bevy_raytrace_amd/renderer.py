@@ -140,15 +140,16 @@ class Renderer:
         check(self.lib, self.ctx, rc)
         return st.as_dict()
 
-    def intersect(self, rays: np.ndarray):
-        """Closest hit for rays (n, 6) float32 [origin, direction] -> (index int32, t float32)."""
+    def intersect(self, rays: np.ndarray, flags=0):
+        """Closest hit for rays (n, 6) float32 [origin, direction] -> (index int32, t float32).
+        flags: RT_FLAG_CULL traces the culled list (rt_intersect_ex; same hits)."""
         r = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 6)
         n = r.shape[0]
         idx = np.empty(n, dtype=np.int32)
         t = np.empty(n, dtype=np.float32)
-        rc = self.lib.rt_intersect(self.ctx, r.ctypes.data_as(ctypes.c_void_p), n,
-                                   idx.ctypes.data_as(ctypes.c_void_p),
-                                   t.ctypes.data_as(ctypes.c_void_p))
+        rc = self.lib.rt_intersect_ex(self.ctx, r.ctypes.data_as(ctypes.c_void_p), n, flags,
+                                      idx.ctypes.data_as(ctypes.c_void_p),
+                                      t.ctypes.data_as(ctypes.c_void_p))
         check(self.lib, self.ctx, rc)
         return idx, t
 

@@ -150,6 +150,13 @@ typedef struct rt_params {
  * identically by the oracle -- the WGSL leaves them to the driver. */
 #define RT_FLAG_JITTER    0x2u
 #define RT_FLAG_THIN_LENS 0x4u
+/* RT_FLAG_CULL: trace against the culled list -- the spheres permuted into
+ * spatial groups of 8 with a conservative bounding sphere per group, so a
+ * wave filters only the groups near some lane's ray. Hits,
+ * segment counts and images are identical to the brute-force walk of
+ * intersect.wgsl:133-143 (ties still go to the lower sphere index); only the
+ * work differs, so it is opt-in like the other non-reference modes. */
+#define RT_FLAG_CULL      0x8u
 #define RT_JITTER_HASH_MUL 0x9E3779B1u
 #define RT_LENS_HASH_MUL   0x85EBCA77u
 
@@ -243,6 +250,10 @@ int rt_wait(rt_ctx* ctx, rt_stats* stats);
  * hit_index[i] = sphere index or -1 (miss), hit_t[i] = t (1e20 on a miss).
  * Synchronous. Used for picking and for the intersection parity tests. */
 int rt_intersect(rt_ctx* ctx, const float* rays, uint32_t n, int32_t* hit_index, float* hit_t);
+
+/* rt_intersect with flags: RT_FLAG_CULL traces the culled list (same hits). */
+int rt_intersect_ex(rt_ctx* ctx, const float* rays, uint32_t n, uint32_t flags,
+                    int32_t* hit_index, float* hit_t);
 
 /* Progressive accumulation: the reference shows independent
  * 1-spp frames (collect.wgsl:115-125, no history). Here a running per-pixel sum

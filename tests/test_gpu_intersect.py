@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 from bevy_raytrace_amd import scene
+from bevy_raytrace_amd.abi import RT_FLAG_CULL
 from oracle import oracle as O
 from raygen import adversarial_rays
 
@@ -47,9 +48,10 @@ SCENES = {  # name -> (spheres, translation applied to spheres and rays)
 }
 
 
+@pytest.mark.parametrize("cull", [False, True], ids=["brute", "cull"])
 @pytest.mark.parametrize("fast", [True, False], ids=["short_math", "ieee"])
 @pytest.mark.parametrize("name", sorted(SCENES))
-def test_intersect_bit_exact(renderer, name, fast, monkeypatch):
+def test_intersect_bit_exact(renderer, name, fast, cull, monkeypatch):
     """fast=False forces the IEEE exact tests (RT_FAST_EXACT=0): both forms
     must give the oracle's bits."""
     if not fast:
@@ -64,8 +66,34 @@ def test_intersect_bit_exact(renderer, name, fast, monkeypatch):
         sp["center"] += np.asarray(off, np.float32)
         rays[:, :3] += np.asarray(off, np.float32)
     renderer.set_scene(sp, mt)
-    gi, gt = renderer.intersect(rays)
+    gi, gt = renderer.intersect(rays, flags=RT_FLAG_CULL if cull else 0)
     ci, ct = O.intersect_batch(sp, rays)
     bad = np.nonzero((gi != ci) | (gt.view(np.uint32) != ct.view(np.uint32)))[0]
     assert bad.size == 0, f"{bad.size} rays differ, e.g. {bad[:5].tolist()}: gpu {gi[bad[:5]]} {gt[bad[:5]]} cpu {ci[bad[:5]]} {ct[bad[:5]]}"
     assert (ci >= 0).mean() > 0.05  # the set really hits things
+
+
+def test_cull_tie_goes_to_lower_index(renderer):
+    """Two unit spheres touching at (1, 0, 0); the culled list holds index 1
+    first (tests/test_cull.py). Rays through the contact point give both the
+    same root: the reference's strict `<` keeps sphere 0, and so must the
+    culled walk (original-index tie-break)."""
+    from test_cull import tangent_pair
+    sp = tangent_pair().objects_gpu()
+    from bevy_raytrace_amd.abi import MATERIAL_DTYPE
+    mt = np.zeros(1, dtype=MATERIAL_DTYPE)
+    rng = np.random.default_rng(5)
+    k = 4096
+    d = rng.normal(size=(k, 3))
+    d[:, 0] = 0.0  # perpendicular to the line of centres: tangent to both
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    o = np.array([1.0, 0.0, 0.0]) - d * rng.uniform(1, 20, (k, 1))
+    rays = np.hstack([o, d]).astype(np.float32)
+    renderer.set_scene(sp, mt)
+    ci, ct = O.intersect_batch(sp, rays)
+    for flags in (0, RT_FLAG_CULL):
+        gi, gt = renderer.intersect(rays, flags=flags)
+        assert np.array_equal(gi, ci) and np.array_equal(gt.view(np.uint32), ct.view(np.uint32))
+    # the ties really occur: with the order reversed the oracle picks sphere 1
+    ri, rt = O.intersect_batch(sp[::-1].copy(), rays)
+    assert ((ci == 0) & (ri == 0)).sum() > 100  # reversed list: index 0 = the old sphere 1

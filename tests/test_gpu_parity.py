@@ -17,6 +17,7 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 NO_REUSE = abi.RT_FLAG_NO_PRIMARY_CACHE
+CULL = abi.RT_FLAG_CULL
 
 
 def arrays(sc):
@@ -57,7 +58,8 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("flags", [0, NO_REUSE], ids=["reuse", "noreuse"])
+@pytest.mark.parametrize("flags", [0, NO_REUSE, CULL, CULL | NO_REUSE],
+                         ids=["reuse", "noreuse", "cull", "cull_noreuse"])
 @pytest.mark.parametrize("name,mk,W,H,S,D,f0", CASES, ids=[c[0] for c in CASES])
 def test_bit_exact(renderer, name, mk, W, H, S, D, f0, flags):
     sp, mt = arrays(mk())
@@ -535,12 +537,49 @@ def stacked_scene():
     return scene.Scene(sp, mats, "stacked")
 
 
-@pytest.mark.parametrize("flags", [0, NO_REUSE], ids=["reuse", "noreuse"])
+@pytest.mark.parametrize("flags", [0, NO_REUSE, CULL | NO_REUSE], ids=["reuse", "noreuse", "cull"])
 def test_coincident_spheres_queue_flushes(renderer, flags):
     sp, mt = arrays(stacked_scene())
     cam = default_camera_block()
     renderer.set_scene(sp, mt)
     img, st = renderer.render(cam, 96, 54, 5, 10, frame0=2, flags=flags)
     ref, segs = O.render(cam, sp, mt, 96, 54, 5, 10, frame0=2)
+    check_exact(img, ref)
+    assert st["segments"] == segs
+
+
+def test_cull_full_1080p64_identical(renderer):
+    """RT_FLAG_CULL at the headline size: the culled walk's frame and segment
+    counts equal the brute-force walk's, bit for bit, and it is faster."""
+    sp, mt = arrays(scene.rtiow_final_scene())
+    cam = default_camera_block()
+    renderer.set_scene(sp, mt)
+    b, sb = renderer.render(cam, 1920, 1080, 64, 16, flags=NO_REUSE)
+    c, sc = renderer.render(cam, 1920, 1080, 64, 16, flags=NO_REUSE | CULL)
+    check_exact(c, b)
+    assert sc["segments"] == sb["segments"] == sc["traced_segments"]
+    assert sc["kernel_ms"] < sb["kernel_ms"]
+
+
+@pytest.mark.parametrize("K,k", [(3, 1), (8, 7)])
+def test_cull_shards_and_updates(renderer, K, k):
+    """Culled list with row shards, and rebuilt after rt_update_spheres."""
+    sc_ = scene.rtiow_final_scene()
+    sp, mt = arrays(sc_)
+    cam = default_camera_block()
+    renderer.set_scene(sp, mt)
+    W, H, S, D = 120, 64, 6, 10
+    a, _ = renderer.render(cam, W, H, S, D, row_block=4, shard_count=K, shard_index=k,
+                           flags=NO_REUSE)
+    c, _ = renderer.render(cam, W, H, S, D, row_block=4, shard_count=K, shard_index=k,
+                           flags=NO_REUSE | CULL)
+    check_exact(c, a)
+    moved = sp[10:30].copy()
+    moved["center"][:, 1] += 1.5  # lift 20 spheres: their groups' bounds must follow
+    renderer.update_spheres(10, moved)
+    sp2 = sp.copy()
+    sp2[10:30] = moved
+    img, st = renderer.render(cam, 64, 36, 4, 8, flags=CULL)
+    ref, segs = O.render(cam, sp2, mt, 64, 36, 4, 8)
     check_exact(img, ref)
     assert st["segments"] == segs
