@@ -193,25 +193,27 @@ def load(path=None):
 
 def cull_layout(spheres, lib=None):
     """The culled list the library builds for RT_FLAG_CULL (host only, no
-    device): (perm, bounds, ngroups, nclusters). perm[p] = original index of
-    permuted position p (-1 = pad); bounds (nclusters*8, 4) = (Cx, Cy, Cz, S_B)
-    per group."""
+    device): (perm, group_bounds, cluster_bounds, ngroups, nclusters).
+    perm[p] = original index of permuted position p (-1 = pad); bounds are
+    (n, 4) rows (Cx, Cy, Cz, S_B): one per group slot (nclusters * 8) and one
+    per cluster slot (supers * 8)."""
     import numpy as np
     lib = lib or load()
     sp = np.ascontiguousarray(spheres)
     n = len(sp)
-    counts = (ctypes.c_uint32 * 3)()
+    counts = (ctypes.c_uint32 * 4)()
     ptr = sp.ctypes.data_as(_VP) if n else None
     if lib.rt_debug_cull_layout(ptr, n, counts, None, 0, None, 0) != 0:
         raise RuntimeError("rt_debug_cull_layout failed")
-    ng, nc, nrec = counts[0], counts[1], counts[2]
+    ng, nc, nrec, ns = counts[0], counts[1], counts[2], counts[3]
     perm = np.empty(nrec, dtype=np.uint32)
-    bnd = np.empty(nc * 32, dtype=np.float32)
+    bnd = np.empty((ns + nc) * 32, dtype=np.float32)
     if lib.rt_debug_cull_layout(ptr, n, counts, perm.ctypes.data_as(_VP), nrec,
-                                bnd.ctypes.data_as(_VP), nc * 32) != 0:
+                                bnd.ctypes.data_as(_VP), (ns + nc) * 32) != 0:
         raise RuntimeError("rt_debug_cull_layout failed")
-    b = bnd.reshape(nc, 4, 8).transpose(0, 2, 1).reshape(nc * 8, 4)
-    return perm.astype(np.int64) - (perm == 0xFFFFFFFF) * (1 << 32), b, ng, nc
+    b = bnd.reshape(ns + nc, 4, 8).transpose(0, 2, 1).reshape((ns + nc) * 8, 4)
+    perm = perm.astype(np.int64) - (perm == 0xFFFFFFFF) * (1 << 32)
+    return perm, b[ns * 8:], b[:ns * 8], ng, nc
 
 
 def check(lib, ctx, status):

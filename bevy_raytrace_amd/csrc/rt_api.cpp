@@ -333,11 +333,13 @@ static void pack_group(rt_ctx* ctx, size_t g) {
 // ---- culled list (RT_FLAG_CULL) ---------------------------------------------
 // The spheres permuted into spatial groups of RT_GROUP (large spheres first, in
 // groups of their own; the rest in Morton order of their centres), clusters of
-// 8 consecutive groups, and per group a bounding sphere (C, R) stored in the
-// group layout -- SoA (Cx[8], Cy[8], Cz[8], S_B[8]) per cluster -- so the
-// kernel runs the same packed filter over a cluster's 8 bounds
-// (rt_dev_intersect.h intersect_world<true>) and walks only the groups some lane
-// passes, against TB = (1 - m - muB)|o|^2, m = 2^-16, muB = 2^-7.
+// 8 consecutive groups, supers of 8 clusters, and per group and per cluster a
+// bounding sphere (C, R) stored in the group layout -- SoA (Cx[8], Cy[8],
+// Cz[8], S_B[8]) per super (its clusters) and per cluster (its groups) -- so
+// the kernel runs the same packed filter over the bounds (rt_dev_intersect.h
+// intersect_world<true>) and walks only the clusters and groups some lane
+// passes, against TB = (1 - m - muB)|o|^2, m = 2^-16, muB = 2^-7. The proof
+// below holds for any member set, so for cluster bounds too.
 //
 // Why a skipped group holds no candidate (all quantities of one lane; exact
 // arithmetic unless marked ~). Filter of sphere (c, r): F = hb~^2 + r^2 -
@@ -364,7 +366,7 @@ static void pack_group(rt_ctx* ctx, size_t g) {
 // every group for a wave with a lane outside |o_i| <= 2^30, |d|^2 in
 // [2^-100, 2^100].
 struct CullLayout {
-    uint32_t ngroups = 0, nclusters = 0, nrec = 0;
+    uint32_t ngroups = 0, nclusters = 0, nsupers = 0, nrec = 0;
     std::vector<uint32_t> perm;  // position -> original index (0xFFFFFFFF = pad)
     std::vector<float4> sph, grp, bnd;
     std::vector<float2> rm;
@@ -469,15 +471,14 @@ static void cull_layout(const float4* sph, const float* S, const float2* rm, uin
     L.grp.assign(L.nrec, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     for (uint32_t g = 0; g < L.nrec / RT_GROUP; ++g)
         pack_group_soa(&L.sph[RT_GROUP * g], &Sp[RT_GROUP * g], &L.grp[RT_GROUP * g]);
-    // group bounds, SoA per cluster
+    // bounds: per cluster the SoA record of its 8 group bounds, per super (8
+    // clusters) the record of its 8 cluster bounds; bnd = supers, then clusters
     const double kB = 1.0 - 0x1p-16 - 0x1p-7;
-    std::vector<float4> bc(slots * 8, make_float4(0.0f, 0.0f, 0.0f, -INFINITY));  // (C, S_B) per group
-    std::vector<float> bs(slots * 8, -INFINITY);
-    for (uint32_t g = 0; g < slots; ++g) {
+    auto bound_of = [&](uint32_t p0, uint32_t p1, float4& C, float& SB) {
         double blo[3] = {INFINITY, INFINITY, INFINITY}, bhi[3] = {-INFINITY, -INFINITY, -INFINITY};
         bool any = false, wild = false;
-        for (uint32_t j = 0; j < RT_GROUP; ++j) {
-            const uint32_t i = L.perm[RT_GROUP * g + j];
+        for (uint32_t p = p0; p < p1; ++p) {
+            const uint32_t i = L.perm[p];
             if (i == 0xFFFFFFFFu) continue;
             any = true;
             const float4 q = sph[i];
@@ -492,16 +493,16 @@ static void cull_layout(const float4* sph, const float* S, const float2* rm, uin
                 bhi[k] = std::max(bhi[k], c[k]);
             }
         }
-        float4 C = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        float SB = -INFINITY;  // empty: never passes
+        C = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        SB = -INFINITY;  // empty: never passes
         if (any && wild) {
             SB = INFINITY;  // always passes
         } else if (any) {
             C = make_float4((float)((blo[0] + bhi[0]) * 0.5), (float)((blo[1] + bhi[1]) * 0.5),
                             (float)((blo[2] + bhi[2]) * 0.5), 0.0f);
             double Lm = 0.0;
-            for (uint32_t j = 0; j < RT_GROUP; ++j) {
-                const uint32_t i = L.perm[RT_GROUP * g + j];
+            for (uint32_t p = p0; p < p1; ++p) {
+                const uint32_t i = L.perm[p];
                 if (i == 0xFFFFFFFFu) continue;
                 const float4 q = sph[i];
                 const double dx = (double)q.x - C.x, dy = (double)q.y - C.y, dz = (double)q.z - C.z;
@@ -512,14 +513,27 @@ static void cull_layout(const float4* sph, const float* S, const float2* rm, uin
             const double CC = (double)C.x * C.x + (double)C.y * C.y + (double)C.z * C.z;
             SB = round_up_f32((R2 - kB * CC) * (1.0 + 0x1p-40) + 0x1p-60);
         }
-        bc[g] = C;
-        bs[g] = SB;
+    };
+    L.nsupers = (L.nclusters + 7) / 8;
+    L.bnd.assign((size_t)(L.nsupers + L.nclusters) * 8, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    float4 q[8];
+    float sb[8];
+    for (uint32_t u = 0; u < L.nsupers; ++u) {
+        for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t k = u * 8 + j;  // cluster
+            if (k < L.nclusters)
+                bound_of(k * 8 * RT_GROUP, (k + 1) * 8 * RT_GROUP, q[j], sb[j]);
+            else
+                q[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f), sb[j] = -INFINITY;
+        }
+        pack_group_soa(q, sb, &L.bnd[(size_t)u * 8]);
     }
-    L.bnd.assign((size_t)L.nclusters * 8, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     for (uint32_t k = 0; k < L.nclusters; ++k) {
-        float4 q[8];
-        for (int j = 0; j < 8; ++j) q[j] = bc[k * 8 + j];
-        pack_group_soa(q, &bs[k * 8], &L.bnd[(size_t)k * 8]);
+        for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t g = k * 8 + j;
+            bound_of(g * RT_GROUP, (g + 1) * RT_GROUP, q[j], sb[j]);
+        }
+        pack_group_soa(q, sb, &L.bnd[(size_t)(L.nsupers + k) * 8]);
     }
 }
 
@@ -803,6 +817,10 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         K_.bnd = ctx->d_bnd_c;
         K_.perm = ctx->d_perm_c;
         K_.nclusters = ctx->nclusters_c;
+        // measured: with the RTIOW scene's 8 clusters the super level costs
+        // more than it saves (18,582 vs 18,919 Mrays/s); with 157 clusters
+        // (10 000 spheres) it saves 14 % (3,115 vs 2,685)
+        K_.cull_supers = ctx->nclusters_c > 16 ? 1u : 0u;
     }
     K_.scene_fast = ctx->scene_fast && env_flag("RT_FAST_EXACT", true) ? 1u : 0u;
     K_.flags = p.flags;
@@ -1124,9 +1142,10 @@ int rt_intersect_ex(rt_ctx* ctx, const float* rays, uint32_t n, uint32_t flags, 
 
 // Internal (not in include/rt_hip.h; tests/test_cull.py, CPU): the culled
 // layout of a sphere list as build_cull makes it, without a device.
-// counts[0..2] = (groups, clusters, records); perm (records entries) and bnd
-// (clusters * 32 floats: per cluster Cx[8] Cy[8] Cz[8] S_B[8]) are filled when
-// their capacities suffice. Returns 0, or -1 on a NULL argument.
+// counts[0..3] = (groups, clusters, records, supers); perm (records entries) and bnd
+// ((supers + clusters) * 32 floats, supers = ceil(clusters / 8): per super
+// its 8 cluster bounds, then per cluster its 8 group bounds, each record
+// Cx[8] Cy[8] Cz[8] S_B[8]) are filled when their capacities suffice. Returns 0, or -1 on a NULL argument.
 int rt_debug_cull_layout(const rt_sphere* spheres, uint32_t n, uint32_t* counts, uint32_t* perm,
                          uint32_t perm_cap, float* bnd, uint32_t bnd_cap) {
     if (!counts || (n && !spheres)) return -1;
@@ -1139,6 +1158,7 @@ int rt_debug_cull_layout(const rt_sphere* spheres, uint32_t n, uint32_t* counts,
     counts[0] = L.ngroups;
     counts[1] = L.nclusters;
     counts[2] = L.nrec;
+    counts[3] = L.nsupers;
     if (perm && perm_cap >= L.nrec) std::copy(L.perm.begin(), L.perm.end(), perm);
     if (bnd && bnd_cap >= L.bnd.size() * 4) std::memcpy(bnd, L.bnd.data(), L.bnd.size() * sizeof(float4));
     return 0;

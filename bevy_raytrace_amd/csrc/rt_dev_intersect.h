@@ -323,15 +323,18 @@ __device__ __forceinline__ void drain_candidates(const uint32_t* cq, uint32_t cn
 // wave pays for max-over-lanes candidates, not for their union.
 // Returns the best index (-1 = miss) and t.
 //
-// CULL (rt_render_cull_kernel; the list permuted into spatial groups and
-// clusters of 8 groups by rt_api.cpp build_cull): before its 8 groups, a
-// cluster's 8 group BOUNDS -- spheres (C_j, R_j) stored exactly like a group
-// of spheres, S_j = R_j^2 - (1 - m - muB)|C_j|^2 -- go through the same packed
-// filter against the threshold TB = (1 - m - muB)|o|^2, and only the groups
-// some lane of the wave passes are filtered. Each bound dominates its members'
+// CULL (rt_render_cull_kernel; the list permuted into spatial groups,
+// clusters of 8 groups and supers of 8 clusters by rt_api.cpp build_cull):
+// a super's 8 cluster BOUNDS, then a passing cluster's 8 group bounds --
+// spheres (C_j, R_j) stored exactly like a group of spheres, S_j = R_j^2 -
+// (1 - m - muB)|C_j|^2 -- go through the same packed filter against the
+// threshold TB = (1 - m - muB)|o|^2, and only the groups some lane of the
+// wave passes are filtered. Each bound dominates its members'
 // filter values (proof in rt_api.cpp build_cull: R_j^2 = (1 + 2^-3) L^2 with
-// L = max(|C_j - c_i| + r_i (1 + 2^-18)), muB = 2^-7): a lane with a candidate
-// in group j passes bound j, so a skipped group held no candidate of any lane
+// L = max(|C_j - c_i| + r_i (1 + 2^-18)) over the members -- the spheres of the
+// group, or of all 8 groups of the cluster -- and muB = 2^-7): a lane with a
+// candidate in group j passes bound j and its cluster's bound, so a skipped
+// group held no candidate of any lane
 // and the candidate lists -- hence the hits -- are those of the full walk.
 // The proof needs finite, moderate operands: a wave with a lane outside
 // |o_i| <= 2^30, |d|^2 in [2^-100, 2^100] walks every group (bounds of groups
@@ -345,7 +348,7 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
                                                Prof& prof_,
 #endif
                                                const float4* bnd, const uint32_t* perm,
-                                               uint32_t nclusters) {
+                                               uint32_t nclusters, bool use_supers = true) {
     const float l = sqrt_x(dot(d, d));
     const float a = l * l;  // sqr(length(r.dir)), intersect.wgsl:98
     const bool fast = ray_fast(scene_fast, o, a);
@@ -422,44 +425,54 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
         const float om = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
         const bool cull_ok = (rt_ballot(!(om <= 0x1p30f)) | rt_ballot(!(a >= 0x1p-100f)) |
                               rt_ballot(!(a <= 0x1p100f))) == 0;
-        for (uint32_t k = 0; k < nclusters; ++k) {
-            uint32_t gm = 0xFFu;  // groups of cluster k to filter
-            if (cull_ok) {
-                const auto* p = bp + (size_t)k * 8;
-                const float4 X0 = p[0], X1 = p[1], Y0 = p[2], Y1 = p[3];
-                const float4 Z0 = p[4], Z1 = p[5], S0 = p[6], S1 = p[7];
+        // The wave's 8-bit mask of the bounds in one SoA record that some lane
+        // passes (the record layout of a group: the same filter8).
+        auto bound_mask = [&](const auto* p) __attribute__((always_inline)) -> uint32_t {
+            const float4 X0 = p[0], X1 = p[1], Y0 = p[2], Y1 = p[3];
+            const float4 Z0 = p[4], Z1 = p[5], S0 = p[6], S1 = p[7];
 #if defined(RT_ASM_FILTER) && defined(__HIP_DEVICE_COMPILE__)
-                f2 b01, b23, b45, b67;
-                float bmax;
-                filter8(RP, f2{X0.x, X0.y}, f2{X0.z, X0.w}, f2{X1.x, X1.y}, f2{X1.z, X1.w},
-                        f2{Y0.x, Y0.y}, f2{Y0.z, Y0.w}, f2{Y1.x, Y1.y}, f2{Y1.z, Y1.w},
-                        f2{Z0.x, Z0.y}, f2{Z0.z, Z0.w}, f2{Z1.x, Z1.y}, f2{Z1.z, Z1.w},
-                        f2{S0.x, S0.y}, f2{S0.z, S0.w}, f2{S1.x, S1.y}, f2{S1.z, S1.w}, b01, b23,
-                        b45, b67, bmax);
+            f2 b01, b23, b45, b67;
+            float bmax;
+            filter8(RP, f2{X0.x, X0.y}, f2{X0.z, X0.w}, f2{X1.x, X1.y}, f2{X1.z, X1.w},
+                    f2{Y0.x, Y0.y}, f2{Y0.z, Y0.w}, f2{Y1.x, Y1.y}, f2{Y1.z, Y1.w},
+                    f2{Z0.x, Z0.y}, f2{Z0.z, Z0.w}, f2{Z1.x, Z1.y}, f2{Z1.z, Z1.w},
+                    f2{S0.x, S0.y}, f2{S0.z, S0.w}, f2{S1.x, S1.y}, f2{S1.z, S1.w}, b01, b23,
+                    b45, b67, bmax);
 #else
-                const f2 b01 = filter2(f2{X0.x, X0.y}, f2{Y0.x, Y0.y}, f2{Z0.x, Z0.y}, f2{S0.x, S0.y}, R);
-                const f2 b23 = filter2(f2{X0.z, X0.w}, f2{Y0.z, Y0.w}, f2{Z0.z, Z0.w}, f2{S0.z, S0.w}, R);
-                const f2 b45 = filter2(f2{X1.x, X1.y}, f2{Y1.x, Y1.y}, f2{Z1.x, Z1.y}, f2{S1.x, S1.y}, R);
-                const f2 b67 = filter2(f2{X1.z, X1.w}, f2{Y1.z, Y1.w}, f2{Z1.z, Z1.w}, f2{S1.z, S1.w}, R);
-                const float bmax = fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(b01.x, b01.y), b23.x),
-                                                             b23.y), b45.x), b45.y), b67.x), b67.y);
+            const f2 b01 = filter2(f2{X0.x, X0.y}, f2{Y0.x, Y0.y}, f2{Z0.x, Z0.y}, f2{S0.x, S0.y}, R);
+            const f2 b23 = filter2(f2{X0.z, X0.w}, f2{Y0.z, Y0.w}, f2{Z0.z, Z0.w}, f2{S0.z, S0.w}, R);
+            const f2 b45 = filter2(f2{X1.x, X1.y}, f2{Y1.x, Y1.y}, f2{Z1.x, Z1.y}, f2{S1.x, S1.y}, R);
+            const f2 b67 = filter2(f2{X1.z, X1.w}, f2{Y1.z, Y1.w}, f2{Z1.z, Z1.w}, f2{S1.z, S1.w}, R);
+            const float bmax = fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(fmaxf(b01.x, b01.y), b23.x),
+                                                         b23.y), b45.x), b45.y), b67.x), b67.y);
 #endif
-                gm = 0u;
-                if (rt_ballot(bmax >= TB) != 0) {
-                    gm = (rt_ballot(b01.x >= TB) != 0 ? 0x01u : 0u) |
-                         (rt_ballot(b01.y >= TB) != 0 ? 0x02u : 0u) |
-                         (rt_ballot(b23.x >= TB) != 0 ? 0x04u : 0u) |
-                         (rt_ballot(b23.y >= TB) != 0 ? 0x08u : 0u) |
-                         (rt_ballot(b45.x >= TB) != 0 ? 0x10u : 0u) |
-                         (rt_ballot(b45.y >= TB) != 0 ? 0x20u : 0u) |
-                         (rt_ballot(b67.x >= TB) != 0 ? 0x40u : 0u) |
-                         (rt_ballot(b67.y >= TB) != 0 ? 0x80u : 0u);
+            if (rt_ballot(bmax >= TB) == 0) return 0u;
+            return (rt_ballot(b01.x >= TB) != 0 ? 0x01u : 0u) |
+                   (rt_ballot(b01.y >= TB) != 0 ? 0x02u : 0u) |
+                   (rt_ballot(b23.x >= TB) != 0 ? 0x04u : 0u) |
+                   (rt_ballot(b23.y >= TB) != 0 ? 0x08u : 0u) |
+                   (rt_ballot(b45.x >= TB) != 0 ? 0x10u : 0u) |
+                   (rt_ballot(b45.y >= TB) != 0 ? 0x20u : 0u) |
+                   (rt_ballot(b67.x >= TB) != 0 ? 0x40u : 0u) |
+                   (rt_ballot(b67.y >= TB) != 0 ? 0x80u : 0u);
+        };
+        // three levels: supers of 8 clusters (bp: nsupers records of cluster
+        // bounds, then nclusters records of group bounds), clusters of 8 groups;
+        // the super level only pays with many clusters (host: use_supers)
+        const uint32_t nsupers = (nclusters + 7u) >> 3;
+        const auto* cp = bp + (size_t)nsupers * 8;
+        for (uint32_t u = 0; u < nsupers; ++u) {
+            const uint32_t valid = nclusters - u * 8u >= 8u ? 0xFFu : (1u << (nclusters - u * 8u)) - 1u;
+            uint32_t cm = cull_ok && use_supers ? bound_mask(bp + (size_t)u * 8) : valid;
+            while (cm) {
+                const uint32_t k = u * 8u + __builtin_ctz(cm);
+                cm &= cm - 1u;
+                uint32_t gm = cull_ok ? bound_mask(cp + (size_t)k * 8) : 0xFFu;
+                while (gm) {
+                    const uint32_t j = __builtin_ctz(gm);
+                    gm &= gm - 1u;
+                    group(k * 8u + j);
                 }
-            }
-            while (gm) {
-                const uint32_t j = __builtin_ctz(gm);
-                gm &= gm - 1u;
-                group(k * 8u + j);
             }
         }
     } else {

@@ -75,9 +75,11 @@ struct KParams {
     uint32_t prio_shift;  // mode 3: one step per 2^prio_shift ticks of 10 ns (RT_PRIO_SHIFT)
     // culled list (RT_FLAG_CULL; rt_render_cull_kernel): grp / sph / sph_rm
     // are then the permuted arrays, nspheres / ngroups their padded sizes
-    const float4* bnd;      // per cluster of 8 groups: the 8 group bounds, SoA like a group; null = brute force
+    const float4* bnd;      // bound records, SoA like a group: per super its 8 cluster bounds,
+                            // then per cluster its 8 group bounds; null = brute force
     const uint32_t* perm;   // permuted position -> original sphere index (ties)
     uint32_t nclusters;
+    uint32_t cull_supers;   // 1: test the cluster bounds (many clusters); 0: walk every cluster
 };
 
 // Row block b of the image -> owning shard (rt_params: serpentine deal).

@@ -269,7 +269,7 @@ __device__ __forceinline__ void render_body(
 #ifdef RT_PROFILE
                                        prof_,
 #endif
-                                       P.bnd, P.perm, P.nclusters);
+                                       P.bnd, P.perm, P.nclusters, P.cull_supers != 0);
         }
         traced += (uint32_t)__popcll(live);
         if (has_item) {

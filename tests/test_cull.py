@@ -63,31 +63,34 @@ def member_S(sp):
 
 
 def check_layout(sp):
-    perm, bnd, ng, nc = abi.cull_layout(sp)
+    perm, bnd, cbnd, ng, nc = abi.cull_layout(sp)
     n = len(sp)
     real = perm[perm >= 0]
     assert sorted(real.tolist()) == list(range(n))
-    assert nc == (ng + 7) // 8 and len(bnd) == nc * 8
+    assert nc == (ng + 7) // 8 and len(bnd) == nc * 8 and len(cbnd) == (nc + 7) // 8 * 8
     assert (perm[ng * 8:] < 0).all()
     for g in range(nc * 8):  # empty groups never pass, non-empty ones may
         members = perm[g * 8:(g + 1) * 8] if g < ng else np.array([-1])
         if (members < 0).all():
             assert bnd[g, 3] == -np.inf
-    return perm, bnd, ng, nc
+    assert (cbnd[nc:, 3] == -np.inf).all()  # pad clusters of the last super
+    return perm, bnd, cbnd, ng, nc
 
 
 def dominance(sp, rays, chunk=4000):
     """Count (ray, group) pairs where a member is a candidate but the bound
     fails, over the rays the kernel culls for; and the bound pass rate."""
-    perm, bnd, ng, nc = check_layout(sp)
+    perm, bnd, cbnd, ng, nc = check_layout(sp)
     S = member_S(sp)
     c = sp["center"].astype(F)
     viol = tested = passed = 0
     for s0 in range(0, len(rays), chunk):
         R = ray_consts(rays[s0:s0 + chunk])
         HB = filt(R, bnd[:, :3].astype(F), bnd[:, 3].astype(F))  # (n, nc*8)
+        HC = filt(R, cbnd[:, :3].astype(F), cbnd[:, 3].astype(F))  # (n, supers*8)
         with np.errstate(invalid="ignore"):
             bpass = HB >= R["TB"][:, None]
+            cpass = HC >= R["TB"][:, None]
         for g in range(ng):
             mem = perm[g * 8:(g + 1) * 8]
             mem = mem[mem >= 0]
@@ -96,7 +99,7 @@ def dominance(sp, rays, chunk=4000):
             H = filt(R, c[mem], S[mem])
             with np.errstate(invalid="ignore"):
                 cand = (H >= R["T"][:, None]).any(1)
-            bad = cand & ~bpass[:, g] & R["ok"]
+            bad = cand & ~(bpass[:, g] & cpass[:, g // 8]) & R["ok"]
             viol += int(bad.sum())
             tested += int(R["ok"].sum())
             passed += int((bpass[:, g] & R["ok"]).sum())
@@ -114,6 +117,7 @@ def tangent_pair():
 
 SCENES = {
     "rtiow": lambda: scene.rtiow_final_scene().objects_gpu(),
+    "spheres10k": lambda: scene.ten_thousand_scene().objects_gpu()[::7].copy(),
     "reference": lambda: scene.reference_scene().objects_gpu(),
     "config1": lambda: scene.config1_scene().objects_gpu(),
     "tangent": lambda: tangent_pair().objects_gpu(),
@@ -141,7 +145,7 @@ def test_bounds_cull_rtiow():
     """The point of the layout: on camera-like rays into the RTIOW scene most
     groups' bounds fail for most rays."""
     sp = scene.rtiow_final_scene().objects_gpu()
-    rng = np.random.default_rng(0)
+    rng = np.random.default_rng(0)  # (pass rate of the group bounds alone)
     o = np.tile([13.0, 2.0, 3.0], (4000, 1))
     tgt = rng.uniform([-11, 0, -11], [11, 1, 11], (4000, 3))
     d = tgt - o
@@ -153,22 +157,23 @@ def test_bounds_cull_rtiow():
 
 def test_layout_edge_cases():
     # empty, one sphere, huge / non-finite members (always-pass bounds)
-    perm, bnd, ng, nc = abi.cull_layout(scene.Scene([], scene.MaterialCache(), "e").objects_gpu())
-    assert ng == 0 and nc == 0
+    perm, bnd, cbnd, ng, nc = abi.cull_layout(scene.Scene([], scene.MaterialCache(), "e").objects_gpu())
+    assert ng == 0 and nc == 0 and len(cbnd) == 0
     sp = scene.rtiow_final_scene().objects_gpu()[:9].copy()
     sp["center"][3] = (2.0 ** 31, 0, 0)
     sp["radius"][5] = np.inf
-    perm, bnd, ng, nc = check_layout(sp)
+    perm, bnd, cbnd, ng, nc = check_layout(sp)
     for bad in (3, 5):
         g = int(np.nonzero(perm == bad)[0][0]) // 8
         assert bnd[g, 3] == np.inf and (bnd[g, :3] == 0).all()
+        assert cbnd[g // 8, 3] == np.inf
     one = sp[:1].copy()
-    perm, bnd, ng, nc = check_layout(one)
+    perm, bnd, cbnd, ng, nc = check_layout(one)
     assert ng == 1 and nc == 1
 
 
 def test_tangent_pair_order():
     """The tie-break test's premise: the later sphere comes first in the
     culled list (so the kernel must compare original indices)."""
-    perm, _, _, _ = abi.cull_layout(tangent_pair().objects_gpu())
+    perm = abi.cull_layout(tangent_pair().objects_gpu())[0]
     assert perm[0] == 1 and perm[1] == 0
