@@ -67,8 +67,9 @@ def parse():
                     help="frames per persistent launch (rt_render_frames_device)")
     ap.add_argument("--reuse-steps", type=int, default=4,
                     help="extra frames timed with primary-hit reuse on (0 = skip)")
-    ap.add_argument("--cull-steps", type=int, default=12,
-                    help="extra frames timed with the culled list, RT_FLAG_CULL (0 = skip)")
+    ap.add_argument("--cull-steps", type=int, default=-1,
+                    help="extra frames timed with the culled list, RT_FLAG_CULL (0 = skip; "
+                         "default 12 at N=1, skipped at N>1)")
     return ap.parse_args()
 
 
@@ -231,6 +232,8 @@ def main():
                          "across a sample block (bit-identical image)"}
 
     culled = None
+    if args.cull_steps < 0:
+        args.cull_steps = 12 if world == 1 else 0
     if args.cull_steps > 0:
         CULLF = NO_REUSE | abi.RT_FLAG_CULL
         run(min(args.cull_steps, FPL), CULLF)  # warm-up launch of the timed size

@@ -377,6 +377,7 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
 #endif
     // The filter of one group of 8 (pass 1 of the walk).
     auto group = [&](uint32_t g) __attribute__((always_inline)) {
+        PROF_ADD(10, 1);  // groups filtered
         const auto* p = gp + (size_t)g * 8;
         const float4 X0 = p[0], X1 = p[1], Y0 = p[2], Y1 = p[3];
         const float4 Z0 = p[4], Z1 = p[5], S0 = p[6], S1 = p[7];

@@ -1,7 +1,7 @@
 """Phase breakdown of rt_render_kernel from the -DRT_PROFILE diagnostic build
 (tools/librt_hip_prof.so), per launch shape / item policy. Shares (not
 absolute times) are meaningful: the stamps perturb the kernel.
-usage: python tools/prof_phases.py [F,n,k[,ENV=VAL;ENV=VAL]] ..."""
+usage: python tools/prof_phases.py [F,n,k[,ENV=VAL;ENV=VAL]] ...   (CULL=1: RT_FLAG_CULL)"""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -24,12 +24,13 @@ for case in cases:
     parts = case.split(",", 3)  # F,n,k[,ENV=VAL;ENV=VAL...] (values may hold commas)
     F, n, k = int(parts[0]), int(parts[1]), int(parts[2])
     env = dict(p.split("=", 1) for p in parts[3].split(";")) if len(parts) > 3 else {}
+    flags = abi.RT_FLAG_NO_PRIMARY_CACHE | (abi.RT_FLAG_CULL if env.pop("CULL", "0") == "1" else 0)
     old = {e: os.environ.get(e) for e in env}
     os.environ.update(env)
     rb = configs.pick_row_block(H, n)
     for _ in range(2):
         r.render_frames_device(cam, F, buf.data_ptr(), W, H, S, D, row_block=rb, shard_count=n,
-                               shard_index=k, flags=abi.RT_FLAG_NO_PRIMARY_CACHE)
+                               shard_index=k, flags=flags)
         st = r.wait()
     c = r.debug_counters()
     for e, v in old.items():
@@ -44,5 +45,6 @@ for case in cases:
           f"wave-cycles/iter {c[8] / it:.0f}", flush=True)
     print("   shares: " + ", ".join(f"{NAMES[i]}={c[i] / tot:.3f}" for i in NAMES) +
           f" | cand-groups/iter {c[5] / it:.2f} drain-max/iter {c[6] / it:.2f} "
-          f"exact wave-max {c[13] / it:.2f} full {c[14] / it:.2f} flushes/iter {c[11] / it:.3f}",
+          f"exact wave-max {c[13] / it:.2f} full {c[14] / it:.2f} flushes/iter {c[11] / it:.3f} "
+          f"groups/iter {c[10] / it:.2f}",
           flush=True)
