@@ -63,6 +63,9 @@ def parse():
                     help="every rank on cuda:0 (rehearsal with --dist-backend gloo)")
     ap.add_argument("--check", action="store_true",
                     help="add a checksum of the assembled frames to the JSON line")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="take the N>1 path (process group, shard gather, assembly) "
+                         "even at world size 1")
     ap.add_argument("--frames-per-launch", type=int, default=12,
                     help="frames per persistent launch (rt_render_frames_device)")
     ap.add_argument("--reuse-steps", type=int, default=4,
@@ -89,6 +92,12 @@ def load_traffic(workload_key, frames_per_launch):
 
 def main():
     args = parse()
+    # stdout carries exactly the one JSON line: libraries that print to fd 1
+    # (RCCL's version banner at communicator init, HIP runtime notes) are sent
+    # to stderr; the result is written to the saved stdout at the end.
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
 
@@ -102,9 +111,18 @@ def main():
             sys.exit(2)
     if args.same_device:
         local = 0
+    # --force-dist at world 1: the N>1 data path (shard slab, gather through the
+    # process group, device re-assembly) on one process, e.g. to exercise the
+    # RCCL gather on a one-GPU box
+    dist_on = world > 1 or args.force_dist
+    if dist_on and world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
     red_dev = "cuda" if args.dist_backend == "nccl" else "cpu"  # scalar reductions
     torch.cuda.set_device(local)
-    if world > 1:
+    if dist_on:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -135,17 +153,17 @@ def main():
     image = (torch.empty((FPL, H, W, 4), dtype=torch.float32, device="cuda")
              if rank == 0 else None)
     # N=1: the single shard is the image; render straight into it.
-    shard = image if world == 1 else torch.empty((FPL, max_rows, W, 4), dtype=torch.float32,
+    shard = image if not dist_on else torch.empty((FPL, max_rows, W, 4), dtype=torch.float32,
                                                   device="cuda")
     gathered = (torch.empty((world, FPL, max_rows, W, 4), dtype=torch.float32, device="cuda")
-                if (rank == 0 and world > 1) else None)
+                if (rank == 0 and dist_on) else None)
 
     def launch(first, nf, flags):
         """Enqueue frames [first, first + nf): render, then (N > 1) one RCCL
         gather of the nf shard slabs to rank 0 and the device re-assembly."""
         r.render_frames_device(cam, nf, shard.data_ptr(), W, H, S, D, first * S, B, world, rank,
                                flags, stream=stream.cuda_stream)
-        if world > 1:
+        if dist_on:
             if args.dist_backend == "nccl":
                 dist.gather(shard[:nf], [gathered[k, :nf] for k in range(world)] if rank == 0
                             else None, dst=0)
@@ -187,16 +205,16 @@ def main():
         run(args.warmup, NO_REUSE)
 
     def timed(nsteps, flags):
-        if world > 1:
+        if dist_on:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         stats, sizes = run(nsteps, flags)
         torch.cuda.synchronize()
-        if world > 1:
+        if dist_on:
             dist.barrier()
         dt = time.perf_counter() - t0
-        if world > 1:
+        if dist_on:
             t = torch.tensor([dt], dtype=torch.float64, device=red_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
@@ -207,11 +225,11 @@ def main():
     traced_local = sum(s["traced_segments"] for s in stats)
     kms = [s["kernel_ms"] for s in stats]
     tot = torch.tensor([segs_local, traced_local], dtype=torch.float64, device=red_dev)
-    if world > 1:
+    if dist_on:
         dist.all_reduce(tot)
     segs_all, traced_all = float(tot[0].item()), float(tot[1].item())
     per_rank = None
-    if world > 1:  # load balance of the row tiling: each rank's render-kernel time
+    if dist_on:  # load balance of the row tiling: each rank's render-kernel time
         mine = torch.tensor([float(sum(kms)), float(segs_local)], dtype=torch.float64,
                             device=red_dev)
         parts = [torch.empty_like(mine) for _ in range(world)]
@@ -240,7 +258,7 @@ def main():
         cdt, cstats, csizes = timed(args.cull_steps, CULLF)
         csegs = torch.tensor([float(sum(s["segments"] for s in cstats))], dtype=torch.float64,
                              device=red_dev)
-        if world > 1:
+        if dist_on:
             dist.all_reduce(csegs)
         cval = float(csegs[0].item()) / cdt / 1e6
         culled = {"value": round(cval, 2), "unit": "Mrays/s",
@@ -253,7 +271,7 @@ def main():
                           "the brute-force 18*N flops per segment are no longer all executed)"}
 
     if rank != 0:
-        if world > 1:
+        if dist_on:
             dist.destroy_process_group()
         return
 
@@ -286,7 +304,7 @@ def main():
                    "parallelism": (f"row-tiled x{world} (blocks of {B} rows) + "
                                    + ("RCCL gather" if args.dist_backend == "nccl"
                                       else "host-staged gloo gather (rehearsal)"))
-                   if world > 1 else "single GPU"},
+                   if dist_on else "single GPU"},
         "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
                      "traffic": traffic,
@@ -313,8 +331,8 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cam, spheres, mats, W, H, S, D, args.cpu_rows,
                                            image[0].cpu().numpy())
-    print(json.dumps(out))
-    if world > 1:
+    os.write(json_fd, (json.dumps(out) + "\n").encode())
+    if dist_on:
         dist.destroy_process_group()
 
 

@@ -489,7 +489,15 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
     PROF_MARK(2);
 #ifdef RT_PROFILE
     PROF_ADD(13, wave_max_u32(ecnt[0]));
+#ifdef RT_PROF_SUMFULL  // c[14]: lanes' full exact tests summed (not the wave max)
+    {
+        uint32_t sum1 = ecnt[1];
+        for (int off = 32; off > 0; off >>= 1) sum1 += __shfl_xor(sum1, off);
+        PROF_ADD(14, sum1);
+    }
+#else
     PROF_ADD(14, wave_max_u32(ecnt[1]));
+#endif
     {
         uint32_t sum0 = ecnt[0];
         for (int off = 32; off > 0; off >>= 1) sum0 += __shfl_xor(sum0, off);

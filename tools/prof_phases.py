@@ -9,7 +9,7 @@ from bevy_raytrace_amd import abi, configs
 from bevy_raytrace_amd.camera import default_camera_block
 from bevy_raytrace_amd.renderer import Renderer
 
-LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librt_hip_prof.so")
+LIB = os.environ.get("RT_PROF_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "librt_hip_prof.so")
 NAMES = {0: "refill", 1: "filter", 2: "drain", 12: "bookkeep", 3: "shade", 7: "tail"}
 wl = configs.WORKLOADS["rtiow1080"]
 sc = wl.make_scene()
@@ -18,8 +18,11 @@ r = Renderer(0, lib_path=LIB)
 r.set_scene(sc.objects_gpu(), sc.materials_gpu())
 W, H, S, D = wl.width, wl.height, wl.spp, wl.max_depth
 nsp = len(sc.objects_gpu())
-buf = torch.empty((8, H, W, 4), dtype=torch.float32, device="cuda:0")
 cases = sys.argv[1:] or ["4,1,0", "4,1,0,RT_SPLIT_ALL=1", "4,8,7", "8,8,7"]
+# the output holds the largest case's frames (the library cannot check a
+# device pointer's extent)
+buf = torch.empty((max(int(c.split(",")[0]) for c in cases), H, W, 4), dtype=torch.float32,
+                  device="cuda:0")
 for case in cases:
     parts = case.split(",", 3)  # F,n,k[,ENV=VAL;ENV=VAL...] (values may hold commas)
     F, n, k = int(parts[0]), int(parts[1]), int(parts[2])
@@ -46,5 +49,6 @@ for case in cases:
     print("   shares: " + ", ".join(f"{NAMES[i]}={c[i] / tot:.3f}" for i in NAMES) +
           f" | cand-groups/iter {c[5] / it:.2f} drain-max/iter {c[6] / it:.2f} "
           f"exact wave-max {c[13] / it:.2f} full {c[14] / it:.2f} flushes/iter {c[11] / it:.3f} "
-          f"groups/iter {c[10] / it:.2f}",
+          f"groups/iter {c[10] / it:.2f} exact lane-mean {c[15] / max(c[9], 1):.2f} "
+          f"c14/lane {c[14] / max(c[9], 1):.2f}",
           flush=True)
