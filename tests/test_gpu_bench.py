@@ -1,0 +1,34 @@
+"""bench.py's data paths on the GPU (one MI355X): the N>1 path -- shard slab,
+gather through the process group (backend nccl = RCCL), device re-assembly --
+taken at world size 1 (`--force-dist`) must give the frames of the
+single-GPU path bit for bit, and stdout must hold exactly the one JSON line
+(RCCL prints a version banner to fd 1 at communicator init)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--config", "config1", "--steps", "4", "--warmup", "1", "--frames-per-launch", "2",
+        "--no-cpu-baseline", "--reuse-steps", "0", "--cull-steps", "0", "--check"]
+
+
+def _bench(*extra):
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *ARGS, *extra],
+                       cwd=ROOT, capture_output=True, text=True, timeout=100)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = p.stdout.splitlines()
+    assert len(lines) == 1, p.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+def test_rccl_gather_path_matches_single_gpu():
+    a = _bench()
+    b = _bench("--force-dist", "--dist-backend", "nccl")
+    assert a["config"]["parallelism"] == "single GPU"
+    assert "RCCL gather" in b["config"]["parallelism"]
+    assert a["check"] == b["check"] and len(a["check"]) == 2  # the last launch's frames
+    assert a["segments_per_frame"] == b["segments_per_frame"]
