@@ -1,0 +1,125 @@
+"""Golden fixtures from the reference's OWN shaders (TEST INFRASTRUCTURE; run
+in the build container, where /root/reference exists -- never at test time).
+
+The six WGSL kernels of the reference (assets/shaders/{clear,generate,prepass,
+intersect,shade,collect}.wgsl) are parsed and executed by tests/golden/
+wgsl_exec.py, scheduled exactly as RayTraceNode::run records them
+(src/ray_trace_node.rs:195-224: clear, generate, 3 x {prepass, intersect,
+shade}, collect; grid floor(W*H*SAMPLES_PER_RAY / 128) workgroups of 128,
+ray_trace_node.rs:16,37-38; prepass one invocation, :74), with the host buffers
+the reference's prepare systems fill: globals {frame, W, H, spp, 5 counters
+reset} (src/ray_trace_globals.rs:56-68), rays / intersections zeroed
+(src/ray_trace_rays.rs:50-66), the sphere list with its 16-B count header
+(src/sphere.rs:166-197), materials (src/ray_trace_materials.rs:129-164) and the
+128-B camera block (src/ray_trace_camera.rs:43-68) -- here our ABI records
+(bevy_raytrace_amd.abi), decoded by the shaders' own struct declarations.
+
+SAMPLES_PER_RAY = 1 and W*H a multiple of 128 (SURVEY.md Appendix B D1, D3:
+the reference's spp > 1 and floor-divided grid are not reproduced by the
+oracle). Each fixture holds the inputs and the per-frame output image; the
+oracle is checked against it in tests/test_oracle.py (depth 3 = the
+reference's loop count).
+
+usage: python tests/golden/make_wgsl_golden.py [--ref /root/reference]
+"""
+import argparse
+import os
+import struct
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, HERE)
+import wgsl_exec as W  # noqa: E402
+
+from bevy_raytrace_amd import scene  # noqa: E402
+from bevy_raytrace_amd.camera import default_camera_block  # noqa: E402
+
+KERNELS = ("clear", "generate", "prepass", "intersect", "shade", "collect")
+WORKGROUP = 128  # ray_trace_node.rs:16
+BOUNCE_LOOPS = 3  # ray_trace_node.rs:213
+
+CASES = [
+    # name, scene, W, H, frames
+    ("wgsl_config1_64x32", scene.config1_scene, 64, 32, (0, 1, 7, 1000)),
+    ("wgsl_reference_32x16", scene.reference_scene, 32, 16, (0, 3)),
+    ("wgsl_rtiow_16x8", scene.rtiow_final_scene, 16, 8, (0, 5)),
+]
+
+
+def run_reference(shaders, cam_bytes, sph_bytes, mat_bytes, width, height, frame):
+    """One frame of RayTraceNode::run through the interpreted WGSL."""
+    R = width * height
+    assert R % WORKGROUP == 0
+    groups = R // WORKGROUP
+    first = shaders["clear"]
+    globals_ = first.decode(first.var_type("globals"),
+                            struct.pack("<9I", frame, width, height, 1, 0, 0, 0, 0, 0))
+    rays = first.decode(first.var_type("ray_buffer"),
+                        struct.pack("<I12x", R) + bytes(48 * R))
+    isect = first.decode(first.var_type("intersection_buffer"), bytes(64 * R))
+    out = np.zeros((height, width, 4), np.float32)
+    for sh in shaders.values():
+        res = {}
+        for name in sh.m["vars"]:
+            ty = sh.var_type(name)
+            if name == "camera":
+                res[name] = sh.decode(ty, cam_bytes)
+            elif name == "globals":
+                res[name] = globals_
+            elif name == "ray_buffer":
+                res[name] = rays
+            elif name == "intersection_buffer":
+                res[name] = isect
+            elif name == "objects":
+                res[name] = sh.decode(ty, struct.pack("<I12x", len(sph_bytes) // 32) + sph_bytes)
+            elif name == "materials":
+                res[name] = sh.decode(ty, mat_bytes)
+            elif name == "output":
+                res[name] = out
+            else:
+                raise KeyError(name)
+        sh.bind(**res)
+    shaders["clear"].dispatch("main", groups, WORKGROUP)
+    shaders["generate"].dispatch("main", groups, WORKGROUP)
+    for _ in range(BOUNCE_LOOPS):
+        shaders["prepass"].dispatch("main", 1, 1)
+        shaders["intersect"].dispatch("main", groups, WORKGROUP)
+        shaders["shade"].dispatch("main", groups, WORKGROUP)
+    shaders["collect"].dispatch("main", groups, WORKGROUP)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    srcs = {k: open(os.path.join(a.ref, "assets", "shaders", k + ".wgsl")).read() for k in KERNELS}
+    shaders = {k: W.Shader(srcs[k]) for k in KERNELS}
+    cam = default_camera_block()
+    for name, mk, w, h, frames in CASES:
+        if a.only and a.only != name:
+            continue
+        sc = mk()
+        sp, mt = sc.objects_gpu(), sc.materials_gpu()
+        imgs = []
+        for f in frames:
+            t0 = time.time()
+            imgs.append(run_reference(shaders, cam.tobytes(), sp.tobytes(), mt.tobytes(), w, h, f))
+            print(f"{name} frame {f}: {time.time() - t0:.1f} s", flush=True)
+        np.savez_compressed(os.path.join(HERE, name + ".npz"),
+                            spheres=np.frombuffer(sp.tobytes(), np.uint8),
+                            materials=np.frombuffer(mt.tobytes(), np.uint8),
+                            camera=np.frombuffer(cam.tobytes(), np.uint8),
+                            params=np.array([w, h, 1, BOUNCE_LOOPS], np.uint32),
+                            frames=np.array(frames, np.uint32),
+                            images=np.stack(imgs))
+
+
+if __name__ == "__main__":
+    main()

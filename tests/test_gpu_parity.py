@@ -5,6 +5,7 @@ algorithmic segment counts, on the same seeded inputs. At full BASELINE sizes
 the oracle checks sampled rows, plus size-independent properties
 (determinism, reuse on/off identity, multi-pass identity, shard assembly).
 """
+import glob
 import os
 
 import numpy as np
@@ -56,6 +57,26 @@ CASES = [
     ("depth1", scene.rtiow_final_scene, 64, 36, 3, 1, 0),
     ("spheres10k", scene.ten_thousand_scene, 96, 54, 2, 8, 0),
 ]
+
+
+WGSL = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                     "wgsl_*.npz")))
+
+
+@pytest.mark.parametrize("flags", [0, NO_REUSE, CULL], ids=["reuse", "noreuse", "cull"])
+@pytest.mark.parametrize("path", WGSL, ids=[os.path.basename(p) for p in WGSL])
+def test_matches_interpreted_reference_wgsl(renderer, path, flags):
+    """The HIP path against frames of the reference's own WGSL kernels,
+    executed by tests/golden/wgsl_exec.py (spp 1, depth 3), bit for bit."""
+    z = np.load(path, allow_pickle=False)
+    sp = z["spheres"].view(abi.SPHERE_DTYPE)
+    mt = z["materials"].view(abi.MATERIAL_DTYPE)
+    cam = z["camera"].view(abi.CAMERA_DTYPE).reshape(())
+    W, H, S, D = (int(v) for v in z["params"])
+    renderer.set_scene(sp, mt)
+    for f, ref in zip(z["frames"], z["images"]):
+        img, _ = renderer.render(cam, W, H, S, D, frame0=int(f), flags=flags)
+        check_exact(img, ref)
 
 
 @pytest.mark.parametrize("flags", [0, NO_REUSE, CULL, CULL | NO_REUSE],
