@@ -9,7 +9,7 @@
  * Build: gcc -O2 -ffp-contract=off -fno-fast-math (oracle/Makefile). Every f32
  * operation below is one IEEE-754 round-to-nearest op; no FMA contraction, no
  * reassociation. Op forms fixed by this restatement (the WGSL leaves them to
- * the driver; SURVEY.md §8c "parity unpinned"):
+ * the driver -- the one part the WGSL-interpreter fixtures cannot pin):
  *   dot(a,b)     = (a.x*b.x + a.y*b.y) + a.z*b.z
  *   length(v)    = sqrt(dot(v,v))                (correctly rounded sqrt)
  *   normalize(v) = v / length(v)                 (3 correctly rounded divides)

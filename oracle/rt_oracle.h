@@ -10,10 +10,14 @@
  * (assets/shaders/{clear,generate,intersect,shade,collect}.wgsl of
  * brandon-reinhart/bevy_raytrace), with every floating-point operation order
  * fixed; see DESIGN.md "Oracle" for the op-form table.
- * Parity with the reference itself is UNPINNED: the reference ships no tests,
- * golden images or known-answer vectors, and its WGSL cannot run here
- * (SURVEY.md §8c). The oracle is pinned by the known-answer values of SURVEY
+ * The reference ships no tests, golden images or known-answer vectors and its
+ * WGSL has no runtime here. The oracle is pinned by the
+ * reference's own six shaders executed by a WGSL interpreter
+ * (tests/golden/wgsl_exec.py; fixtures tests/golden/wgsl_*.npz, bit-exact per
+ * frame at the reference's depth 3), by the known-answer values of SURVEY
  * Appendix C and by an independent numpy restatement (oracle/rt_oracle_np.py).
+ * Unpinned: the precision of the builtins the WGSL leaves to the driver
+ * (normalize, length, pow, tan; FMA fusion), fixed below.
  */
 #ifndef RT_ORACLE_H
 #define RT_ORACLE_H
