@@ -484,12 +484,22 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
     PROF_MARK(1);
 #ifdef RT_PROFILE
     PROF_ADD(6, wave_max_u32(cnt));
+#ifdef RT_PROF_NESTED  // c[14]: the nested drain's wave iterations, sum_k max_lanes popcount(m_k)
+    {
+        const uint32_t kmax = wave_max_u32(cnt);
+        for (uint32_t k = 0; k < kmax; ++k) {
+            const uint32_t pc = k < cnt ? (uint32_t)__popc(cq[k * 64 + lane] & 0xFFu) : 0u;
+            PROF_ADD(14, wave_max_u32(pc));
+        }
+    }
+#endif
 #endif
     drain_candidates<CULL>(cq, cnt, sph, o, d, a, fast, best_t, best_i, perm EXACT_PASS);
     PROF_MARK(2);
 #ifdef RT_PROFILE
     PROF_ADD(13, wave_max_u32(ecnt[0]));
-#ifdef RT_PROF_SUMFULL  // c[14]: lanes' full exact tests summed (not the wave max)
+#if defined(RT_PROF_NESTED)
+#elif defined(RT_PROF_SUMFULL)  // c[14]: lanes' full exact tests summed (not the wave max)
     {
         uint32_t sum1 = ecnt[1];
         for (int off = 32; off > 0; off >>= 1) sum1 += __shfl_xor(sum1, off);
