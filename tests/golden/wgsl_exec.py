@@ -1,6 +1,7 @@
-"""A small WGSL interpreter -- TEST INFRASTRUCTURE ONLY (golden-fixture
-generation, run in the build container; never imported by the product, by
-`pytest`, or on the GPU box).
+"""A small WGSL interpreter -- TEST INFRASTRUCTURE ONLY: used by
+tests/golden/make_wgsl_golden.py (fixture generation from the reference's
+shaders, in the build container) and by its own self-tests
+(tests/test_wgsl_exec.py, inline snippets); never imported by the product.
 
 It parses the subset of WGSL (naga 0.9 dialect) that the reference's compute
 shaders use and executes a kernel invocation by invocation on the CPU, with
