@@ -50,7 +50,7 @@ FLOPS_PER_SPHERE_TEST = 18  # intersect.wgsl:97-102, SURVEY §8d
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=12)
+    ap.add_argument("--steps", type=int, default=24)
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--config", default=HEADLINE, choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -66,7 +66,7 @@ def parse():
     ap.add_argument("--force-dist", action="store_true",
                     help="take the N>1 path (process group, shard gather, assembly) "
                          "even at world size 1")
-    ap.add_argument("--frames-per-launch", type=int, default=12,
+    ap.add_argument("--frames-per-launch", type=int, default=24,
                     help="frames per persistent launch (rt_render_frames_device)")
     ap.add_argument("--reuse-steps", type=int, default=4,
                     help="extra frames timed with primary-hit reuse on (0 = skip)")
@@ -142,6 +142,11 @@ def main():
 
     r = Renderer(local)
     r.set_scene(spheres, mats)
+    # work buffers of the largest launch this run makes, allocated before any
+    # step (rt_reserve) so no allocation lands inside a timed region
+    biggest = min(max(1, args.frames_per_launch),
+                  max(args.steps, args.warmup, args.reuse_steps, args.cull_steps, 1))
+    r.reserve(biggest, W, H, S, D, row_block=B, shard_count=world, shard_index=rank)
     # All device work of a step runs on ONE dedicated stream (non-null handle,
     # so the library enqueues on it rather than on its own stream).
     stream = torch.cuda.Stream()

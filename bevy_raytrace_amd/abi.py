@@ -122,6 +122,7 @@ _PROTOS = {
     "rt_render_device": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(RtParams), _VP, _VP]),
     "rt_render_frames_device": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(RtParams), ctypes.c_uint32,
                                                _VP, _VP]),
+    "rt_reserve": (ctypes.c_int, [_VP, ctypes.POINTER(RtParams), ctypes.c_uint32]),
     "rt_render_async": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(RtParams), _VP]),
     "rt_wait": (ctypes.c_int, [_VP, ctypes.POINTER(RtStats)]),
     "rt_assemble_shards": (ctypes.c_int, [_VP, _VP, _U32, _VP, _U32, _U32, _U32, _U32, _VP]),

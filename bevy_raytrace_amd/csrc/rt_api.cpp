@@ -157,7 +157,7 @@ static size_t scratch_limit() {
         unsigned long long v = strtoull(s, nullptr, 10);
         if (v >= 16) return (size_t)v;
     }
-    return (size_t)8 << 30;  // 8 GiB of block sums per pass (of 288 GB HBM)
+    return (size_t)16 << 30;  // 16 GiB of block sums per pass (of 288 GB HBM)
 }
 
 // RT_TAIL_SPLIT=0 turns the single-sample tail items off (A/B measurements).
@@ -691,10 +691,13 @@ int rt_update_materials(rt_ctx* ctx, uint32_t first, const rt_material* material
 // item of long paths when the queue runs dry. Frames go in one launch while
 // their block sums fit RT_SCRATCH_BYTES; a single frame larger than that runs
 // in several passes over its blocks (acc carries the partial sum).
+// reserve_only (rt_reserve): size and allocate the slot's buffers exactly as
+// the launch would, then return without enqueueing any work.
 static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params* prm,
                    uint32_t nframes, float4* d_out, hipStream_t stream, int prog_mode = 0,
-                   float prog_total = 0.0f) {
-    if (!cam || !prm) return fail(ctx, RT_ERR_INVALID_ARG, "camera or params is NULL");
+                   float prog_total = 0.0f, bool reserve_only = false) {
+    if ((!cam && !reserve_only) || !prm)
+        return fail(ctx, RT_ERR_INVALID_ARG, "camera or params is NULL");
     if (!ctx->has_scene) return fail(ctx, RT_ERR_NO_SCENE, "rt_render before rt_set_scene");
     const rt_params p = *prm;
     if (p.width == 0 || p.height == 0 || p.spp == 0 || p.max_depth == 0)
@@ -714,7 +717,7 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     const uint32_t rows = rt_shard_rows(p.height, B, K, p.shard_index);
     const uint32_t npix = rows * p.width;
     const uint32_t blocks_total = (p.spp + RT_SAMPLE_BLOCK - 1) / RT_SAMPLE_BLOCK;
-    if (!d_out) return fail(ctx, RT_ERR_INVALID_ARG, "output pointer is NULL");
+    if (!d_out && !reserve_only) return fail(ctx, RT_ERR_INVALID_ARG, "output pointer is NULL");
 
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     std::vector<Pass> passes;
@@ -799,6 +802,7 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         HIP_TRY(ctx, hipEventCreate(&e));
         f.ev.push_back(e);
     }
+    if (reserve_only) return RT_OK;
 
     KParams K_{};
     K_.width = p.width;
@@ -960,6 +964,17 @@ static int no_pending(rt_ctx* ctx, const char* who) {
     if (ctx->npending)
         return fail(ctx, RT_ERR_INVALID_ARG, "%s: %u async call(s) not waited for", who,
                     ctx->npending);
+    return RT_OK;
+}
+
+int rt_reserve(rt_ctx* ctx, const rt_params* params, uint32_t nframes) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_reserve: ctx is NULL");
+    int rc = no_pending(ctx, "rt_reserve");
+    if (rc) return rc;
+    for (int i = 0; i < RT_MAX_PENDING; ++i) {
+        rc = enqueue(ctx, ctx->fr[i], nullptr, params, nframes, nullptr, nullptr, 0, 0.0f, true);
+        if (rc) return rc;
+    }
     return RT_OK;
 }
 

@@ -134,6 +134,14 @@ class Renderer:
                                               ctypes.c_void_p(int(stream)) if stream else None)
         check(self.lib, self.ctx, rc)
 
+    def reserve(self, nframes, width, height, spp, max_depth, frame0=0, row_block=8,
+                shard_count=1, shard_index=0, flags=0):
+        """Allocate the work buffers of a render_frames_device(nframes, ...) in
+        every in-flight slot now (rt_reserve), so later renders allocate nothing."""
+        p = make_params(width, height, spp, max_depth, frame0, row_block, shard_count, shard_index,
+                        flags)
+        check(self.lib, self.ctx, self.lib.rt_reserve(self.ctx, ctypes.byref(p), int(nframes)))
+
     def wait(self):
         st = RtStats()
         rc = self.lib.rt_wait(self.ctx, ctypes.byref(st))

@@ -59,6 +59,8 @@ extern "C" {
     pub fn rt_render_frames_device(ctx: *mut rt_ctx, camera: *const c_void, params: *const rt_params,
                                    nframes: u32, out_rgba_device: *mut f32,
                                    stream: *mut c_void) -> c_int;
+    // allocate a launch's work buffers up front (RayTraceNode setup, not run)
+    pub fn rt_reserve(ctx: *mut rt_ctx, params: *const rt_params, nframes: u32) -> c_int;
     pub fn rt_wait(ctx: *mut rt_ctx, stats: *mut rt_stats) -> c_int;
     pub fn rt_intersect(ctx: *mut rt_ctx, rays: *const f32, n: u32, hit_index: *mut i32,
                         hit_t: *mut f32) -> c_int;

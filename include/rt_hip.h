@@ -238,6 +238,14 @@ int rt_render_device(rt_ctx* ctx, const rt_camera* camera, const rt_params* para
 int rt_render_frames_device(rt_ctx* ctx, const rt_camera* camera, const rt_params* params,
                             uint32_t nframes, float* out_rgba_device, void* stream);
 
+/* Allocate, up front, the device work buffers (block sums, pixel table,
+ * counters) that rt_render_frames_device(params, nframes) needs, in every
+ * frames-in-flight slot, without rendering -- the analogue of the reference
+ * sizing its ray / intersection buffers in its prepare systems
+ * (src/ray_trace_rays.rs:50-66) rather than inside RayTraceNode::run. Renders
+ * of that size or smaller then allocate nothing. No call may be pending. */
+int rt_reserve(rt_ctx* ctx, const rt_params* params, uint32_t nframes);
+
 /* Asynchronous host-output variant: enqueue, return; rt_wait() completes the
  * device->host copy into out_rgba and fills stats. */
 int rt_render_async(rt_ctx* ctx, const rt_camera* camera, const rt_params* params,

@@ -474,6 +474,30 @@ def test_frames_batch_errors(renderer):
         renderer.render_frames_device(cam, 2, 0, 8, 8, 1, 1)
 
 
+def test_reserve_then_render(renderer):
+    """rt_reserve allocates a launch's buffers up front; renders of that size
+    (and smaller) then match the oracle; reserve with a call pending fails."""
+    import torch
+    sp, mt = arrays(scene.rtiow_final_scene())
+    renderer.set_scene(sp, mt)
+    cam = default_camera_block()
+    W, H, S, D = 48, 27, 9, 6
+    renderer.reserve(3, W, H, S, D)
+    buf = torch.empty((3, H, W, 4), dtype=torch.float32, device="cuda")
+    renderer.render_frames_device(cam, 3, buf.data_ptr(), W, H, S, D, flags=NO_REUSE)
+    with pytest.raises(abi.RayTraceError) as e:
+        renderer.reserve(3, W, H, S, D)
+    assert e.value.status == abi.RT_ERR_INVALID_ARG
+    renderer.wait()
+    for i in range(3):
+        ref, _ = O.render(cam, sp, mt, W, H, S, D, frame0=i * S)
+        check_exact(buf[i].cpu().numpy(), ref)
+    img, _ = renderer.render(cam, W, H, 2, D)  # smaller than reserved
+    check_exact(img, O.render(cam, sp, mt, W, H, 2, D)[0])
+    with pytest.raises(abi.RayTraceError):
+        renderer.reserve(1, 0, H, S, D)
+
+
 @pytest.mark.parametrize("flags", [abi.RT_FLAG_JITTER, abi.RT_FLAG_THIN_LENS,
                                    abi.RT_FLAG_JITTER | abi.RT_FLAG_THIN_LENS,
                                    abi.RT_FLAG_JITTER | abi.RT_FLAG_THIN_LENS | NO_REUSE],

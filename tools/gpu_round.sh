@@ -14,6 +14,6 @@ timeout -k 10 400 python bench.py --config spheres10k1080 --steps 2 --warmup 1 -
     --reuse-steps 0 --cull-steps 2 --frames-per-launch 2 > gpurun_out/bench_10k.json 2>> gpurun_out/bench.err
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv \
-    -- python3 "$R/bench.py" --no-cpu-baseline --reuse-steps 0 --warmup 12 \
+    -- python3 "$R/bench.py" --no-cpu-baseline --reuse-steps 0 --warmup 24 \
     > "$R/gpurun_out/prof.log" 2>&1
 echo done
