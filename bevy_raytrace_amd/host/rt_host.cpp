@@ -258,6 +258,8 @@ void Renderer::update_materials(uint32_t first, const rt_material* mt, uint32_t 
     check(rt_update_materials(ctx_, first, mt, count));
 }
 
+void Renderer::reserve(const rt_params& p, uint32_t nframes) { check(rt_reserve(ctx_, &p, nframes)); }
+
 rt_stats Renderer::render(const rt_camera& cam, const rt_params& p, float* out) {
     rt_stats st{};
     check(rt_render(ctx_, &cam, &p, out, &st));
@@ -319,6 +321,18 @@ void RayTraceNode::update(World& world) {
     }
     sp_ = std::move(sp);
     mt_ = std::move(mt);
+    // size the frame's work buffers here, as the reference re-sizes its ray
+    // and intersection buffers in prepare when the ray count changes
+    // (ray_trace_rays.rs:50-66), not inside run
+    if (world.camera) {
+        const std::array<uint32_t, 4> key{world.camera->render_width, world.camera->render_height,
+                                          world.settings.samples_per_ray, world.settings.max_depth};
+        if (key != reserved_) {
+            renderer_->reserve(make_params(key[0], key[1], key[2], key[3], 0,
+                                           world.settings.flags), 1);
+            reserved_ = key;
+        }
+    }
 }
 
 rt_stats RayTraceNode::run(World& world) {

@@ -137,6 +137,8 @@ public:
     void set_scene(const std::vector<rt_sphere>& sp, const std::vector<rt_material>& mt);
     void update_spheres(uint32_t first, const rt_sphere* sp, uint32_t count);
     void update_materials(uint32_t first, const rt_material* mt, uint32_t count);
+    // allocate the work buffers of nframes-frame renders of p up front (rt_reserve)
+    void reserve(const rt_params& p, uint32_t nframes);
     // synchronous frame into host RGBA32F (rows x width x 4 floats)
     rt_stats render(const rt_camera& cam, const rt_params& p, float* out);
     rt_ctx* ctx() const { return ctx_; }
@@ -200,6 +202,8 @@ private:
     std::vector<rt_material> mt_;
     UploadCounts uploads_;
     rt_stats last_{};
+    // (width, height, spp, max_depth) the work buffers were last sized for
+    std::array<uint32_t, 4> reserved_{};
 };
 
 class RayTracePlugin {
