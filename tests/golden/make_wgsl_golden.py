@@ -14,9 +14,10 @@ reset} (src/ray_trace_globals.rs:56-68), rays / intersections zeroed
 128-B camera block (src/ray_trace_camera.rs:43-68) -- here our ABI records
 (bevy_raytrace_amd.abi), decoded by the shaders' own struct declarations.
 
-SAMPLES_PER_RAY = 1 and W*H a multiple of 128 (SURVEY.md Appendix B D1, D3:
-the reference's spp > 1 and floor-divided grid are not reproduced by the
-oracle). Each fixture holds the inputs and the per-frame output image; the
+SAMPLES_PER_RAY = 1 (the reference's spp > 1 is not
+reproduced by the oracle); where W*H is not a multiple of 128 the floor-divided
+grid leaves the last pixels untraced (D1) and `processed` says how many
+(row-major) pixels the comparison covers. Each fixture holds the inputs and the per-frame output image; the
 oracle is checked against it in tests/test_oracle.py (depth 3 = the
 reference's loop count).
 
@@ -48,14 +49,16 @@ CASES = [
     ("wgsl_config1_64x32", scene.config1_scene, 64, 32, (0, 1, 7, 1000)),
     ("wgsl_reference_32x16", scene.reference_scene, 32, 16, (0, 3)),
     ("wgsl_rtiow_16x8", scene.rtiow_final_scene, 16, 8, (0, 5)),
+    # W*H = 800: the reference's floor(800/128) = 6 workgroups trace the first
+    # 768 pixels only (D1); the test compares those
+    ("wgsl_config1_40x20_ragged", scene.config1_scene, 40, 20, (0, 2)),
 ]
 
 
 def run_reference(shaders, cam_bytes, sph_bytes, mat_bytes, width, height, frame):
     """One frame of RayTraceNode::run through the interpreted WGSL."""
     R = width * height
-    assert R % WORKGROUP == 0
-    groups = R // WORKGROUP
+    groups = R // WORKGROUP  # ray_trace_node.rs:37-38 (floor)
     first = shaders["clear"]
     globals_ = first.decode(first.var_type("globals"),
                             struct.pack("<9I", frame, width, height, 1, 0, 0, 0, 0, 0))
@@ -118,6 +121,7 @@ def main():
                             camera=np.frombuffer(cam.tobytes(), np.uint8),
                             params=np.array([w, h, 1, BOUNCE_LOOPS], np.uint32),
                             frames=np.array(frames, np.uint32),
+                            processed=np.array([(w * h) // WORKGROUP * WORKGROUP], np.uint32),
                             images=np.stack(imgs))
 
 

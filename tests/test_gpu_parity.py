@@ -74,9 +74,10 @@ def test_matches_interpreted_reference_wgsl(renderer, path, flags):
     cam = z["camera"].view(abi.CAMERA_DTYPE).reshape(())
     W, H, S, D = (int(v) for v in z["params"])
     renderer.set_scene(sp, mt)
+    n = int(z["processed"][0])  # pixels the reference's floor-divided grid traces (D1)
     for f, ref in zip(z["frames"], z["images"]):
         img, _ = renderer.render(cam, W, H, S, D, frame0=int(f), flags=flags)
-        check_exact(img, ref)
+        check_exact(img.reshape(-1, 4)[:n], ref.reshape(-1, 4)[:n])
 
 
 @pytest.mark.parametrize("flags", [0, NO_REUSE, CULL, CULL | NO_REUSE],

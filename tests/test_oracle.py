@@ -205,7 +205,7 @@ def test_golden_fixture(path):
 
 def test_golden_fixtures_present():
     assert len(GOLDEN) >= 4
-    assert len(WGSL) >= 3
+    assert len(WGSL) >= 4
 
 
 @pytest.mark.parametrize("path", WGSL, ids=[os.path.basename(p) for p in WGSL])
@@ -220,9 +220,11 @@ def test_oracle_matches_interpreted_reference_wgsl(path):
     cam = z["camera"].view(np.float32)
     W, H, S, D = (int(v) for v in z["params"])
     assert (S, D) == (1, 3)
+    n = int(z["processed"][0])  # pixels the reference's floor-divided grid traces (D1)
     for f, ref in zip(z["frames"], z["images"]):
         img, _ = O.render(cam, sp, mt, W, H, S, D, frame0=int(f), nthreads=4)
-        assert np.array_equal(img, ref, equal_nan=True), f"frame {int(f)}"
+        assert np.array_equal(img.reshape(-1, 4)[:n], ref.reshape(-1, 4)[:n],
+                              equal_nan=True), f"frame {int(f)}"
     # the fixture is not trivially sky: hits and misses, several materials
     assert len(np.unique(z["images"][0].reshape(-1, 4), axis=0)) > W * H // 4
 
