@@ -1,13 +1,13 @@
 #!/bin/bash
 # PMC passes over the headline bench command (one counter group per rocprofv3
 # run, --kernel-trace only; no sys/runtime trace with --pmc), each pass under
-# its own time limit. The command renders exactly one 12-frame launch
-# (--steps 12 --warmup 0), the launch the default bench line reports. Output under gpurun_out/pmc_*;
+# its own time limit. The command renders exactly one FPL-frame launch
+# (--steps FPL --warmup 0; FPL=24 = the default bench launch). Output under gpurun_out/pmc_*;
 # tools/pmc_summary.py turns it into profiles/.
 set -uo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd /tmp && export TMPDIR=/tmp
-FPL=${FPL:-12}
+FPL=${FPL:-24}
 CMD="python3 $R/bench.py --steps $FPL --warmup 0 --frames-per-launch $FPL --no-cpu-baseline --reuse-steps 0 --cull-steps 0"
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS" \

@@ -11,7 +11,7 @@ root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 out_dir = sys.argv[1] if len(sys.argv) > 1 else os.path.join(root, "gpurun_out")
 tag = sys.argv[2] if len(sys.argv) > 2 else "r01"
 wl = sys.argv[3] if len(sys.argv) > 3 else "rtiow1080"
-fpl = int(sys.argv[4]) if len(sys.argv) > 4 else 12
+fpl = int(sys.argv[4]) if len(sys.argv) > 4 else 24
 
 vals = defaultdict(lambda: defaultdict(list))   # kernel -> counter -> per-dispatch values
 durs = defaultdict(list)
