@@ -2,6 +2,8 @@
 intersect_world) against the oracle's brute-force reference loop
 (intersect.wgsl:94-143), bit-exact index and t, on adversarial rays aimed at
 the filter's decision boundary (tests/raygen.py)."""
+import glob
+import os
 import zlib
 
 import numpy as np
@@ -97,3 +99,24 @@ def test_cull_tie_goes_to_lower_index(renderer):
     # the ties really occur: with the order reversed the oracle picks sphere 1
     ri, rt = O.intersect_batch(sp[::-1].copy(), rays)
     assert ((ci == 0) & (ri == 0)).sum() > 100  # reversed list: index 0 = the old sphere 1
+
+
+WGSL_ISECT = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                           "wgsl_isect_*.npz")))
+
+
+@pytest.mark.parametrize("flags", [0, RT_FLAG_CULL], ids=["brute", "cull"])
+@pytest.mark.parametrize("path", WGSL_ISECT, ids=[os.path.basename(p) for p in WGSL_ISECT])
+def test_matches_reference_intersect_world(renderer, path, flags):
+    """rt_intersect against intersect.wgsl's own intersect_world (executed by
+    tests/golden/wgsl_exec.py) on adversarial rays: t bit for bit, misses,
+    and the hit sphere's material."""
+    from bevy_raytrace_amd.abi import MATERIAL_DTYPE, SPHERE_DTYPE
+    z = np.load(path, allow_pickle=False)
+    sp = z["spheres"].view(SPHERE_DTYPE)
+    renderer.set_scene(sp, z["materials"].view(MATERIAL_DTYPE))
+    idx, t = renderer.intersect(z["rays"], flags=flags)
+    assert np.array_equal(t, z["t"], equal_nan=True)
+    hit = idx >= 0
+    assert np.array_equal(~hit, z["t"] == np.float32(1e20))
+    assert np.array_equal(sp["material"][idx[hit]], z["material"][hit])

@@ -188,7 +188,19 @@ def test_nan_paths_are_reference_behaviour():
 # ------------------------------------------------------------ golden fixtures
 GOLDEN = sorted(p for p in glob.glob(os.path.join(HERE, "golden", "*.npz"))
                 if not os.path.basename(p).startswith("wgsl_"))
-WGSL = sorted(glob.glob(os.path.join(HERE, "golden", "wgsl_*.npz")))
+WGSL = sorted(p for p in glob.glob(os.path.join(HERE, "golden", "wgsl_*.npz"))
+              if not os.path.basename(p).startswith("wgsl_isect_"))
+WGSL_ISECT = sorted(glob.glob(os.path.join(HERE, "golden", "wgsl_isect_*.npz")))
+
+
+def check_against_reference_intersect(sp, z, idx, t):
+    """(index, t) of a closest-hit loop vs the record the reference's own
+    intersect_world returned: t bit for bit, misses at VERY_FAR, and the hit
+    sphere's material."""
+    assert np.array_equal(t, z["t"], equal_nan=True)
+    hit = idx >= 0
+    assert np.array_equal(~hit, z["t"] == np.float32(1e20))
+    assert np.array_equal(sp["material"][idx[hit]], z["material"][hit])
 
 
 @pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p) for p in GOLDEN])
@@ -205,7 +217,19 @@ def test_golden_fixture(path):
 
 def test_golden_fixtures_present():
     assert len(GOLDEN) >= 4
-    assert len(WGSL) >= 4
+    assert len(WGSL) >= 4 and len(WGSL_ISECT) >= 3
+
+
+@pytest.mark.parametrize("path", WGSL_ISECT, ids=[os.path.basename(p) for p in WGSL_ISECT])
+def test_oracle_intersect_matches_reference_intersect_world(path):
+    """Adversarial rays (grazing, on/inside surfaces, far origins, NaN/inf and
+    unnormalised directions; tests/raygen.py) through intersect.wgsl's own
+    intersect_world, executed by the WGSL interpreter."""
+    z = np.load(path, allow_pickle=False)
+    sp = z["spheres"].view(SPHERE_DTYPE)
+    idx, t = O.intersect_batch(sp, z["rays"])
+    check_against_reference_intersect(sp, z, idx, t)
+    assert 0 < (idx >= 0).sum() < len(idx)
 
 
 @pytest.mark.parametrize("path", WGSL, ids=[os.path.basename(p) for p in WGSL])
