@@ -59,8 +59,9 @@ CASES = [
 ]
 
 
-WGSL = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
-                                     "wgsl_*.npz")))
+WGSL = sorted(p for p in glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                "golden", "wgsl_*.npz"))
+              if not os.path.basename(p).startswith("wgsl_isect_"))  # frames only
 
 
 @pytest.mark.parametrize("flags", [0, NO_REUSE, CULL], ids=["reuse", "noreuse", "cull"])
