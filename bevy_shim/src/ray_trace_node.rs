@@ -29,6 +29,8 @@ pub struct SceneUploadState {
     spheres: Vec<u8>,
     materials: Vec<u8>,
     camera: Vec<u8>,
+    /// (width, height) the tracer's work buffers were last sized for
+    reserved: (u32, u32),
 }
 
 /// RenderStage::Prepare, after the reference's own prepare systems have filled
@@ -95,6 +97,25 @@ pub fn prepare_scene(
             state.materials = mat;
         }
         Err(e) => error!("scene upload: {e}"),
+    }
+
+    // Size the frame's work buffers here, not inside RayTraceNode::run, as the
+    // reference re-sizes its ray buffers in prepare (ray_trace_rays.rs:50-66).
+    let size = (camera.render_width, camera.render_height);
+    if size != state.reserved {
+        let params = rt_params {
+            width: size.0,
+            height: size.1,
+            spp: SAMPLES_PER_RAY as u32,
+            max_depth: 3, // ray_trace_node.rs:213
+            row_block: 8,
+            shard_count: 1,
+            ..Default::default()
+        };
+        match ctx.check(unsafe { rt_reserve(ctx.0, &params, 1) }) {
+            Ok(()) => state.reserved = size,
+            Err(e) => error!("rt_reserve: {e}"),
+        }
     }
 }
 
