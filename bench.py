@@ -7,7 +7,9 @@ through the persistent HIP kernel, depth 16, written to an HBM image. Inputs
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config rtiow1080]
 
-N > 1 is launched by torch.distributed.run (one process per GPU): the image
+N > 1 runs one process per GPU under torch.distributed.run; a bare
+`python bench.py --gpus N` (no WORLD_SIZE in the environment) launches that
+itself as a child process before touching the GPU and relays rank 0's line. The image
 is row-tiled in blocks dealt serpentine to the ranks, each rank
 renders its rows,
 then one RCCL gather over xGMI lands the shards on rank 0, which re-assembles
@@ -90,8 +92,41 @@ def load_traffic(workload_key, frames_per_launch):
         return None
 
 
+def spawn_ranks(args):
+    """`--gpus N` (N > 1) without a torch.distributed launcher around us: run
+    N ranks as a CHILD `python -m torch.distributed.run` (never an exec: this
+    process may not replace itself once anything touched the GPU, and nothing
+    has yet), relay rank 0's JSON line and exit with the launcher's status."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    proc = subprocess.run(cmd, stdout=subprocess.PIPE, env=env)
+    line = None
+    for raw in proc.stdout.decode(errors="replace").splitlines():
+        t = raw.strip()
+        if t.startswith("{") and '"metric"' in t:
+            line = t
+        elif t:
+            print(t, file=sys.stderr)
+    if proc.returncode == 0 and line is None:
+        print("bench.py: no result line from rank 0", file=sys.stderr)
+        return 3
+    if line is not None:
+        print(line, flush=True)
+    return proc.returncode
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     # stdout carries exactly the one JSON line: libraries that print to fd 1
     # (RCCL's version banner at communicator init, HIP runtime notes) are sent
     # to stderr; the result is written to the saved stdout at the end.
@@ -105,10 +140,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print(f"--gpus {args.gpus} needs torch.distributed.run (one process per GPU)",
-                  file=sys.stderr)
-            sys.exit(2)
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; using the launcher's "
+              f"{world} ranks", file=sys.stderr)
     if args.same_device:
         local = 0
     # --force-dist at world 1: the N>1 data path (shard slab, gather through the
@@ -341,11 +374,23 @@ def main():
         dist.destroy_process_group()
 
 
+def cpu_quota():
+    """CPUs granted by the cgroup v2 quota (cpu.max), or None when unlimited."""
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(period), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(cam, spheres, mats, W, H, S, D, nrows, gpu_image):
     """Time the C oracle (scalar port of the WGSL) on a bounded row sample."""
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
-    cores = max(1, min(16, os.cpu_count() or 1))
+    # every host core this process may run on (no cap); the cgroup CPU quota,
+    # when there is one, is reported beside it
+    cores = len(os.sched_getaffinity(0)) or 1
+    quota = cpu_quota()
     # calibrate on `cores` spread rows (one row per thread), then size the
     # sample for ~10 s of wall time
     rows = [int(i * H / cores) for i in range(cores)]
@@ -360,7 +405,8 @@ def cpu_baseline(cam, spheres, mats, W, H, S, D, nrows, gpu_image):
     img, segs = O.render_rows(cam, spheres, mats, W, H, S, D, rows, nthreads=cores)
     dt = time.perf_counter() - t0
     exact = bool(np.array_equal(img, gpu_image[rows], equal_nan=True))
-    return {"value": round(segs / dt / 1e6, 3), "unit": "Mrays/s", "cores": cores, "kind": "port",
+    return {"value": round(segs / dt / 1e6, 3), "unit": "Mrays/s", "cores": cores,
+            "cpu_quota_cores": quota, "kind": "port",
             "sample": f"{len(rows)} rows (every {stride}th) of the same {W}x{H} {S}spp frame, "
                       f"{segs} segments in {dt:.2f} s",
             "gpu_rows_bit_exact": exact}

@@ -185,6 +185,12 @@ def load(path=None):
     if hasattr(lib, "rt_debug_counters"):  # internal diagnostic symbol
         lib.rt_debug_counters.restype = ctypes.c_int
         lib.rt_debug_counters.argtypes = [_VP, ctypes.POINTER(ctypes.c_uint64)]
+    if hasattr(lib, "rt_debug_tune"):  # internal A/B knobs (tests, tools/)
+        lib.rt_debug_tune.restype = ctypes.c_int
+        lib.rt_debug_tune.argtypes = [_VP, ctypes.c_char_p, ctypes.c_char_p]
+    if hasattr(lib, "rt_debug_alloc_count"):  # internal (tests)
+        lib.rt_debug_alloc_count.restype = ctypes.c_uint64
+        lib.rt_debug_alloc_count.argtypes = [_VP]
     if hasattr(lib, "rt_debug_cull_layout"):  # internal, host only (tests/test_cull.py)
         lib.rt_debug_cull_layout.restype = ctypes.c_int
         lib.rt_debug_cull_layout.argtypes = [_VP, _U32, _VP, _VP, _U32, _VP, _U32]

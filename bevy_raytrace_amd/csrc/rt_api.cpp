@@ -10,7 +10,7 @@
 //
 // Per call: memset the work/segment counters, then per sample-block pass one
 // persistent render launch + one collect launch (a single pass unless the
-// block-sum scratch would exceed RT_SCRATCH_BYTES), timed with HIP events on
+// block-sum scratch would exceed the scratch_bytes budget, 16 GiB), timed with HIP events on
 // the stream they run on.
 
 #include <hip/hip_runtime.h>
@@ -60,14 +60,35 @@ struct Frame {
     uint32_t short_math = 0;        // KParams.scene_fast of the call
 };
 
+// A/B and fault-injection knobs of one context (rt_debug_tune, internal). The
+// defaults ARE the product: nothing reads the environment, so a stray
+// variable in a host application cannot change the schedule. Every setting
+// gives the same bits (tested); they exist for the measurements in DESIGN.md.
+struct Tuning {
+    size_t scratch_bytes = (size_t)16 << 30;  // block sums per launch (of 288 GB HBM)
+    bool split_all = false;       // without primary reuse, every block as single samples
+    bool tail_split = true;       // single-sample tail items at the end of a launch
+    double tail[3] = {0.0, 0.0, 12.0};  // tail regions (4-, 2-, 1-sample items) x D x lanes
+    bool prefetch = true;         // waves prefetch their next work chunk
+    uint32_t prio_mode = 1;       // s_setprio rotation: 0 off, 1 by iteration, 3 by wall time
+    uint32_t prio_shift = 14;     // mode 3 step: 2^prio_shift ticks of 10 ns
+    uint32_t wg_per_cu = 0;       // resident workgroups per CU (0 = occupancy limit)
+    int64_t wide_max = -1;        // sphere-parallel threshold (-1 = cost model)
+    bool fast_exact = true;       // short correctly-rounded exact test when in domain
+    int64_t fail_alloc_after = -1;  // fault injection: device allocations left (-1 = off)
+};
+
 struct rt_ctx {
     int device = 0;
     std::string err;
     int cu_count = 0;
     int blocks_per_cu = 0;
+    Tuning tune;
+    uint64_t allocs = 0;            // device allocations made (rt_debug_alloc_count)
 
     // scene
     bool has_scene = false;
+    bool cull_dirty = true;         // the culled list is rebuilt at the next RT_FLAG_CULL call
     bool scene_fast = false;  // scene_fast_ok(): the exact tests may take the short divide/sqrt
     uint32_t n = 0, ngroups = 0, m = 0;
     float4* d_grp = nullptr;        // groups of RT_GROUP=8 spheres, SoA (cx[8], cy[8], cz[8], S[8])
@@ -134,8 +155,13 @@ static int ensure(rt_ctx* ctx, T** p, size_t* cap, size_t bytes) {
         *cap = 0;
     }
     if (bytes == 0) return RT_OK;
+    if (ctx->tune.fail_alloc_after == 0)
+        return fail(ctx, RT_ERR_OUT_OF_MEMORY, "hipMalloc(%zu) failed: injected (rt_debug_tune)",
+                    bytes);
+    if (ctx->tune.fail_alloc_after > 0) --ctx->tune.fail_alloc_after;
     HIP_TRY(ctx, hipMalloc((void**)p, bytes));
     *cap = bytes;
+    ++ctx->allocs;
     return RT_OK;
 }
 
@@ -151,47 +177,48 @@ static FastDiv make_fastdiv(uint32_t d) {
     return f;
 }
 
-static size_t scratch_limit() {
-    const char* s = getenv("RT_SCRATCH_BYTES");
-    if (s && *s) {
-        unsigned long long v = strtoull(s, nullptr, 10);
-        if (v >= 16) return (size_t)v;
+// One knob of rt_debug_tune: name -> field. Returns false for an unknown name
+// or a malformed value (the knob is left unchanged).
+static bool tune_set(Tuning& t, const char* name, const char* v) {
+    char* end = nullptr;
+    auto num = [&](double& out) {
+        out = strtod(v, &end);
+        return end != v && *end == '\0';
+    };
+    double x = 0.0;
+    if (!strcmp(name, "tail")) {
+        double w[3];
+        if (sscanf(v, "%lf,%lf,%lf", &w[0], &w[1], &w[2]) != 3 || w[0] < 0 || w[1] < 0 || w[2] < 0)
+            return false;
+        for (int i = 0; i < 3; ++i) t.tail[i] = w[i];
+        return true;
     }
-    return (size_t)16 << 30;  // 16 GiB of block sums per pass (of 288 GB HBM)
-}
-
-// RT_TAIL_SPLIT=0 turns the single-sample tail items off (A/B measurements).
-// RT_SPLIT_ALL=1: without primary reuse, trace EVERY block as single samples
-// (the round-1 policy; A/B measurements).
-static bool split_all_enabled() {
-    const char* s = getenv("RT_SPLIT_ALL");
-    return s && s[0] == '1';
-}
-
-// RT_TAIL="a4,a2,a1": tail region lengths (A/B measurements; see enqueue).
-static void tail_weights(double w[3]) {
-    const char* s = getenv("RT_TAIL");
-    if (!s || !*s) return;
-    double v[3];
-    if (sscanf(s, "%lf,%lf,%lf", &v[0], &v[1], &v[2]) == 3 && v[0] >= 0 && v[1] >= 0 && v[2] >= 0)
-        for (int i = 0; i < 3; ++i) w[i] = v[i];
-}
-
-static bool tail_split_enabled() {
-    const char* s = getenv("RT_TAIL_SPLIT");
-    return !(s && s[0] == '0');
-}
-
-static uint32_t env_uint(const char* name, uint32_t dflt) {
-    const char* s = getenv(name);
-    if (!s || !*s) return dflt;
-    return (uint32_t)strtoul(s, nullptr, 10);
-}
-
-static bool env_flag(const char* name, bool dflt) {
-    const char* s = getenv(name);
-    if (!s || !*s) return dflt;
-    return s[0] != '0';
+    if (!num(x)) return false;
+    if (!strcmp(name, "scratch_bytes")) {
+        if (x < 16) return false;
+        t.scratch_bytes = (size_t)x;
+    } else if (!strcmp(name, "split_all")) {
+        t.split_all = x != 0;
+    } else if (!strcmp(name, "tail_split")) {
+        t.tail_split = x != 0;
+    } else if (!strcmp(name, "prefetch")) {
+        t.prefetch = x != 0;
+    } else if (!strcmp(name, "prio_mode")) {
+        t.prio_mode = (uint32_t)x;
+    } else if (!strcmp(name, "prio_shift")) {
+        t.prio_shift = (uint32_t)x;
+    } else if (!strcmp(name, "wg_per_cu")) {
+        t.wg_per_cu = (uint32_t)x;
+    } else if (!strcmp(name, "wide_max")) {
+        t.wide_max = (int64_t)x;
+    } else if (!strcmp(name, "fast_exact")) {
+        t.fast_exact = x != 0;
+    } else if (!strcmp(name, "fail_alloc_after")) {
+        t.fail_alloc_after = (int64_t)x;
+    } else {
+        return false;
+    }
+    return true;
 }
 
 extern "C" {
@@ -610,6 +637,12 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n, const rt_mat
     ctx->h_mats.assign(materials, materials + m);
     rc = quiesce(ctx);
     if (rc) return rc;
+    // From here on the device buffers change: until every upload succeeded
+    // there is no scene (a failed call leaves RT_ERR_NO_SCENE, never a
+    // half-written or freed list behind stale counts).
+    ctx->has_scene = false;
+    ctx->cull_dirty = true;
+    ctx->n = ctx->ngroups = ctx->m = 0;
     rc = ensure(ctx, &ctx->d_sph, &ctx->sph_cap, sizeof(float4) * nrec);
     if (rc) return rc;
     rc = ensure(ctx, &ctx->d_grp, &ctx->grp_cap, sizeof(float4) * nrec);
@@ -628,9 +661,20 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n, const rt_mat
     ctx->ngroups = ngroups;
     ctx->m = m;
     ctx->scene_fast = scene_fast_ok(ctx);
-    rc = build_cull(ctx);
+    ctx->has_scene = true;  // the culled list follows lazily (cull_ready)
+    return RT_OK;
+}
+
+// The culled list of the current scene, (re)built on the first RT_FLAG_CULL
+// call after rt_set_scene / rt_update_spheres. No kernel can be reading the
+// old one: those calls quiesce, and the first culled call after them builds
+// before it enqueues. A failed build leaves it dirty (the next call retries).
+static int cull_ready(rt_ctx* ctx) {
+    if (!ctx->cull_dirty) return RT_OK;
+    ctx->n_c = ctx->ngroups_c = ctx->nclusters_c = 0;
+    int rc = build_cull(ctx);
     if (rc) return rc;
-    ctx->has_scene = true;
+    ctx->cull_dirty = false;
     return RT_OK;
 }
 
@@ -656,7 +700,8 @@ int rt_update_spheres(rt_ctx* ctx, uint32_t first, const rt_sphere* spheres, uin
     HIP_TRY(ctx, hipMemcpy(ctx->d_grp + RT_GROUP * g0, &ctx->h_grp[RT_GROUP * g0],
                            sizeof(float4) * RT_GROUP * (g1 - g0), hipMemcpyHostToDevice));
     ctx->scene_fast = scene_fast_ok(ctx);
-    return build_cull(ctx);
+    ctx->cull_dirty = true;  // the permutation and bounds follow at the next culled call
+    return RT_OK;
 }
 
 int rt_update_materials(rt_ctx* ctx, uint32_t first, const rt_material* materials,
@@ -689,7 +734,7 @@ int rt_update_materials(rt_ctx* ctx, uint32_t first, const rt_material* material
 // tail (the last `ksplit` blocks of every frame, dealt after all block items)
 // is traced as single-sample items, so no wave is left holding an 8-sample
 // item of long paths when the queue runs dry. Frames go in one launch while
-// their block sums fit RT_SCRATCH_BYTES; a single frame larger than that runs
+// their block sums fit the scratch budget; a single frame larger than that runs
 // in several passes over its blocks (acc carries the partial sum).
 // reserve_only (rt_reserve): size and allocate the slot's buffers exactly as
 // the launch would, then return without enqueueing any work.
@@ -723,21 +768,21 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     std::vector<Pass> passes;
     const size_t per_block = (size_t)npix * sizeof(float4);  // one slot per pixel
     // Tail: per lane ~a1*D single samples, and before them optionally a2*D
-    // samples in 2-sample items and a4*D in 4-sample items (RT_TAIL="a4,a2,a1";
+    // samples in 2-sample items and a4*D in 4-sample items (knob tail="a4,a2,a1";
     // default 0,0,12 = single samples only, the measured best on the RTIOW
     // frames): a block item (<= 8*D iterations) taken before the tail has
     // finished when the queue runs dry, and an item taken in the tail leaves
     // at most one short path per lane to drain. In samples per pixel:
+    const Tuning& tn = ctx->tune;
     const uint64_t lanes = (uint64_t)ctx->cu_count * ctx->blocks_per_cu * RT_BLOCK_THREADS;
-    bool tail_on = tail_split_enabled();
-    double ta[3] = {0.0, 0.0, 12.0};
-    tail_weights(ta);
+    bool tail_on = tn.tail_split;
+    const double* ta = tn.tail;
     auto per_px = [&](double a, uint64_t mult) -> uint64_t {
         if (!npix || a <= 0.0) return 0;
         const uint64_t v = (uint64_t)std::ceil(a * p.max_depth * (double)lanes / (double)npix);
         return (v + mult - 1) / mult * mult;
     };
-    const bool all_single = split_all_enabled() && (p.flags & RT_FLAG_NO_PRIMARY_CACHE);
+    const bool all_single = tn.split_all && (p.flags & RT_FLAG_NO_PRIMARY_CACHE);
     const uint64_t A4 = all_single ? 0 : per_px(ta[0], 4), A2 = all_single ? 0 : per_px(ta[1], 2);
     const uint64_t A1 = all_single ? ~0ull / 4 : per_px(ta[2], 1);
     auto tail_pairs = [&](uint64_t pairs) -> uint64_t {
@@ -759,7 +804,7 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         return pairs - L + (g_end - g0);
     };
     if (npix) {
-        uint64_t slots_cap = scratch_limit() / per_block;
+        uint64_t slots_cap = tn.scratch_bytes / per_block;
         const uint64_t by_index = 0x7FFFFFFFull / npix;  // work items fit in u32
         if (slots_cap > by_index) slots_cap = by_index;
         if (slots_cap < 1) slots_cap = 1;
@@ -803,6 +848,11 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         f.ev.push_back(e);
     }
     if (reserve_only) return RT_OK;
+    const bool cull = (p.flags & RT_FLAG_CULL) != 0;
+    if (cull) {
+        int rc = cull_ready(ctx);
+        if (rc) return rc;
+    }
 
     KParams K_{};
     K_.width = p.width;
@@ -814,7 +864,6 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     K_.shard_count = K;
     K_.shard_index = p.shard_index;
     K_.npix = npix;
-    const bool cull = (p.flags & RT_FLAG_CULL) != 0;
     K_.nspheres = cull ? ctx->n_c : ctx->n;
     K_.ngroups = cull ? ctx->ngroups_c : ctx->ngroups;
     if (cull) {
@@ -826,7 +875,7 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         // (10 000 spheres) it saves 14 % (3,115 vs 2,685)
         K_.cull_supers = ctx->nclusters_c > 16 ? 1u : 0u;
     }
-    K_.scene_fast = ctx->scene_fast && env_flag("RT_FAST_EXACT", true) ? 1u : 0u;
+    K_.scene_fast = ctx->scene_fast && tn.fast_exact ? 1u : 0u;
     K_.flags = p.flags;
     std::memcpy(K_.T, cam->transform, sizeof(K_.T));
     K_.tan_half = (float)std::tan((double)(cam->fov / 2.0f));                 // generate.wgsl:67
@@ -844,13 +893,13 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     K_.tile_wrem = p.width % 8;
     K_.div_8w = make_fastdiv(8 * p.width);
     K_.div_wrem = make_fastdiv(K_.tile_wrem ? K_.tile_wrem : 1);
-    K_.prefetch = env_flag("RT_PREFETCH", true) ? 1u : 0u;
-    K_.prio_mode = env_uint("RT_PRIO", 1);
-    K_.prio_shift = env_uint("RT_PRIO_SHIFT", 14);
+    K_.prefetch = tn.prefetch ? 1u : 0u;
+    K_.prio_mode = tn.prio_mode;
+    K_.prio_shift = tn.prio_shift;
     // wide (sphere-parallel) tracing pays ~32 VALU per 64 spheres per ray plus
     // a reduction; the ray-parallel walk ~34 per 8-sphere group per wave plus
-    // the drain: switch while k rays cost less sphere-parallel. RT_WIDE_MAX
-    // overrides (0 = never).
+    // the drain: switch while k rays cost less sphere-parallel. The wide_max
+    // knob overrides (0 = never).
     {
         const uint64_t per_ray = (uint64_t)((K_.nspheres + 63) / 64) * 32 + 48;
         // culled walk: the cluster bounds plus, measured on the RTIOW scene,
@@ -858,18 +907,30 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         uint64_t k = ((cull ? (uint64_t)K_.nclusters * 40 + (uint64_t)K_.ngroups * 34 / 4
                             : (uint64_t)K_.ngroups * 34) + 300) / per_ray;
         if (k > 16) k = 16;
-        const char* e = getenv("RT_WIDE_MAX");
-        if (e && *e) k = strtoul(e, nullptr, 10);
+        if (tn.wide_max >= 0) k = (uint64_t)tn.wide_max;
         K_.wide_max = (uint32_t)k;
     }
 
-    HIP_TRY(ctx, hipEventRecord(f.ev_t0, stream));
-    HIP_TRY(ctx, hipMemsetAsync(f.d_counters, 0, words_pad * sizeof(uint32_t), stream));
-    // RT_WG_PER_CU < occupancy: fewer co-resident waves per SIMD (A/B)
-    const uint32_t wg_per_cu = std::min<uint32_t>(env_uint("RT_WG_PER_CU", ctx->blocks_per_cu),
-                                                  ctx->blocks_per_cu);
+    // From the first enqueued operation on, a failure must not leave work
+    // running that the slot does not know about (the next enqueue could free
+    // buffers under it): HIP_TRY_Q waits for what was enqueued, then reports.
+#define HIP_TRY_Q(call)                                                   \
+    do {                                                                  \
+        hipError_t eq_ = (call);                                          \
+        if (eq_ != hipSuccess) {                                          \
+            hipStreamSynchronize(stream);                                 \
+            return fail(ctx, RT_ERR_DEVICE, "%s failed: %s", #call,       \
+                        hipGetErrorString(eq_));                          \
+        }                                                                 \
+    } while (0)
+    HIP_TRY_Q(hipEventRecord(f.ev_t0, stream));
+    HIP_TRY_Q(hipMemsetAsync(f.d_counters, 0, words_pad * sizeof(uint32_t), stream));
+    // wg_per_cu < occupancy: fewer co-resident waves per SIMD (A/B)
+    const uint32_t wg_per_cu = std::min<uint32_t>(
+        ctx->tune.wg_per_cu ? ctx->tune.wg_per_cu : (uint32_t)ctx->blocks_per_cu,
+        (uint32_t)ctx->blocks_per_cu);
     const uint32_t grid_full = (uint32_t)(ctx->cu_count * (wg_per_cu ? wg_per_cu : 1));
-    if (npix) HIP_TRY(ctx, rt_launch_primary(&K_, f.d_pd, stream));
+    if (npix) HIP_TRY_Q(rt_launch_primary(&K_, f.d_pd, stream));
     for (size_t i = 0; i < passes.size(); ++i) {
         const Pass& ps = passes[i];
         K_.block_begin = ps.block_begin;
@@ -900,23 +961,24 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         const uint32_t grid = (uint32_t)(need_blocks < grid_full ? need_blocks : grid_full);
         const uint64_t tail_items = 2ull * RT_WAVE_CHUNK * grid * (RT_BLOCK_THREADS / 64);
         K_.tail_start = (uint32_t)(items > tail_items ? items - tail_items : 0);
-        HIP_TRY(ctx, hipEventRecord(f.ev[2 * i], stream));
-        HIP_TRY(ctx, rt_launch_render(&K_, cull ? ctx->d_grp_c : ctx->d_grp,
+        HIP_TRY_Q(hipEventRecord(f.ev[2 * i], stream));
+        HIP_TRY_Q(rt_launch_render(&K_, cull ? ctx->d_grp_c : ctx->d_grp,
                                       cull ? ctx->d_sph_c : ctx->d_sph,
                                       cull ? ctx->d_rm_c : ctx->d_sph_rm, ctx->d_mats, f.d_pd,
                                       f.d_block_sums,
                                       f.d_counters + RT_CNT_WORK_OFFSET + i,
                                       reinterpret_cast<unsigned long long*>(f.d_counters),
                                       grid, stream));
-        HIP_TRY(ctx, hipEventRecord(f.ev[2 * i + 1], stream));
+        HIP_TRY_Q(hipEventRecord(f.ev[2 * i + 1], stream));
         const bool first_pass = ps.block_begin == 0;
         const bool last_pass = ps.block_begin + ps.nblocks == blocks_total;
-        HIP_TRY(ctx, rt_launch_collect(&K_, f.d_pd, f.d_block_sums, f.d_acc, first_pass, last_pass,
+        HIP_TRY_Q(rt_launch_collect(&K_, f.d_pd, f.d_block_sums, f.d_acc, first_pass, last_pass,
                                        (float)p.spp, d_out + (size_t)ps.frame_begin * npix,
                                        ctx->d_prog, prog_mode, prog_total, stream));
     }
-    HIP_TRY(ctx, hipMemcpyAsync(f.h_segs, f.d_counters, 18 * sizeof(unsigned long long),
+    HIP_TRY_Q(hipMemcpyAsync(f.h_segs, f.d_counters, 18 * sizeof(unsigned long long),
                                 hipMemcpyDeviceToHost, stream));
+#undef HIP_TRY_Q
     f.passes = (uint32_t)passes.size();
     f.short_math = K_.scene_fast;
     f.paths = (uint64_t)npix * p.spp * nframes;
@@ -967,12 +1029,41 @@ static int no_pending(rt_ctx* ctx, const char* who) {
     return RT_OK;
 }
 
+// Host-output bytes of one frame of `p` (rt_render_async; its staging buffer
+// holds at least 16 bytes).
+static size_t out_bytes(const rt_params* p) {
+    const uint32_t K = p->shard_count ? p->shard_count : 1;
+    const uint32_t rows = rt_shard_rows(p->height, p->row_block, K, p->shard_index);
+    return (size_t)rows * p->width * sizeof(float4);
+}
+
+// The enqueue's completion: the optional device->host copy and the slot's end
+// event, then the slot counts as pending. If either fails, the work already
+// enqueued is waited for (nothing keeps running that no slot tracks).
+static int commit(rt_ctx* ctx, Frame& f, hipStream_t s, void* host_dst, const void* dev_src,
+                  size_t bytes) {
+    hipError_t e = hipSuccess;
+    if (bytes) e = hipMemcpyAsync(host_dst, dev_src, bytes, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipEventRecord(f.ev_t1, s);
+    if (e != hipSuccess) {
+        hipStreamSynchronize(s);
+        return fail(ctx, RT_ERR_DEVICE, "enqueue completion failed: %s", hipGetErrorString(e));
+    }
+    f.pending_stream = s;
+    ++ctx->npending;
+    return RT_OK;
+}
+
 int rt_reserve(rt_ctx* ctx, const rt_params* params, uint32_t nframes) {
     if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_reserve: ctx is NULL");
     int rc = no_pending(ctx, "rt_reserve");
     if (rc) return rc;
     for (int i = 0; i < RT_MAX_PENDING; ++i) {
-        rc = enqueue(ctx, ctx->fr[i], nullptr, params, nframes, nullptr, nullptr, 0, 0.0f, true);
+        Frame& f = ctx->fr[i];
+        rc = enqueue(ctx, f, nullptr, params, nframes, nullptr, nullptr, 0, 0.0f, true);
+        if (rc) return rc;
+        // and the host-output staging of rt_render / rt_render_async (one frame)
+        rc = ensure(ctx, &f.d_out, &f.out_cap, std::max<size_t>(out_bytes(params), 16));
         if (rc) return rc;
     }
     return RT_OK;
@@ -986,10 +1077,7 @@ int rt_render_device(rt_ctx* ctx, const rt_camera* camera, const rt_params* para
     hipStream_t s = stream ? (hipStream_t)stream : f->stream;
     int rc = enqueue(ctx, *f, camera, params, 1, reinterpret_cast<float4*>(out_rgba_device), s);
     if (rc) return rc;
-    HIP_TRY(ctx, hipEventRecord(f->ev_t1, s));
-    f->pending_stream = s;
-    ++ctx->npending;
-    return RT_OK;
+    return commit(ctx, *f, s, nullptr, nullptr, 0);
 }
 
 int rt_render_frames_device(rt_ctx* ctx, const rt_camera* camera, const rt_params* params,
@@ -1000,10 +1088,7 @@ int rt_render_frames_device(rt_ctx* ctx, const rt_camera* camera, const rt_param
     hipStream_t s = stream ? (hipStream_t)stream : f->stream;
     int rc = enqueue(ctx, *f, camera, params, nframes, reinterpret_cast<float4*>(out_rgba_device), s);
     if (rc) return rc;
-    HIP_TRY(ctx, hipEventRecord(f->ev_t1, s));
-    f->pending_stream = s;
-    ++ctx->npending;
-    return RT_OK;
+    return commit(ctx, *f, s, nullptr, nullptr, 0);
 }
 
 int rt_render_async(rt_ctx* ctx, const rt_camera* camera, const rt_params* params, float* out_rgba) {
@@ -1012,19 +1097,12 @@ int rt_render_async(rt_ctx* ctx, const rt_camera* camera, const rt_params* param
     if (!params) return fail(ctx, RT_ERR_INVALID_ARG, "rt_render_async: params is NULL");
     Frame* f = next_slot(ctx, "rt_render_async");
     if (!f) return RT_ERR_INVALID_ARG;
-    const uint32_t K = params->shard_count ? params->shard_count : 1;
-    const uint32_t rows = rt_shard_rows(params->height, params->row_block, K, params->shard_index);
-    const size_t bytes = (size_t)rows * params->width * sizeof(float4);
-    int rc = ensure(ctx, &f->d_out, &f->out_cap, bytes ? bytes : 16);
+    const size_t bytes = out_bytes(params);
+    int rc = ensure(ctx, &f->d_out, &f->out_cap, std::max<size_t>(bytes, 16));
     if (rc) return rc;
     rc = enqueue(ctx, *f, camera, params, 1, f->d_out, f->stream);
     if (rc) return rc;
-    if (bytes)
-        HIP_TRY(ctx, hipMemcpyAsync(out_rgba, f->d_out, bytes, hipMemcpyDeviceToHost, f->stream));
-    HIP_TRY(ctx, hipEventRecord(f->ev_t1, f->stream));
-    f->pending_stream = f->stream;
-    ++ctx->npending;
-    return RT_OK;
+    return commit(ctx, *f, f->stream, out_rgba, f->d_out, bytes);
 }
 
 int rt_wait(rt_ctx* ctx, rt_stats* stats) {
@@ -1128,6 +1206,8 @@ int rt_intersect_ex(rt_ctx* ctx, const float* rays, uint32_t n, uint32_t flags, 
         return fail(ctx, RT_ERR_INVALID_ARG, "rt_intersect: NULL array");
     int rc = no_pending(ctx, "rt_intersect");
     if (rc) return rc;
+    const bool cull = (flags & RT_FLAG_CULL) != 0;
+    if (cull && (rc = cull_ready(ctx)) != RT_OK) return rc;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     void* buf = nullptr;
     const size_t rb = sizeof(float) * 6 * (size_t)n, ob = sizeof(int32_t) * (size_t)n;
@@ -1136,10 +1216,9 @@ int rt_intersect_ex(rt_ctx* ctx, const float* rays, uint32_t n, uint32_t flags, 
     hipError_t e = hipMemcpyAsync(b, rays, rb, hipMemcpyHostToDevice, ctx->stream);
     if (e == hipSuccess)
     {
-        const bool cull = (flags & RT_FLAG_CULL) != 0 && ctx->d_bnd_c;
         e = rt_launch_intersect(cull ? ctx->d_grp_c : ctx->d_grp, cull ? ctx->d_sph_c : ctx->d_sph,
                                 cull ? ctx->ngroups_c : ctx->ngroups,
-                                ctx->scene_fast && env_flag("RT_FAST_EXACT", true) ? 1u : 0u,
+                                ctx->scene_fast && ctx->tune.fast_exact ? 1u : 0u,
                                 (const float*)b, n, (int*)(b + rb), (float*)(b + rb + ob),
                                 cull ? ctx->d_bnd_c : nullptr, cull ? ctx->d_perm_c : nullptr,
                                 cull ? ctx->nclusters_c : 0u, ctx->stream);
@@ -1186,6 +1265,27 @@ int rt_debug_counters(const rt_ctx* ctx, uint64_t* out16) {
     for (int i = 0; i < 16; ++i) out16[i] = ctx->dbg[i];
     return RT_OK;
 }
+
+// Internal (not in include/rt_hip.h): set one A/B or fault-injection knob of
+// ctx (struct Tuning above; names: scratch_bytes, split_all, tail_split, tail
+// "a4,a2,a1", prefetch, prio_mode, prio_shift, wg_per_cu, wide_max,
+// fast_exact, fail_alloc_after). name == NULL restores every default. Used by
+// the tests and tools/ only; the product path never calls it.
+int rt_debug_tune(rt_ctx* ctx, const char* name, const char* value) {
+    if (!ctx) return RT_ERR_INVALID_ARG;
+    if (!name) {
+        ctx->tune = Tuning();
+        return RT_OK;
+    }
+    if (!value || !tune_set(ctx->tune, name, value))
+        return fail(ctx, RT_ERR_INVALID_ARG, "rt_debug_tune: bad knob %s=%s", name,
+                    value ? value : "(null)");
+    return RT_OK;
+}
+
+// Internal: device allocations the ctx has made so far (tests: a reserved
+// render allocates nothing).
+uint64_t rt_debug_alloc_count(const rt_ctx* ctx) { return ctx ? ctx->allocs : 0; }
 
 const char* rt_last_error(const rt_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
 

@@ -32,11 +32,6 @@ __device__ __forceinline__ v3 normalize(v3 a) {
 // a branch the wave skips when no lane needs it. The result is the IEEE one
 // in every case (GPU parity tests; rt_debug_math + tests/test_gpu_math.py on
 // zeros, denormals, huge, inf and NaN operands).
-#ifdef RT_FAST_NOGUARD  // measurement only (NOT exact): no IEEE fallback lanes
-#define RT_GUARD_ON 0
-#else
-#define RT_GUARD_ON 1
-#endif
 #if defined(RT_NO_FAST_MATH) || defined(RT_SHADE_IEEE)  // A/B: plain IEEE operations
 __device__ __forceinline__ float sqrt_x(float x) { return sqrtf(x); }
 __device__ __forceinline__ float length_x(v3 a) { return sqrtf(dot(a, a)); }
@@ -52,7 +47,7 @@ __device__ __forceinline__ float sqrt_x(float x) {
     float r = rt_sqrt_rn(x);
     // x outside [2^-100, 2^100] (0, NaN, inf, < 0: IEEE) as one unsigned compare
     const bool bad = __float_as_uint(x) - 0x0D800000u > 0x71800000u - 0x0D800000u;
-    if (RT_GUARD_ON && rt_ballot(bad) != 0) {
+    if (rt_ballot(bad) != 0) {
         if (bad) r = sqrtf(rt_cold(x));
     }
     return r;
@@ -64,7 +59,7 @@ __device__ __forceinline__ float length_x(v3 a) { return sqrt_x(dot(a, a)); }
 __device__ __forceinline__ float div_x(float n, float b, float yb) {
     float r = rt_div_rn(n, b, yb);
     const bool ok = yb == yb && rt_num_ok(n);
-    if (RT_GUARD_ON && rt_ballot(!ok) != 0) {
+    if (rt_ballot(!ok) != 0) {
         if (!ok) r = n / b;
     }
     return r;
@@ -85,7 +80,7 @@ __device__ __forceinline__ v3 div3_x(v3 v, float b) {
     const uint32_t az = __float_as_uint(v.z) & 0x7FFFFFFFu, ab = __float_as_uint(b) & 0x7FFFFFFFu;
     const uint32_t lo = min(min(min(ax, ay), az), ab), hi = max(max(max(ax, ay), az), ab);
     const bool small = lo < 0x2B800000u /* 2^-40 */, big = hi > 0x53800000u /* 2^40 */;
-    if (RT_GUARD_ON && (rt_ballot(small) | rt_ballot(big)) != 0) {
+    if ((rt_ballot(small) | rt_ballot(big)) != 0) {
         if (small || big) {
             const float bb = rt_cold(b);
             r = mk(v.x / bb, v.y / bb, v.z / bb);
@@ -106,7 +101,7 @@ __device__ __forceinline__ v3 normalize_x(v3 v) {
     const float y = rt_recip_rn(l);
     v3 r = mk(rt_div_rn(v.x, l, y), rt_div_rn(v.y, l, y), rt_div_rn(v.z, l, y));
     const bool small = !(fminf(fminf(px, py), pz) >= 0x1p-80f), big = !(d2 <= 0x1p80f);
-    if (RT_GUARD_ON && (rt_ballot(small) | rt_ballot(big)) != 0) {
+    if ((rt_ballot(small) | rt_ballot(big)) != 0) {
         if (small || big) r = normalize(mk(rt_cold(v.x), v.y, v.z));
     }
     return r;

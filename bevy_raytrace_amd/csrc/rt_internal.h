@@ -70,9 +70,9 @@ struct KParams {
     uint32_t tile_full_cols;  // width / 8
     uint32_t tile_wrem;       // width % 8
     FastDiv div_8w, div_wrem;
-    uint32_t prefetch;  // 1: waves prefetch their next work chunk (RT_PREFETCH=0 off)
-    uint32_t prio_mode;   // s_setprio rotation (RT_PRIO): 0 off, 1 by iteration, 3 by wall time
-    uint32_t prio_shift;  // mode 3: one step per 2^prio_shift ticks of 10 ns (RT_PRIO_SHIFT)
+    uint32_t prefetch;  // 1: waves prefetch their next work chunk (knob prefetch)
+    uint32_t prio_mode;   // s_setprio rotation (knob prio_mode): 0 off, 1 by iteration, 3 by wall time
+    uint32_t prio_shift;  // mode 3: one step per 2^prio_shift ticks of 10 ns (knob prio_shift)
     // culled list (RT_FLAG_CULL; rt_render_cull_kernel): grp / sph / sph_rm
     // are then the permuted arrays, nspheres / ngroups their padded sizes
     const float4* bnd;      // bound records, SoA like a group: per super its 8 cluster bounds,

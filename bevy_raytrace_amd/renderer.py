@@ -161,6 +161,23 @@ class Renderer:
         check(self.lib, self.ctx, rc)
         return idx, t
 
+    def tune(self, name=None, value=None, **knobs):
+        """Set A/B knobs of this context (internal rt_debug_tune; the product
+        defaults need none): tune("scratch_bytes", 4096), tune(wide_max=0),
+        tune(tail="0,0,6"). tune(None) restores every default."""
+        if name is None and not knobs:
+            check(self.lib, self.ctx, self.lib.rt_debug_tune(self.ctx, None, None))
+            return
+        if name is not None:
+            knobs[name] = value
+        for k, v in knobs.items():
+            check(self.lib, self.ctx, self.lib.rt_debug_tune(self.ctx, str(k).encode(),
+                                                            str(v).encode()))
+
+    def alloc_count(self):
+        """Device allocations this context has made (internal)."""
+        return int(self.lib.rt_debug_alloc_count(self.ctx))
+
     def debug_counters(self):
         """Diagnostic counters of the last call (non-zero only for -DRT_PROFILE builds)."""
         out = (ctypes.c_uint64 * 16)()

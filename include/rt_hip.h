@@ -192,7 +192,9 @@ void rt_destroy(rt_ctx* ctx);
 
 /* Upload the scene (replaces sphere.rs:180-197 and ray_trace_materials.rs:129-164).
  * Arrays are borrowed and copied during the call. Sphere order = list order =
- * tie-break order of intersect_world (intersect.wgsl:135-139). n may be 0. */
+ * tie-break order of intersect_world (intersect.wgsl:135-139). n may be 0.
+ * If it fails after validation (e.g. RT_ERR_OUT_OF_MEMORY), the context has
+ * no scene until the next successful call (renders return RT_ERR_NO_SCENE). */
 int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n,
                  const rt_material* materials, uint32_t m);
 
@@ -200,7 +202,9 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n,
  * the reference re-uploads the whole list every frame, sphere.rs:180-197, and
  * the materials when their count changes, ray_trace_materials.rs:129-164).
  * Replace records [first, first+count) of the current scene; counts N and M
- * are unchanged. Only the touched sphere groups are re-packed and uploaded. */
+ * are unchanged. Only the touched sphere records and 8-sphere groups are
+ * re-packed and uploaded; the culled list (RT_FLAG_CULL), which depends on
+ * every sphere, is rebuilt once, at the next culled call. */
 int rt_update_spheres(rt_ctx* ctx, uint32_t first, const rt_sphere* spheres, uint32_t count);
 int rt_update_materials(rt_ctx* ctx, uint32_t first, const rt_material* materials,
                         uint32_t count);
@@ -242,7 +246,8 @@ int rt_render_frames_device(rt_ctx* ctx, const rt_camera* camera, const rt_param
  * counters) that rt_render_frames_device(params, nframes) needs, in every
  * frames-in-flight slot, without rendering -- the analogue of the reference
  * sizing its ray / intersection buffers in its prepare systems
- * (src/ray_trace_rays.rs:50-66) rather than inside RayTraceNode::run. Renders
+ * (src/ray_trace_rays.rs:50-66) rather than inside RayTraceNode::run -- and
+ * the one-frame host-output staging of rt_render / rt_render_async. Renders
  * of that size or smaller then allocate nothing. No call may be pending. */
 int rt_reserve(rt_ctx* ctx, const rt_params* params, uint32_t nframes);
 

@@ -420,10 +420,17 @@ static void* worker(void* arg) {
     job_t* j = (job_t*)arg;
     uint64_t segs = 0;
     const uint32_t W = j->p->width;
-    /* interleave rows over threads for load balance */
-    for (uint32_t r = (uint32_t)j->tid; r < j->nrows; r += (uint32_t)j->nthreads) {
-        uint32_t y = j->rows[r];
-        for (uint32_t x = 0; x < W; ++x)
+    /* interleave 32-pixel row pieces over threads for load balance (a few
+     * rows of an 8K frame still keep every thread busy); pixels are
+     * independent, so the split does not change any result */
+    const uint32_t pieces = (W + 31u) / 32u;
+    const uint64_t units = (uint64_t)j->nrows * pieces;
+    for (uint64_t u = (uint64_t)j->tid; u < units; u += (uint64_t)j->nthreads) {
+        const uint32_t r = (uint32_t)(u / pieces);
+        const uint32_t x0 = (uint32_t)(u % pieces) * 32u;
+        const uint32_t x1 = x0 + 32u < W ? x0 + 32u : W;
+        const uint32_t y = j->rows[r];
+        for (uint32_t x = x0; x < x1; ++x)
             render_pixel(j, x, y, j->out + ((size_t)r * W + x) * 4, &segs);
     }
     j->segs = segs;

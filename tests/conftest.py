@@ -13,8 +13,17 @@ def pytest_configure(config):
 
 
 @pytest.fixture(scope="session")
-def renderer():
+def _session_renderer():
     from bevy_raytrace_amd.renderer import Renderer
     r = Renderer(0)
     yield r
     r.close()
+
+
+@pytest.fixture
+def renderer(_session_renderer):
+    """The session's context, with every A/B knob (rt_debug_tune) at its
+    product default on entry and on exit."""
+    _session_renderer.tune(None)
+    yield _session_renderer
+    _session_renderer.tune(None)

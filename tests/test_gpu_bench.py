@@ -32,3 +32,17 @@ def test_rccl_gather_path_matches_single_gpu():
     assert "RCCL gather" in b["config"]["parallelism"]
     assert a["check"] == b["check"] and len(a["check"]) == 2  # the last launch's frames
     assert a["segments_per_frame"] == b["segments_per_frame"]
+
+
+@pytest.mark.gpu
+def test_bench_launches_its_own_ranks():
+    """`python bench.py --gpus 2` with no launcher around it (the driver's
+    scaling command) starts the two ranks itself and relays rank 0's line;
+    the assembled frames equal the single-GPU run's (both ranks on the one
+    GPU of this box, host-staged gloo gather)."""
+    a = _bench()
+    b = _bench("--gpus", "2", "--same-device", "--dist-backend", "gloo")
+    assert b["n_gpus"] == 2 and len(b["ranks"]["segments"]) == 2
+    assert sum(b["ranks"]["segments"]) == 4 * a["segments_per_frame"]
+    assert a["check"] == b["check"]
+    assert a["segments_per_frame"] == b["segments_per_frame"]

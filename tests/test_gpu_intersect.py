@@ -53,11 +53,11 @@ SCENES = {  # name -> (spheres, translation applied to spheres and rays)
 @pytest.mark.parametrize("cull", [False, True], ids=["brute", "cull"])
 @pytest.mark.parametrize("fast", [True, False], ids=["short_math", "ieee"])
 @pytest.mark.parametrize("name", sorted(SCENES))
-def test_intersect_bit_exact(renderer, name, fast, cull, monkeypatch):
-    """fast=False forces the IEEE exact tests (RT_FAST_EXACT=0): both forms
+def test_intersect_bit_exact(renderer, name, fast, cull):
+    """fast=False forces the IEEE exact tests (knob fast_exact=0): both forms
     must give the oracle's bits."""
     if not fast:
-        monkeypatch.setenv("RT_FAST_EXACT", "0")
+        renderer.tune(fast_exact=0)
     sp, off = SCENES[name]()
     from bevy_raytrace_amd.abi import MATERIAL_DTYPE
     mt = np.zeros(int(sp["material"].max()) + 1, dtype=MATERIAL_DTYPE)

@@ -120,7 +120,7 @@ def test_other_camera(renderer):
     assert st["segments"] == segs
 
 
-def test_multi_pass_scratch_identical(renderer, monkeypatch):
+def test_multi_pass_scratch_identical(renderer):
     """Block sums folded over several passes == one pass (sequential fold)."""
     sp, mt = arrays(scene.config1_scene())
     cam = default_camera_block()
@@ -128,7 +128,7 @@ def test_multi_pass_scratch_identical(renderer, monkeypatch):
     one, st1 = renderer.render(cam, 80, 45, 40, 6)
     # 16 slots: a small image splits every block into single samples (8 slots
     # per block), so 2 blocks per pass
-    monkeypatch.setenv("RT_SCRATCH_BYTES", str(80 * 45 * 16 * 16))
+    renderer.tune(scratch_bytes=80 * 45 * 16 * 16)
     many, st2 = renderer.render(cam, 80, 45, 40, 6)
     assert st2["kernel_launches"] == 3 and st1["kernel_launches"] == 1
     check_exact(many, one)
@@ -139,14 +139,14 @@ def test_multi_pass_scratch_identical(renderer, monkeypatch):
 @pytest.mark.parametrize("wide", ["0", "64"], ids=["never_wide", "always_wide"])
 @pytest.mark.parametrize("name,mk", [("rtiow", scene.rtiow_final_scene), ("glass", glass_scene),
                                      ("empty", None)])
-def test_sphere_parallel_tail(renderer, monkeypatch, wide, name, mk):
+def test_sphere_parallel_tail(renderer, wide, name, mk):
     """intersect_wide (the nearly-empty-wave path) and the ray-parallel walk
     give the same image: forced on for every wave, and forced off."""
     from bevy_raytrace_amd.abi import MATERIAL_DTYPE, SPHERE_DTYPE
     sp, mt = arrays(mk()) if mk else (np.zeros(0, SPHERE_DTYPE), np.zeros(0, MATERIAL_DTYPE))
     cam = default_camera_block()
     renderer.set_scene(sp, mt)
-    monkeypatch.setenv("RT_WIDE_MAX", wide)
+    renderer.tune(wide_max=wide)
     img, st = renderer.render(cam, 80, 45, 9, 12, frame0=1, flags=NO_REUSE)
     ref, segs = O.render(cam, sp, mt, 80, 45, 9, 12, frame0=1)
     check_exact(img, ref)
@@ -154,19 +154,18 @@ def test_sphere_parallel_tail(renderer, monkeypatch, wide, name, mk):
 
 
 @pytest.mark.parametrize("S", [1, 6, 8, 21, 64])
-def test_tail_split_identical(renderer, monkeypatch, S):
+def test_tail_split_identical(renderer, S):
     """The single-sample tail items (last block of a pass, summed in sample
     order by the collect kernel) give the same image as whole-block items."""
     sp, mt = arrays(scene.rtiow_final_scene())
     cam = default_camera_block()
     renderer.set_scene(sp, mt)
     on, st_on = renderer.render(cam, 72, 40, S, 10, frame0=5, flags=NO_REUSE)
-    monkeypatch.setenv("RT_TAIL_SPLIT", "0")
+    renderer.tune(tail_split=0)
     off, st_off = renderer.render(cam, 72, 40, S, 10, frame0=5, flags=NO_REUSE)
     check_exact(on, off)
     assert st_on["segments"] == st_off["segments"]
-    monkeypatch.setenv("RT_SCRATCH_BYTES", str(72 * 40 * 16 * 8))  # 1 (split) block per pass
-    monkeypatch.delenv("RT_TAIL_SPLIT")
+    renderer.tune(scratch_bytes=72 * 40 * 16 * 8, tail_split=1)  # 1 (split) block per pass
     passes, _ = renderer.render(cam, 72, 40, S, 10, frame0=5)
     check_exact(passes, on)
     ref, segs = O.render(cam, sp, mt, 72, 40, S, 10, frame0=5)
@@ -428,7 +427,7 @@ def test_srgb8_encode(renderer):
 @pytest.mark.parametrize("K,k,scratch", [(1, 0, None), (3, 2, None), (1, 0, "frame"),
                                          (1, 0, "pass")], ids=["one_launch", "shard",
                                                                 "launch_per_frame", "multi_pass"])
-def test_frames_batch_identical(renderer, monkeypatch, flags, K, k, scratch):
+def test_frames_batch_identical(renderer, flags, K, k, scratch):
     """rt_render_frames_device: frame i of one launch == rt_render with
     frame0 + i*spp (bit-identical, same total segments), also when the scratch
     limit splits the frames over launches or a frame over passes."""
@@ -442,9 +441,9 @@ def test_frames_batch_identical(renderer, monkeypatch, flags, K, k, scratch):
     refs = [renderer.render(cam, W, H, S, D, frame0=f0 + i * S, row_block=B, shard_count=K,
                             shard_index=k, flags=flags) for i in range(F)]
     if scratch == "frame":   # room for one frame's slots per launch
-        monkeypatch.setenv("RT_SCRATCH_BYTES", str(rows * W * 16 * 3 * 8))
+        renderer.tune(scratch_bytes=rows * W * 16 * 3 * 8)
     elif scratch == "pass":  # less than one frame: several passes per frame
-        monkeypatch.setenv("RT_SCRATCH_BYTES", str(rows * W * 16 * 9))
+        renderer.tune(scratch_bytes=rows * W * 16 * 9)
     out = torch.full((F, rows, W, 4), -1.0, dtype=torch.float32, device="cuda")
     renderer.render_frames_device(cam, F, out.data_ptr(), W, H, S, D, frame0=f0, row_block=B,
                                   shard_count=K, shard_index=k, flags=flags)
@@ -543,9 +542,9 @@ def test_camera_sampling_frames_and_shards(renderer):
 
 
 @pytest.mark.parametrize("name,mk", [("rtiow", scene.rtiow_final_scene), ("glass", glass_scene)])
-def test_short_math_and_ieee_identical(renderer, monkeypatch, name, mk):
+def test_short_math_and_ieee_identical(renderer, name, mk):
     """The exact sphere test's short correctly-rounded sqrt/divide (in-domain
-    scenes) and the IEEE forms (RT_FAST_EXACT=0) render the oracle's bits; a
+    scenes) and the IEEE forms (knob fast_exact=0) render the oracle's bits; a
     zero-radius sphere takes the scene out of the short domain."""
     sp, mt = arrays(mk())
     cam = default_camera_block()
@@ -554,11 +553,11 @@ def test_short_math_and_ieee_identical(renderer, monkeypatch, name, mk):
     img, st = renderer.render(cam, 128, 72, 6, 10)
     check_exact(img, ref)
     assert st["segments"] == segs and st["short_math"] == 1
-    monkeypatch.setenv("RT_FAST_EXACT", "0")
+    renderer.tune(fast_exact=0)
     img, st = renderer.render(cam, 128, 72, 6, 10)
     check_exact(img, ref)
     assert st["short_math"] == 0
-    monkeypatch.delenv("RT_FAST_EXACT")
+    renderer.tune(fast_exact=1)
     sp0 = np.concatenate([sp, sp[:1]])
     sp0["radius"][-1] = 0.0
     sp0["center"][-1] = (0.0, 30.0, 0.0)  # out of view; only the domain check changes
@@ -597,7 +596,8 @@ def test_coincident_spheres_queue_flushes(renderer, flags):
 
 def test_cull_full_1080p64_identical(renderer):
     """RT_FLAG_CULL at the headline size: the culled walk's frame and segment
-    counts equal the brute-force walk's, bit for bit, and it is faster."""
+    counts equal the brute-force walk's, bit for bit (its speed is bench.py's
+    `culled` line, not a test: a shared or throttled box says nothing there)."""
     sp, mt = arrays(scene.rtiow_final_scene())
     cam = default_camera_block()
     renderer.set_scene(sp, mt)
@@ -605,7 +605,6 @@ def test_cull_full_1080p64_identical(renderer):
     c, sc = renderer.render(cam, 1920, 1080, 64, 16, flags=NO_REUSE | CULL)
     check_exact(c, b)
     assert sc["segments"] == sb["segments"] == sc["traced_segments"]
-    assert sc["kernel_ms"] < sb["kernel_ms"]
 
 
 @pytest.mark.parametrize("K,k", [(3, 1), (8, 7)])
@@ -630,3 +629,56 @@ def test_cull_shards_and_updates(renderer, K, k):
     ref, segs = O.render(cam, sp2, mt, 64, 36, 4, 8)
     check_exact(img, ref)
     assert st["segments"] == segs
+
+
+def test_reserved_renders_allocate_nothing(renderer):
+    """After rt_reserve, rt_render (host output, both in-flight slots) and
+    rt_render_frames_device of the reserved size make no device allocation."""
+    import torch
+    sp, mt = arrays(scene.rtiow_final_scene())
+    renderer.set_scene(sp, mt)
+    cam = default_camera_block()
+    W, H, S, D = 64, 40, 9, 6
+    renderer.reserve(2, W, H, S, D)
+    before = renderer.alloc_count()
+    for f0 in (0, 9, 18):  # rt_render alternates the two slots
+        img, _ = renderer.render(cam, W, H, S, D, frame0=f0)
+    buf = torch.empty((2, H, W, 4), dtype=torch.float32, device="cuda")
+    renderer.render_frames_device(cam, 2, buf.data_ptr(), W, H, S, D)
+    renderer.wait()
+    assert renderer.alloc_count() == before
+    check_exact(img, O.render(cam, sp, mt, W, H, S, D, frame0=18)[0])
+
+
+def test_failed_scene_upload_leaves_no_scene():
+    """A device allocation failing inside rt_set_scene (injected) returns
+    RT_ERR_OUT_OF_MEMORY and leaves NO scene -- the next render is refused
+    with RT_ERR_NO_SCENE instead of reading freed or half-written buffers; a
+    later rt_set_scene recovers. A culled-list build failure is retried."""
+    from bevy_raytrace_amd.renderer import Renderer
+    small, smt = arrays(scene.config1_scene())
+    big, bmt = arrays(scene.rtiow_final_scene())
+    cam = default_camera_block()
+    with Renderer(0) as r:
+        r.set_scene(small, smt)
+        r.render(cam, 16, 9, 1, 2)
+        r.tune(fail_alloc_after=1)  # the list grows: the 2nd reallocation fails
+        with pytest.raises(abi.RayTraceError) as e:
+            r.set_scene(big, bmt)
+        assert e.value.status == abi.RT_ERR_OUT_OF_MEMORY
+        with pytest.raises(abi.RayTraceError) as e:
+            r.render(cam, 16, 9, 1, 2)
+        assert e.value.status == abi.RT_ERR_NO_SCENE
+        r.tune(None)
+        r.set_scene(big, bmt)
+        for _ in range(2):  # both in-flight slots get their work buffers
+            plain, _ = r.render(cam, 32, 18, 2, 4)
+        r.tune(fail_alloc_after=0)  # the culled list is built at the first culled call
+        with pytest.raises(abi.RayTraceError) as e:
+            r.render(cam, 32, 18, 2, 4, flags=CULL)
+        assert e.value.status == abi.RT_ERR_OUT_OF_MEMORY
+        again, _ = r.render(cam, 32, 18, 2, 4)  # the brute-force list is untouched
+        check_exact(again, plain)
+        r.tune(None)
+        img, _ = r.render(cam, 32, 18, 2, 4, flags=CULL)
+        check_exact(img, O.render(cam, big, bmt, 32, 18, 2, 4)[0])

@@ -2,6 +2,7 @@
 library (loads, exports every symbol of include/rt_hip.h, host-only entry
 points and error paths without a GPU)."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -148,3 +149,32 @@ def test_create_without_gpu_reports_device_error():
     assert rc == abi.RT_ERR_DEVICE
     assert not ctx.value
     assert b"no HIP device" in lib.rt_last_error(None)
+
+
+def test_bench_spawn_relays_rank0_line(monkeypatch, capsys):
+    """bench.py --gpus N without WORLD_SIZE: a child torch.distributed.run on
+    127.0.0.1 with N ranks and the same arguments; only rank 0's JSON line
+    reaches stdout, and the launcher's exit status is returned."""
+    import subprocess
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    seen = {}
+
+    def fake_run(cmd, stdout=None, env=None):
+        seen["cmd"], seen["env"] = cmd, env
+        out = b'RCCL banner\n{"metric": "m", "value": 1.0}\n'
+        return subprocess.CompletedProcess(cmd, 0, stdout=out)
+
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "3"])
+    rc = bench.spawn_ranks(bench.parse())
+    assert rc == 0
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "3"]
+    assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    out = capsys.readouterr()
+    assert out.out.strip() == '{"metric": "m", "value": 1.0}'
+    assert "RCCL banner" in out.err

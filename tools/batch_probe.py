@@ -30,11 +30,11 @@ def per_frame(F, n=1, k=0, reps=2):
 
 per_frame(2, reps=1)
 for tail in (sys.argv[3].split(";") if len(sys.argv) > 3 else ("2,1,1",)):
-    os.environ["RT_TAIL"] = tail
+    r.tune(tail=tail)
     for F in (1, 2, 4, 8):
         full = per_frame(F)
         sh = [per_frame(F, 8, k) for k in (0, 3, 7)]
         print(f"tail={tail} F={F}: full {full:.3f} ms/frame | N=8 shards {' '.join('%.3f' % t for t in sh)}"
               f" -> pred {full / max(sh):.2f}x", flush=True)
-os.environ["RT_SPLIT_ALL"] = "1"
+r.tune(split_all=1)
 print(f"split-all F=1: full {per_frame(1):.3f} | N=8 k=7 {per_frame(1, 8, 7):.3f}", flush=True)

@@ -24,7 +24,7 @@ N = 1 << 22
 
 def trace(F, n=1, k=0, tail=None):
     if tail:
-        os.environ["RT_TAIL"] = tail
+        r.tune(tail=tail)
     rb = configs.pick_row_block(H, n)
     for _ in range(2):
         out = np.zeros(N, dtype=np.uint64)

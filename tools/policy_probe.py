@@ -6,6 +6,7 @@ import torch
 from bevy_raytrace_amd import abi, configs
 from bevy_raytrace_amd.camera import default_camera_block
 from bevy_raytrace_amd.renderer import Renderer
+import _knobs
 
 wl = configs.WORKLOADS["rtiow1080"]
 sc = wl.make_scene()
@@ -33,16 +34,11 @@ settings = sys.argv[1:] or ["", "RT_SPLIT_ALL=1"]
 for rep in range(2):
     for setting in settings:
         env = dict(p.split("=") for p in setting.split(";") if p)
-        saved = {e: os.environ.get(e) for e in env}
-        os.environ.update(env)
+        _knobs.apply(r, env)
         for F in FS:
             full = per_frame(F)
             sh = [per_frame(F, 8, k) for k in range(8)]
             print(f"[{setting or 'default'}] F={F}: full {full:.3f} ms/frame | N=8 shards "
                   f"{' '.join('%.3f' % t for t in sh)} -> pred {full / max(sh):.2f}x, "
                   f"vs full@default-ish {23.5 / max(sh):.2f}x", flush=True)
-        for e, v in saved.items():
-            if v is None:
-                os.environ.pop(e)
-            else:
-                os.environ[e] = v
+        r.tune(None)

@@ -8,6 +8,7 @@ import torch
 from bevy_raytrace_amd import abi, configs
 from bevy_raytrace_amd.camera import default_camera_block
 from bevy_raytrace_amd.renderer import Renderer
+import _knobs
 
 LIB = os.environ.get("RT_PROF_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "librt_hip_prof.so")
 NAMES = {0: "refill", 1: "filter", 2: "drain", 12: "bookkeep", 3: "shade", 7: "tail"}
@@ -28,19 +29,14 @@ for case in cases:
     F, n, k = int(parts[0]), int(parts[1]), int(parts[2])
     env = dict(p.split("=", 1) for p in parts[3].split(";")) if len(parts) > 3 else {}
     flags = abi.RT_FLAG_NO_PRIMARY_CACHE | (abi.RT_FLAG_CULL if env.pop("CULL", "0") == "1" else 0)
-    old = {e: os.environ.get(e) for e in env}
-    os.environ.update(env)
+    _knobs.apply(r, env)
     rb = configs.pick_row_block(H, n)
     for _ in range(2):
         r.render_frames_device(cam, F, buf.data_ptr(), W, H, S, D, row_block=rb, shard_count=n,
                                shard_index=k, flags=flags)
         st = r.wait()
     c = r.debug_counters()
-    for e, v in old.items():
-        if v is None:
-            os.environ.pop(e)
-        else:
-            os.environ[e] = v
+    r.tune(None)
     tot = sum(c[i] for i in NAMES)
     it = max(c[4], 1)
     print(f"{case}: kernel {st['kernel_ms']:.2f} ms ({st['kernel_ms'] / F:.2f}/frame), "

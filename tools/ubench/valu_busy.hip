@@ -1,0 +1,110 @@
+// Calibration of the VALU counters on gfx950: kernels whose VALU stream is
+// known instruction by instruction (inline asm, independent operands, 6
+// waves per SIMD like rt_render_kernel), timed with HIP events. Run under
+//   rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES
+//             SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -- ./valu_busy
+// to relate SQ_ACTIVE_INST_VALU (quad-cycles per the counter description) and
+// GRBM_GUI_ACTIVE (summed over the 8 XCDs) to the issue cycles each class
+// of instruction really takes (tools/valu_calib.py reads the output).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+#define ITERS 8192
+
+// 8 independent v_pk_fma_f32 per iteration (vector operands only)
+__global__ __launch_bounds__(256) void k_pk8(float* out, float a) {
+    f2 x0 = {(float)threadIdx.x, 1.f}, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3;
+    f2 x4 = x0 + 4, x5 = x0 + 5, x6 = x0 + 6, x7 = x0 + 7;
+    f2 va = {a, a};
+    for (int i = 0; i < ITERS; ++i) {
+        asm volatile(
+            "v_pk_fma_f32 %0, %0, %8, %8\n\tv_pk_fma_f32 %1, %1, %8, %8\n\t"
+            "v_pk_fma_f32 %2, %2, %8, %8\n\tv_pk_fma_f32 %3, %3, %8, %8\n\t"
+            "v_pk_fma_f32 %4, %4, %8, %8\n\tv_pk_fma_f32 %5, %5, %8, %8\n\t"
+            "v_pk_fma_f32 %6, %6, %8, %8\n\tv_pk_fma_f32 %7, %7, %8, %8"
+            : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(x4), "+v"(x5), "+v"(x6), "+v"(x7)
+            : "v"(va));
+    }
+    f2 s = ((x0 + x1) + (x2 + x3)) + ((x4 + x5) + (x6 + x7));
+    out[blockIdx.x * 256 + threadIdx.x] = s.x + s.y;
+}
+
+// 8 independent v_fma_f32 per iteration
+__global__ __launch_bounds__(256) void k_fma8(float* out, float a) {
+    float x0 = threadIdx.x, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3, x4 = x0 + 4, x5 = x0 + 5,
+          x6 = x0 + 6, x7 = x0 + 7;
+    for (int i = 0; i < ITERS; ++i) {
+        asm volatile(
+            "v_fma_f32 %0, %0, %8, %8\n\tv_fma_f32 %1, %1, %8, %8\n\t"
+            "v_fma_f32 %2, %2, %8, %8\n\tv_fma_f32 %3, %3, %8, %8\n\t"
+            "v_fma_f32 %4, %4, %8, %8\n\tv_fma_f32 %5, %5, %8, %8\n\t"
+            "v_fma_f32 %6, %6, %8, %8\n\tv_fma_f32 %7, %7, %8, %8"
+            : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(x4), "+v"(x5), "+v"(x6), "+v"(x7)
+            : "v"(a));
+    }
+    out[blockIdx.x * 256 + threadIdx.x] = ((x0 + x1) + (x2 + x3)) + ((x4 + x5) + (x6 + x7));
+}
+
+// 8 independent v_add_u32 per iteration (integer ops of the bookkeeping)
+__global__ __launch_bounds__(256) void k_add8(float* out, float a) {
+    unsigned x0 = threadIdx.x, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3, x4 = x0 + 4, x5 = x0 + 5,
+             x6 = x0 + 6, x7 = x0 + 7, k = __float_as_uint(a);
+    for (int i = 0; i < ITERS; ++i) {
+        asm volatile(
+            "v_add_u32 %0, %0, %8\n\tv_add_u32 %1, %1, %8\n\t"
+            "v_add_u32 %2, %2, %8\n\tv_add_u32 %3, %3, %8\n\t"
+            "v_add_u32 %4, %4, %8\n\tv_add_u32 %5, %5, %8\n\t"
+            "v_add_u32 %6, %6, %8\n\tv_add_u32 %7, %7, %8"
+            : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(x4), "+v"(x5), "+v"(x6), "+v"(x7)
+            : "v"(k));
+    }
+    out[blockIdx.x * 256 + threadIdx.x] = (float)(x0 ^ x1 ^ x2 ^ x3 ^ x4 ^ x5 ^ x6 ^ x7);
+}
+
+// the filter group's shape: 4 v_pk_fma_f32 + 4 v_max3_f32-like scalar ops
+__global__ __launch_bounds__(256) void k_mix(float* out, float a) {
+    f2 x0 = {(float)threadIdx.x, 1.f}, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3;
+    float y0 = threadIdx.x, y1 = y0 + 1, y2 = y0 + 2, y3 = y0 + 3;
+    f2 va = {a, a};
+    for (int i = 0; i < ITERS; ++i) {
+        asm volatile(
+            "v_pk_fma_f32 %0, %0, %8, %8\n\tv_max3_f32 %4, %4, %9, %9\n\t"
+            "v_pk_fma_f32 %1, %1, %8, %8\n\tv_max3_f32 %5, %5, %9, %9\n\t"
+            "v_pk_fma_f32 %2, %2, %8, %8\n\tv_max3_f32 %6, %6, %9, %9\n\t"
+            "v_pk_fma_f32 %3, %3, %8, %8\n\tv_max3_f32 %7, %7, %9, %9"
+            : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(y0), "+v"(y1), "+v"(y2), "+v"(y3)
+            : "v"(va), "v"(a));
+    }
+    f2 s = (x0 + x1) + (x2 + x3);
+    out[blockIdx.x * 256 + threadIdx.x] = s.x + s.y + y0 + y1 + y2 + y3;
+}
+
+int main() {
+    int cus = 0;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    const int grid = cus * 6;  // 6 workgroups of 4 waves per CU = 6 waves per SIMD
+    float* d;
+    hipMalloc(&d, (size_t)grid * 256 * sizeof(float));
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    struct K { const char* name; void (*fn)(float*, float); } ks[] = {
+        {"pk_fma x8", k_pk8}, {"fma x8", k_fma8}, {"add_u32 x8", k_add8},
+        {"pk_fma x4 + max3 x4", k_mix}};
+    for (int rep = 0; rep < 2; ++rep)
+        for (const K& k : ks) {
+            float ms = 0.0f;
+            hipEventRecord(e0);
+            hipLaunchKernelGGL(k.fn, dim3(grid), dim3(256), 0, 0, d, 0.999f);
+            hipEventRecord(e1);
+            hipEventSynchronize(e1);
+            hipEventElapsedTime(&ms, e0, e1);
+            const double inst_per_simd = 8.0 * ITERS * 6;  // 6 waves, 8 VALU per iteration
+            // cycles per VALU instruction per SIMD at the nominal 2.4 GHz
+            printf("%-22s %8.3f ms  %.3f cyc/inst/SIMD @2.4GHz\n", k.name, ms,
+                   ms * 1e-3 * 2.4e9 / inst_per_simd);
+        }
+    hipFree(d);
+    return 0;
+}
