@@ -75,6 +75,9 @@ def parse():
     ap.add_argument("--cull-steps", type=int, default=-1,
                     help="extra frames timed with the culled list, RT_FLAG_CULL (0 = skip; "
                          "default 12 at N=1, skipped at N>1)")
+    ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE",
+                    help="A/B only: set a library knob (rt_debug_tune; the defaults are the "
+                         "product), e.g. --tune wg_per_cu=6")
     return ap.parse_args()
 
 
@@ -174,6 +177,8 @@ def main():
     max_rows = max(len(abi.shard_rows(H, B, world, k)) for k in range(world))
 
     r = Renderer(local)
+    for kv in args.tune:
+        r.tune(*kv.split("=", 1))
     r.set_scene(spheres, mats)
     # work buffers of the largest launch this run makes, allocated before any
     # step (rt_reserve) so no allocation lands inside a timed region
@@ -195,12 +200,21 @@ def main():
                                                   device="cuda")
     gathered = (torch.empty((world, FPL, max_rows, W, 4), dtype=torch.float32, device="cuda")
                 if (rank == 0 and dist_on) else None)
+    # The library writes frame i of a launch at i * rows * W (this rank's own
+    # row count); the gather needs equal slabs of max_rows. With uneven shards
+    # (H not a multiple of B*world) a shorter rank renders into its own buffer
+    # and copies each frame into the padded slab.
+    packed = (torch.empty((FPL, len(rows), W, 4), dtype=torch.float32, device="cuda")
+              if dist_on and len(rows) != max_rows else None)
 
     def launch(first, nf, flags):
         """Enqueue frames [first, first + nf): render, then (N > 1) one RCCL
         gather of the nf shard slabs to rank 0 and the device re-assembly."""
-        r.render_frames_device(cam, nf, shard.data_ptr(), W, H, S, D, first * S, B, world, rank,
+        dst = shard if packed is None else packed
+        r.render_frames_device(cam, nf, dst.data_ptr(), W, H, S, D, first * S, B, world, rank,
                                flags, stream=stream.cuda_stream)
+        if packed is not None:
+            shard[:nf, :len(rows)].copy_(packed[:nf])
         if dist_on:
             if args.dist_backend == "nccl":
                 dist.gather(shard[:nf], [gathered[k, :nf] for k in range(world)] if rank == 0
@@ -366,6 +380,8 @@ def main():
         out["check"] = {f"frame{args.steps - last + i}":
                         hashlib.sha1(image[i].cpu().numpy().tobytes()).hexdigest()[:16]
                         for i in range(last)}
+    if args.tune:
+        out["tune"] = args.tune
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cam, spheres, mats, W, H, S, D, args.cpu_rows,
                                            image[0].cpu().numpy())

@@ -795,13 +795,14 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         const uint64_t fr = q / nb;
         return fr * p.spp + (bb + (q - fr * nb)) * RT_SAMPLE_BLOCK;
     };
-    // slots (= work items per pixel) of a launch of F frames x blocks [bb, bb + nb)
+    // slots per pixel of a launch of F frames x blocks [bb, bb + nb): one per
+    // frame with main blocks (its lane-folded sum) + one per tail sample
     auto launch_slots = [&](uint64_t F, uint64_t nb, uint64_t bb) -> uint64_t {
         const uint64_t pairs = F * nb, L = tail_pairs(pairs);
         const uint64_t g_end = (F - 1) * p.spp +
                                std::min<uint64_t>(p.spp, (bb + nb) * RT_SAMPLE_BLOCK);
         const uint64_t g0 = L ? pair_g(pairs - L, nb, bb) : g_end;
-        return pairs - L + (g_end - g0);
+        return (pairs - L + nb - 1) / nb + (g_end - g0);
     };
     if (npix) {
         uint64_t slots_cap = tn.scratch_bytes / per_block;
@@ -833,7 +834,7 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         }
         int rc = ensure(ctx, &f.d_block_sums, &f.bs_cap, per_block * (size_t)bs_slots);
         if (rc) return rc;
-        rc = ensure(ctx, &f.d_pd, &f.pd_cap, 2 * per_block);  // 32-B pixel table entries
+        rc = ensure(ctx, &f.d_pd, &f.pd_cap, per_block);  // 16-B pixel table entries
         if (rc) return rc;
     }
     const size_t words = RT_CNT_WORK_OFFSET + passes.size();
@@ -864,6 +865,7 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     K_.shard_count = K;
     K_.shard_index = p.shard_index;
     K_.npix = npix;
+    K_.acc_in = f.d_acc;
     K_.nspheres = cull ? ctx->n_c : ctx->n;
     K_.ngroups = cull ? ctx->ngroups_c : ctx->ngroups;
     if (cull) {
@@ -944,7 +946,7 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
                                                              RT_SAMPLE_BLOCK);
         const uint64_t g0 = L ? pair_g(pairs - L, ps.nblocks, ps.block_begin) : g_end;
         K_.qmain = (uint32_t)(pairs - L);
-        K_.main_all = K_.qmain * npix;
+        K_.main_all = (K_.qmain + ps.nblocks - 1) / ps.nblocks * npix;  // (frame, pixel) items
         // tail regions from the end: single samples, 2-sample, 4-sample items
         const uint64_t g2 = g_end - std::min<uint64_t>(A1, g_end - g0);
         const uint64_t g1 = g2 - std::min<uint64_t>(A2, g2 - g0);
@@ -1095,6 +1097,7 @@ int rt_render_async(rt_ctx* ctx, const rt_camera* camera, const rt_params* param
     if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_render_async: ctx is NULL");
     if (!out_rgba) return fail(ctx, RT_ERR_INVALID_ARG, "rt_render_async: out_rgba is NULL");
     if (!params) return fail(ctx, RT_ERR_INVALID_ARG, "rt_render_async: params is NULL");
+    if (!ctx->has_scene) return fail(ctx, RT_ERR_NO_SCENE, "rt_render before rt_set_scene");
     Frame* f = next_slot(ctx, "rt_render_async");
     if (!f) return RT_ERR_INVALID_ARG;
     const size_t bytes = out_bytes(params);

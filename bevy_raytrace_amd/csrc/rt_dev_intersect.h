@@ -526,6 +526,20 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
 // takes the smallest t, ties to the smallest index -- exactly the answer of
 // the sequential strict-`<` scan (intersect.wgsl:133-143).
 // CULL: the permuted list; ties go to the smaller original index perm[i].
+// x from lane (lane ^ off) -- ds_bpermute with the address computed here from
+// a fresh lane id: HIP's __shfl_xor lets the compiler hoist every (lane ^ off)
+// address of a loop into its own VGPR for the whole kernel (5 VGPRs for the
+// reduction below, at the 80-register occupancy limit).
+__device__ __forceinline__ uint32_t xor_shuffle(uint32_t x, uint32_t off) {
+    uint32_t l = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    asm volatile("" : "+v"(l));
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)((l ^ off) << 2), (int)x);
+}
+
+__device__ __forceinline__ float lane_value(float x, int src) {  // src wave-uniform
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), src));
+}
+
 template <bool CULL>
 __device__ __forceinline__ void intersect_wide(const float4* __restrict__ sph, uint32_t n,
                                                uint32_t scene_fast, uint64_t active, v3 o, v3 d,
@@ -534,8 +548,8 @@ __device__ __forceinline__ void intersect_wide(const float4* __restrict__ sph, u
     while (active) {
         const int src = (int)__builtin_ctzll(active);
         active &= active - 1;
-        const v3 ro = mk(__shfl(o.x, src), __shfl(o.y, src), __shfl(o.z, src));
-        const v3 rd = mk(__shfl(d.x, src), __shfl(d.y, src), __shfl(d.z, src));
+        const v3 ro = mk(lane_value(o.x, src), lane_value(o.y, src), lane_value(o.z, src));
+        const v3 rd = mk(lane_value(d.x, src), lane_value(d.y, src), lane_value(d.z, src));
         const float l = sqrt_x(dot(rd, rd));
         const float a = l * l;  // sqr(length(r.dir)), intersect.wgsl:98
         const bool fast = ray_fast(scene_fast, ro, a);
@@ -551,8 +565,8 @@ __device__ __forceinline__ void intersect_wide(const float4* __restrict__ sph, u
 #endif
         }
         for (int off = 32; off > 0; off >>= 1) {
-            const float ot = __shfl_xor(bt, off);
-            const int oi = __shfl_xor(bi, off);
+            const float ot = __uint_as_float(xor_shuffle(__float_as_uint(bt), (uint32_t)off));
+            const int oi = (int)xor_shuffle((uint32_t)bi, (uint32_t)off);
             bool take;
             if (CULL)  // key: original index, a miss (-1) last
                 take = ot < bt || (ot == bt && (oi < 0 ? 0xFFFFFFFFu : perm[oi]) <

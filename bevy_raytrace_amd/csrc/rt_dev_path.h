@@ -5,30 +5,45 @@
 // Lane state of one in-flight path.
 struct PathState {
     v3 o, d;            // current ray
-    v3 pd;              // primary direction of this pixel (generate.wgsl: pixel-only)
     v3 color;           // throughput (intersection.color, clear.wgsl:86)
     v3 bsum;            // sum of finished samples of the current block
     v3 nseed;           // normalize(seed)
     float seedx;        // seed.x (dielectric Schlick test)
-    uint32_t x, y;      // global pixel
-    uint32_t item;      // work item = (block - block_begin) * npix + pixel
-    uint32_t s, s_end;  // current sample, end of the block
+    uint32_t pix;       // global pixel x + W*y (the seed's pixel term, shade.wgsl:216-218)
+    uint32_t item;      // main item: its queue index (= output slot); tail: RT_TAIL_ITEM | pixel
+    uint32_t s, s_end;  // current sample, end of the current sample block
     uint32_t bounce;
 };
 
-// New sample s of the lane's pixel: seed (shade.wgsl:216-218), primary ray
-// (generate.wgsl:109-129; origin = camera translation, direction cached per
-// item since it depends on the pixel only), throughput 1 (clear.wgsl:86).
-__device__ __forceinline__ void start_sample(const KParams& P, PathState& st) {
+// Per-lane item state that changes at most once per sample, kept in LDS (no
+// VGPRs at the 80-register occupancy limit), one record per lane so a single
+// VGPR address (+ immediate offsets) reaches every field: the pixel's primary
+// direction, the item's running fold of its block sums (xyz; w != 0 once a
+// block was folded), the primary hit (reuse mode) and the end of its samples.
+struct LaneLds {
+    float4 pd;        // primary direction of the lane's pixel (xyz)
+    float4 acc;       // fold of the item's block sums so far
+    float2 cache;     // primary hit (index bits, t) -- primary-hit reuse only
+    uint32_t iend;    // end of the item's samples
+    uint32_t pad;
+};
+typedef LaneLds* ItemLds;  // the lane's own record
+
+// New sample s of the lane's pixel: seed (shade.wgsl:216-218; u32 wrap, so
+// (x + W*y) + W*H*frame is the reference's index), primary ray
+// (generate.wgsl:109-129; origin = camera translation, direction from the
+// pixel table since it depends on the pixel only), throughput 1 (clear.wgsl:86).
+__device__ __forceinline__ void start_sample(const KParams& P, PathState& st, ItemLds L) {
     const uint32_t frame = P.frame0 + st.s;
-    const uint32_t idx = st.x + P.width * st.y + (P.width * P.height) * frame;
+    const uint32_t idx = st.pix + (P.width * P.height) * frame;
     const v3 seed = hash3(idx);
     st.seedx = seed.x;
     st.nseed = normalize_seed(seed);
     // (with the opt-in camera sampling the main loop replaces this primary
     // ray before tracing it: one call site for sampled_primary_ray)
     st.o = mk(0.0f + P.T[12], 0.0f + P.T[13], 0.0f + P.T[14]);
-    st.d = st.pd;
+    const float4 pd = L->pd;
+    st.d = mk(pd.x, pd.y, pd.z);
     st.color = mk(1.0f, 1.0f, 1.0f);
     st.bounce = 0;
 }
@@ -78,26 +93,40 @@ __device__ __forceinline__ uint32_t order_to_pixel(const KParams& P, uint32_t k)
     return r * W + x;
 }
 
-// Work item -> (sample block, pixel). block_sums is indexed by (block, pixel)
-// for the collect pass.
-// pixel table entry (rt_primary_kernel): k-th pixel of the processing order
-// -> its primary direction and (shard pixel index, x | y << 16).
+// Pixel table entry (rt_primary_kernel), 16 B: the k-th pixel of the
+// processing order -> its primary direction (xyz) and x + W*y (w, as bits).
 struct PixelEntry {
-    float4 d;       // xyz: primary direction, w: unused
-    uint32_t p, xy;
-    uint32_t pad0, pad1;
+    float4 d;
 };
 
+// Work item -> samples, pixel. A main item (item < main_all) is (frame f,
+// pixel k) with all of f's main blocks (pairs q = f*nblocks + b < qmain) in
+// block order: the lane sums each block of RT_SAMPLE_BLOCK samples in
+// registers (st.s_end = the block's end), folds the block sums in block order
+// (acc = bsum_0; acc = acc + bsum_b -- rt_collect_kernel's fold), and stores the
+// fold once, at slot = its queue index. A tail item is z = 4, 2 or 1
+// consecutive samples of one pixel, each sample's colour stored on its own.
 __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint32_t item,
-                                           const PixelEntry* __restrict__ tab) {
-    uint32_t k, s0, s1;  // pixel in processing order; the item's samples [s0, s1)
-    if (item < P.main_all) {  // block item of pair q = (frame f, block b)
-        const uint32_t q = fdiv(item, P.div_npix);
-        k = item - q * P.npix;
-        const uint32_t f = fdiv(q, P.div_nblocks);
-        const uint32_t sl = (P.block_begin + (q - f * P.nblocks)) * RT_SAMPLE_BLOCK;
-        s0 = P.sample_base + f * P.spp + sl;
-        s1 = P.sample_base + f * P.spp + min(P.spp, sl + RT_SAMPLE_BLOCK);
+                                           const PixelEntry* __restrict__ tab, ItemLds L) {
+    uint32_t k, s0, s1;  // pixel in processing order; the (first block's) samples [s0, s1)
+    if (item < P.main_all) {
+        const uint32_t f = fdiv(item, P.div_npix);
+        k = item - f * P.npix;
+        const uint32_t mb = min(P.nblocks, P.qmain - f * P.nblocks);  // main blocks of f
+        const uint32_t base = P.sample_base + f * P.spp;
+        s0 = base + P.block_begin * RT_SAMPLE_BLOCK;
+        const uint32_t iend = base + min(P.spp, (P.block_begin + mb) * RT_SAMPLE_BLOCK);
+        s1 = min(s0 + RT_SAMPLE_BLOCK, iend);
+        L->iend = iend;
+        // a later pass over the frame's blocks (frames above the scratch
+        // budget) continues the fold of the earlier passes (rt_collect_kernel
+        // left it in acc_in): ((acc + b0) + b1) ..., the single-pass order
+        float4 a0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (P.block_begin) {
+            a0 = P.acc_in[order_to_pixel(P, k)];
+            a0.w = 1.0f;
+        }
+        L->acc = a0;
     } else {  // tail item: z = 4, 2 or 1 consecutive samples, each stored on its own
         uint32_t j = item - P.main_all, z, gb, ge;
         if (j < P.ti1) {
@@ -112,18 +141,15 @@ __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint
         s0 = P.sample_base + gb + g * z;
         s1 = P.sample_base + min(gb + g * z + z, ge);
     }
-    const PixelEntry& e = tab[k];
-    const uint4 pxy = *reinterpret_cast<const uint4*>(&e.p);
-    const float4 q4 = e.d;
-    // block item: its output slot (= queue index); tail item: RT_TAIL_ITEM | k
+    const float4 q4 = tab[k].d;
+    // main item: its output slot (= queue index); tail item: RT_TAIL_ITEM | k
     st.item = item < P.main_all ? item : (RT_TAIL_ITEM | k);
-    st.x = pxy.y & 0xFFFFu;
-    st.y = pxy.y >> 16;
+    st.pix = __float_as_uint(q4.w);
     st.s = s0;
     st.s_end = s1;
     st.bsum = mk(0.0f, 0.0f, 0.0f);
-    st.pd = mk(q4.x, q4.y, q4.z);
-    start_sample(P, st);
+    L->pd = q4;
+    start_sample(P, st, L);
 }
 
 // One path step after an intersection: shade.wgsl:199-258 for hit `hi` at t.

@@ -39,15 +39,17 @@ struct KParams {
     // Work queue of one launch. The launch covers nframes frames (samples
     // sample_base + f*spp + [0, spp) of launch frame f; the seed frame is
     // frame0 + that) x blocks [block_begin, block_begin + nblocks) of each.
-    // Its (frame, block) pairs q = f*nblocks + b are dealt in order: pairs
-    // q < qmain as block items (pixel, 8 samples), items [0, main_all =
-    // qmain*npix), each storing its block sum at slot = its queue index. The
-    // rest -- the launch's tail, launch samples g = f*spp + s in [g0, g_end)
-    // -- is dealt as shrinking items so no wave holds a long item when the
-    // queue runs dry: 4-sample items over [g0, g1), 2-sample over [g1, g2),
-    // single samples over [g2, g_end), each region sample-major; a tail item
-    // stores every sample's colour at slot main_all + (g - g0)*npix + k.
-    // rt_collect_kernel folds the slots per pixel in sample order.
+    // Its (frame, block) pairs q = f*nblocks + b: pairs q < qmain are the main
+    // part, dealt as one item per (frame, pixel) -- items [0, main_all =
+    // ceil(qmain / nblocks) * npix), frame-major -- covering that frame's main
+    // blocks; the lane folds their block sums and stores the fold at slot =
+    // its queue index. The rest -- the launch's tail, launch samples
+    // g = f*spp + s in [g0, g_end) -- is dealt as shrinking items so no wave
+    // holds a long item when the queue runs dry: 4-sample items over [g0, g1),
+    // 2-sample over [g1, g2), single samples over [g2, g_end), each region
+    // sample-major; a tail item stores every sample's colour at slot
+    // main_all + (g - g0)*npix + k. rt_collect_kernel folds them per pixel in
+    // block / sample order.
     uint32_t nframes, sample_base, qmain, main_all;
     uint32_t g0, g1, g2, g_end;
     uint32_t ti1, ti2, tail_items;  // tail item offsets of the 2- and 1-sample regions, count
@@ -80,6 +82,7 @@ struct KParams {
     const uint32_t* perm;   // permuted position -> original sphere index (ties)
     uint32_t nclusters;
     uint32_t cull_supers;   // 1: test the cluster bounds (many clusters); 0: walk every cluster
+    const float4* acc_in;   // passes after the first (block_begin > 0): the fold so far, per pixel
 };
 
 // Row block b of the image -> owning shard (rt_params: serpentine deal).

@@ -106,14 +106,19 @@ __device__ __forceinline__ void render_body(
     const PixelEntry* __restrict__ tab, float4* __restrict__ block_sums,
     uint32_t* __restrict__ work_counter,
     unsigned long long* __restrict__ seg_counter, unsigned long long* __restrict__ dbg) {
-    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t lane = __lane_id();
     PROF_DECL
     PROF_START();
 #ifdef RT_PROFILE
     const unsigned long long t_begin = prof_.last;
 #endif
+    // the wave's slices of the workgroup's LDS arrays: wave-uniform bases
+    // (SGPRs) indexed by the lane id, so no VGPR holds an LDS address
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
     __shared__ uint32_t s_cq[RT_BLOCK_THREADS * RT_CQ_CAP];  // per-lane candidate queues
-    uint32_t* cq = s_cq + (threadIdx.x / 64u) * (64u * RT_CQ_CAP);
+    uint32_t* cq = s_cq + wave * (64u * RT_CQ_CAP);
+    __shared__ LaneLds s_lane[RT_BLOCK_THREADS];  // per-lane item state (rt_dev_path.h)
+    const ItemLds lds = s_lane + wave * 64u + lane;
 #ifdef RT_SPHERES_LDS
     // Experiment variant: the filter reads the sphere groups from LDS (staged
     // once per workgroup) instead of the scalar cache.
@@ -151,8 +156,6 @@ __device__ __forceinline__ void render_body(
     uint32_t q_next = 0, q_end = 0;  // wave-uniform chunk of work items
     bool exhausted = false;
     uint32_t traced = 0, segs = 0;  // wave totals (wave-uniform: SGPRs, not a VGPR per lane)
-    int cache_hi = -1;      // primary hit of this item's pixel (generate.wgsl: pixel-only ray)
-    float cache_t = 0.0f;
     // Chunk prefetch: the atomic for the wave's NEXT chunk is issued as soon as
     // the current one is taken, so its round trip to the device-scope counter
     // (one address shared by every wave of the chip) overlaps a whole filter
@@ -183,7 +186,7 @@ __device__ __forceinline__ void render_body(
                     chunk = q_end >= P.tail_start ? RT_WAVE_CHUNK_TAIL : RT_WAVE_CHUNK;
                     if (lane == 0) base = atomicAdd(work_counter, chunk);
                 }
-                base = __shfl(base, 0);
+                base = __builtin_amdgcn_readlane(base, 0);
                 pref_chunk = 0;
                 if (base >= total) {
 #ifdef RT_WAVE_TRACE
@@ -210,7 +213,7 @@ __device__ __forceinline__ void render_body(
             const uint32_t rank = lanemask_lt_count(need);
             const uint32_t cnt = (uint32_t)__popcll(need);
             if (!has_item && rank < avail) {
-                start_item(P, st, q_next + rank, tab);
+                start_item(P, st, q_next + rank, tab, lds);
                 has_item = true;
             }
 #ifdef RT_WAVE_TRACE
@@ -253,8 +256,9 @@ __device__ __forceinline__ void render_body(
         // ---- opt-in camera sampling: a lane at bounce 0 holds a fresh sample
         // whose primary ray varies per sample (no primary-hit reuse then)
         if ((P.flags & (RT_FLAG_JITTER | RT_FLAG_THIN_LENS)) && has_item && st.bounce == 0) {
-            const uint32_t idx = st.x + P.width * st.y + (P.width * P.height) * (P.frame0 + st.s);
-            sampled_primary_ray(P, st.x, st.y, idx, st.o, st.d);
+            const uint32_t idx = st.pix + (P.width * P.height) * (P.frame0 + st.s);
+            const uint32_t y = fdiv(st.pix, P.div_width);
+            sampled_primary_ray(P, st.pix - y * P.width, y, idx, st.o, st.d);
         }
 
         // ---- intersect (intersect.wgsl:145-163): every lane with an item holds
@@ -271,13 +275,9 @@ __device__ __forceinline__ void render_body(
 #endif
                                        P.bnd, P.perm, P.nclusters, P.cull_supers != 0);
         }
-        traced += (uint32_t)__popcll(live);
-        if (has_item) {
-            if (st.bounce == 0) {  // first sample of the block: remember the primary hit
-                cache_hi = hi;
-                cache_t = t;
-            }
-        }
+        traced = __builtin_amdgcn_readfirstlane(traced + (uint32_t)__popcll(live));
+        if (use_cache && has_item && st.bounce == 0)  // the item's first sample: its primary hit
+            lds->cache = make_float2(__int_as_float(hi), t);
         // ---- shade; a finished path starts the next sample, whose primary hit
         // is reused (result-identical) so the lane goes on to its bounce-1 ray.
         bool shading = has_item;
@@ -287,7 +287,7 @@ __device__ __forceinline__ void render_body(
         for (;;) {
             const uint64_t sh = rt_ballot(shading);
             if (sh == 0) break;
-            segs += (uint32_t)__popcll(sh);
+            segs = __builtin_amdgcn_readfirstlane(segs + (uint32_t)__popcll(sh));
             if (shading) {
                 const bool done = shade(P, st, hi, t, sph, sph_rm, mats);
                 shading = false;
@@ -303,16 +303,33 @@ __device__ __forceinline__ void render_body(
                         st.bsum = add(st.bsum, st.color);
                     }
                     ++st.s;
-                    if (st.s < st.s_end) {
-                        start_sample(P, st);
+                    bool next = st.s < st.s_end;
+                    if (!next && !(st.item & RT_TAIL_ITEM)) {
+                        // a sample block of a main item ends: fold its sum into
+                        // the item's running sum in block order (as
+                        // rt_collect_kernel folds: first block as is, then
+                        // acc + bsum); the item's last block stores the fold
+                        const float4 a = lds->acc;
+                        const v3 acc = a.w != 0.0f ? add(mk(a.x, a.y, a.z), st.bsum) : st.bsum;
+                        const uint32_t iend = lds->iend;
+                        if (st.s < iend) {
+                            lds->acc = make_float4(acc.x, acc.y, acc.z, 1.0f);
+                            st.bsum = mk(0.0f, 0.0f, 0.0f);
+                            st.s_end = min(st.s + RT_SAMPLE_BLOCK, iend);
+                            next = true;
+                        } else {
+                            block_sums[st.item] = make_float4(acc.x, acc.y, acc.z, 0.0f);
+                        }
+                    }
+                    if (next) {
+                        start_sample(P, st, lds);
                         if (use_cache) {
-                            hi = cache_hi;
-                            t = cache_t;
+                            const float2 c = lds->cache;
+                            hi = __float_as_int(c.x);
+                            t = c.y;
                             shading = true;
                         }
                     } else {
-                        if (!(st.item & RT_TAIL_ITEM))
-                            block_sums[st.item] = make_float4(st.bsum.x, st.bsum.y, st.bsum.z, 0.0f);
                         has_item = false;
                     }
                 }
@@ -392,12 +409,7 @@ __global__ void rt_primary_kernel(KParams P, PixelEntry* __restrict__ tab) {
     pixel_xy(P, p, x, y);
     v3 o, d;
     primary_ray(P, x, y, o, d);
-    PixelEntry e;
-    e.d = make_float4(d.x, d.y, d.z, 0.0f);
-    e.p = p;
-    e.xy = x | (y << 16);
-    e.pad0 = e.pad1 = 0;
-    tab[k] = e;
+    tab[k].d = make_float4(d.x, d.y, d.z, __uint_as_float(x + P.width * y));
 }
 
 // Batch closest-hit query (rt_intersect): one ray per lane, same intersect_world.
@@ -441,19 +453,20 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_cull_kernel(
     intersect_body<true>(grp, sph, ngroups, scene_fast, rays, n, out_i, out_t, bnd, perm, nclusters);
 }
 
-// Fold one frame's block sums (launch frame f = blockIdx.y) into acc (block
-// order) and, on the frame's last pass, write out = acc / spp with alpha 1
-// (collect.wgsl:115-125). One thread per pixel of the processing order k
-// (pixel table -> image pixel p). Block b of frame f is pair q = f*nblocks +
-// b: a block item's sum at slot q*npix + k if q < qmain, else a tail block
-// whose samples' colours sit at main_all + (g - g0)*npix + k (g = f*spp + s)
-// and are summed here exactly as a lane sums a block, ((0 + c0) + c1) + ...,
-// in sample order, then folded like any other block.
+// Fold one frame's results into acc (block order) and, on the frame's last
+// pass, write out = acc / spp with alpha 1 (collect.wgsl:115-125). One thread
+// per pixel of the processing order k (-> image pixel p = order_to_pixel).
+// Launch frame f = blockIdx.y. Its main blocks (pairs q = f*nblocks + b <
+// qmain) were folded by the lane that traced them (render loop: first block
+// as is -- or acc + it on a later pass -- then acc + block sum) and stored at
+// slot f*npix + k; each remaining
+// block is a tail block whose samples' colours sit at main_all + (g - g0)*npix
+// + k (g = f*spp + s), summed here exactly as a lane sums a block, ((0 + c0) +
+// c1) + ..., in sample order, then folded the same way.
 // Progressive mode (rt_render_progressive): on the last pass the frame's sum
 // is folded into the running sum, prog = prog + sum (prog_mode 2) or
 // prog = sum (1, reset), and out = prog / total_spp.
-__global__ void rt_collect_kernel(KParams P, const PixelEntry* __restrict__ tab,
-                                  const float4* __restrict__ block_sums,
+__global__ void rt_collect_kernel(KParams P, const float4* __restrict__ block_sums,
                                   float4* __restrict__ acc, int first_pass,
                                   int last_pass, float spp, float4* __restrict__ out,
                                   float4* __restrict__ prog, int prog_mode, float prog_total) {
@@ -461,31 +474,32 @@ __global__ void rt_collect_kernel(KParams P, const PixelEntry* __restrict__ tab,
     if (k >= P.npix) return;
     const uint32_t f = blockIdx.y;
     out += (size_t)f * P.npix;
-    const uint32_t p = tab[k].p;
+    const uint32_t p = order_to_pixel(P, k);
     float ax = 0.0f, ay = 0.0f, az = 0.0f;
     bool have = !first_pass;
     if (have) {
         const float4 v = acc[p];
         ax = v.x; ay = v.y; az = v.z;
     }
-    for (uint32_t b = 0; b < P.nblocks; ++b) {
-        const uint32_t q = f * P.nblocks + b;
-        float4 v;
-        if (q < P.qmain) {
-            v = block_sums[(size_t)q * P.npix + k];
-        } else {  // a tail block: its samples' colours, summed in sample order
-            const uint32_t sl = (P.block_begin + b) * RT_SAMPLE_BLOCK;
-            const uint32_t g_end = f * P.spp + min(P.spp, sl + RT_SAMPLE_BLOCK);
-            v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            for (uint32_t g = f * P.spp + sl; g < g_end; ++g) {
-                const float4 c = block_sums[(size_t)P.main_all + (size_t)(g - P.g0) * P.npix + k];
-                v.x = v.x + c.x; v.y = v.y + c.y; v.z = v.z + c.z;
-            }
+    const uint32_t q0 = f * P.nblocks;
+    const uint32_t mb = P.qmain > q0 ? min(P.nblocks, P.qmain - q0) : 0u;  // main blocks of f
+    if (mb) {  // the lane's fold already continued acc (start_item, later passes)
+        const float4 v = block_sums[(size_t)f * P.npix + k];
+        ax = v.x; ay = v.y; az = v.z;
+        have = true;
+    }
+    for (uint32_t b = mb; b < P.nblocks; ++b) {  // tail blocks: their samples' colours
+        const uint32_t sl = (P.block_begin + b) * RT_SAMPLE_BLOCK;
+        const uint32_t g_end = f * P.spp + min(P.spp, sl + RT_SAMPLE_BLOCK);
+        float vx = 0.0f, vy = 0.0f, vz = 0.0f;
+        for (uint32_t g = f * P.spp + sl; g < g_end; ++g) {
+            const float4 c = block_sums[(size_t)P.main_all + (size_t)(g - P.g0) * P.npix + k];
+            vx = vx + c.x; vy = vy + c.y; vz = vz + c.z;
         }
         if (have) {
-            ax = ax + v.x; ay = ay + v.y; az = az + v.z;
+            ax = ax + vx; ay = ay + vy; az = az + vz;
         } else {
-            ax = v.x; ay = v.y; az = v.z;
+            ax = vx; ay = vy; az = vz;
             have = true;
         }
     }
@@ -568,9 +582,10 @@ hipError_t rt_launch_collect(const KParams* P, const float4* pd, const float4* b
                              float4* acc, int first_pass, int last_pass, float spp, float4* out,
                              float4* prog, int prog_mode, float prog_total, hipStream_t stream) {
     const uint32_t T = 256;
+    (void)pd;
     hipLaunchKernelGGL(rt_collect_kernel, dim3((P->npix + T - 1) / T, P->nframes), dim3(T), 0, stream, *P,
-                       reinterpret_cast<const PixelEntry*>(pd), block_sums, acc, first_pass,
-                       last_pass, spp, out, prog, prog_mode, prog_total);
+                       block_sums, acc, first_pass, last_pass, spp, out, prog, prog_mode,
+                       prog_total);
     return hipGetLastError();
 }
 

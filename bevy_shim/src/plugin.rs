@@ -1,16 +1,16 @@
 //! RayTracePlugin (replaces the reference's src/plugin.rs:19-122): same name,
 //! same sub-plugins for the camera / globals / materials / output resources,
 //! but no wgpu pipelines or bind groups -- the render-graph node calls the
-//! MI355X path tracer through the C-ABI.
+//! MI355X path tracer through the C-ABI (include/rt_hip.h).
 use bevy::{
     prelude::*,
-    render::{render_graph::RenderGraph, RenderApp, RenderStage},
+    render::{render_graph::RenderGraph, RenderApp},
 };
 
 use crate::ray_trace_camera::RayTraceCameraPlugin;
 use crate::ray_trace_globals::RayTraceGlobalsPlugin;
 use crate::ray_trace_materials::RayTraceMaterialsPlugin;
-use crate::ray_trace_node::{prepare_scene, RayTraceNode, SceneUploadState};
+use crate::ray_trace_node::RayTraceNode;
 use crate::ray_trace_output::RayTraceOutputPlugin;
 use crate::rt_hip::RtContext;
 
@@ -23,18 +23,25 @@ impl Plugin for RayTracePlugin {
             .add_plugin(RayTraceMaterialsPlugin)
             .add_plugin(RayTraceOutputPlugin);
 
+        // One context on HIP device 0. Without a device (or librt_hip.so's
+        // kernels) the app keeps running with the cleared output image, like
+        // the reference while its pipelines are still loading
+        // (ray_trace_node.rs:201-202): the error is logged, nothing panics.
+        let ctx = match RtContext::new(0) {
+            Ok(ctx) => ctx,
+            Err(e) => {
+                error!("RayTracePlugin: rt_create failed, ray tracing disabled: {e}");
+                return;
+            }
+        };
         let render_app = app.sub_app_mut(RenderApp);
-        let ctx = RtContext::new(0).expect("rt_create failed (no MI355X / librt_hip.so?)");
-        render_app
-            .insert_resource(ctx)
-            .init_resource::<SceneUploadState>()
-            // after sphere.rs / ray_trace_materials.rs `prepare` have packed the bytes
-            .add_system_to_stage(RenderStage::Prepare, prepare_scene.at_end());
-
         let mut render_graph = render_app.world.resource_mut::<RenderGraph>();
-        render_graph.add_node("raytrace", RayTraceNode::default());
-        render_graph
-            .add_node_edge("raytrace", bevy::render::main_graph::node::CAMERA_DRIVER)
-            .unwrap();
+        // the node owns the context: rt_destroy runs when the render graph drops it
+        render_graph.add_node("raytrace", RayTraceNode::new(ctx));
+        if let Err(e) =
+            render_graph.add_node_edge("raytrace", bevy::render::main_graph::node::CAMERA_DRIVER)
+        {
+            error!("RayTracePlugin: render graph edge: {e:?}");
+        }
     }
 }

@@ -1,6 +1,23 @@
 //! RayTraceNode (replaces the reference's src/ray_trace_node.rs:16-225).
-//! The six compute dispatches become one rt_render call; the result is written
-//! into the Rgba32Float texture behind RayTraceOutputImage.
+//! The reference's six compute dispatches become one rt_render_async call on
+//! the MI355X; the finished Rgba32Float frame is written into the texture
+//! behind RayTraceOutputImage.
+//!
+//! Per frame, in `update` (it has `&mut World`, runs after every RenderStage
+//! ::Prepare system, so sphere.rs / ray_trace_materials.rs / ray_trace_globals.rs
+//! have packed this frame's bytes):
+//!   1. rt_wait for the frame enqueued one frame ago (it had a whole frame of
+//!      wall time to finish) -- its texels become the frame `run` shows;
+//!   2. dirty-tracked scene upload: rt_update_* for a same-size edit,
+//!      rt_set_scene when the counts change, nothing when the bytes are equal
+//!      (the reference re-uploads everything every frame, sphere.rs:180-197);
+//!   3. rt_reserve when the output size changes (the reference sizes its
+//!      buffers in prepare, ray_trace_rays.rs:50-66, not in run);
+//!   4. rt_render_async of this frame into the other host buffer.
+//! `run` only copies the finished frame into the texture. The displayed frame
+//! is one frame behind the camera, and the CPU never blocks on a render it
+//! just enqueued. A failing call is logged and skipped (the previous image
+//! stays); nothing panics across the render thread.
 use std::num::NonZeroU32;
 
 use bevy::{
@@ -20,101 +37,150 @@ use crate::ray_trace_materials::MaterialGPUStorage;
 use crate::ray_trace_output::RayTraceOutputImage;
 use crate::rt_hip::*;
 use crate::sphere::ObjectListStorage;
-use crate::SAMPLES_PER_RAY;
+use crate::{RENDER_TARGET_SIZE, SAMPLES_PER_RAY};
 
-/// Bytes last handed to the tracer (dirty tracking) and the
-/// camera block for this frame.
+/// The reference's loop count of (prepass, intersect, shade), ray_trace_node.rs:213.
+const MAX_DEPTH: u32 = 3;
+
+/// Bytes last handed to the tracer (dirty tracking).
 #[derive(Default)]
-pub struct SceneUploadState {
+struct Uploaded {
     spheres: Vec<u8>,
     materials: Vec<u8>,
-    camera: Vec<u8>,
-    /// (width, height) the tracer's work buffers were last sized for
+    /// the tracer holds exactly these bytes (false: upload in full)
+    scene_ok: bool,
+    /// (width, height) the work buffers were last reserved for
     reserved: (u32, u32),
 }
 
-/// RenderStage::Prepare, after the reference's own prepare systems have filled
-/// ObjectListStorage / MaterialGPUStorage (sphere.rs:180-197,
-/// ray_trace_materials.rs:129-164). Uploads the scene only when its packed bytes
-/// changed: rt_update_* for a same-size edit, rt_set_scene otherwise.
-pub fn prepare_scene(
-    ctx: Res<RtContext>,
-    camera: Res<RayTraceCamera>,
-    objects: Res<ObjectListStorage>,
-    materials: Res<MaterialGPUStorage>,
-    mut state: ResMut<SceneUploadState>,
-) {
-    // ObjectListGPU = {u32 sphere_count; pad to 16; N x 32-B SphereGPU} (sphere.rs:19-24)
-    let mut sb = encase::StorageBuffer::new(Vec::<u8>::new());
-    sb.write(objects.buffer.get()).unwrap();
-    let sb = sb.into_inner();
-    let n = u32::from_le_bytes([sb[0], sb[1], sb[2], sb[3]]);
-    let sph = sb[16..16 + 32 * n as usize].to_vec();
-    // Vec<MaterialGPU>: M x 32 B (ray_trace_materials.rs:33-43)
-    let mut mb = encase::StorageBuffer::new(Vec::<u8>::new());
-    mb.write(materials.buffer.get()).unwrap();
-    let mat = mb.into_inner();
-    let m = (mat.len() / 32) as u32;
+/// One host frame buffer and the geometry it holds.
+#[derive(Default)]
+struct HostFrame {
+    texels: Vec<f32>,
+    size: (u32, u32),
+}
 
-    // CameraGPU exactly as ray_trace_camera.rs:50-63 builds it.
-    let t = camera.transform;
-    let mut cb = encase::UniformBuffer::new(Vec::<u8>::new());
-    cb.write(&CameraGPU {
-        transform: t.compute_matrix(),
-        forward: t.forward(),
-        up: t.up(),
-        right: t.right(),
-        position: t.translation,
-        fov: 1.5708,
-        image_plane_distance: 10.0,
-        lens_focal_length: 0.1,
-        fstop: 1.0 / 32.0,
-    })
-    .unwrap();
-    state.camera = cb.into_inner();
+pub struct RayTraceNode {
+    ctx: RtContext,
+    uploaded: Uploaded,
+    camera: Vec<u8>,
+    frames: [HostFrame; 2],
+    /// index of the frame an rt_render_async is pending into
+    pending: Option<usize>,
+    /// index of the last finished frame (what `run` shows)
+    ready: Option<usize>,
+}
 
-    let rc = if state.spheres.len() == sph.len() && state.materials.len() == mat.len()
-        && !state.spheres.is_empty()
-    {
-        let mut rc = 0;
-        if let Some((i0, i1)) = dirty_range(&state.materials, &mat, 32) {
-            rc = unsafe { rt_update_materials(ctx.0, i0, mat[32 * i0 as usize..].as_ptr() as _, i1 - i0) };
+impl RayTraceNode {
+    pub fn new(ctx: RtContext) -> Self {
+        RayTraceNode {
+            ctx,
+            uploaded: Uploaded::default(),
+            camera: Vec::new(),
+            frames: [HostFrame::default(), HostFrame::default()],
+            pending: None,
+            ready: None,
         }
-        if rc == 0 {
-            if let Some((i0, i1)) = dirty_range(&state.spheres, &sph, 32) {
-                rc = unsafe { rt_update_spheres(ctx.0, i0, sph[32 * i0 as usize..].as_ptr() as _, i1 - i0) };
-            }
-        }
-        rc
-    } else if sph == state.spheres && mat == state.materials {
-        0
-    } else {
-        unsafe { rt_set_scene(ctx.0, sph.as_ptr() as _, n, mat.as_ptr() as _, m) }
-    };
-    match ctx.check(rc) {
-        Ok(()) => {
-            state.spheres = sph;
-            state.materials = mat;
-        }
-        Err(e) => error!("scene upload: {e}"),
     }
 
-    // Size the frame's work buffers here, not inside RayTraceNode::run, as the
-    // reference re-sizes its ray buffers in prepare (ray_trace_rays.rs:50-66).
-    let size = (camera.render_width, camera.render_height);
-    if size != state.reserved {
-        let params = rt_params {
+    fn params(&self, size: (u32, u32), frame: u32) -> rt_params {
+        rt_params {
             width: size.0,
             height: size.1,
             spp: SAMPLES_PER_RAY as u32,
-            max_depth: 3, // ray_trace_node.rs:213
+            max_depth: MAX_DEPTH,
+            frame0: frame,
             row_block: 8,
             shard_count: 1,
             ..Default::default()
+        }
+    }
+
+    /// Step 1: complete the render enqueued last frame.
+    fn finish_pending(&mut self) {
+        if let Some(i) = self.pending.take() {
+            let mut st = rt_stats::default();
+            match self.ctx.check(unsafe { rt_wait(self.ctx.0, &mut st) }) {
+                Ok(()) => self.ready = Some(i),
+                Err(e) => error!("rt_wait: {e}"),
+            }
+        }
+    }
+
+    /// Step 2: the scene, only when its packed bytes changed.
+    fn upload_scene(&mut self, world: &World) {
+        // ObjectListGPU = {u32 sphere_count; pad to 16; N x 32-B SphereGPU} (sphere.rs:19-24)
+        let mut sb = encase::StorageBuffer::new(Vec::<u8>::new());
+        if sb.write(world.resource::<ObjectListStorage>().buffer.get()).is_err() {
+            error!("scene upload: cannot pack the sphere list");
+            return;
+        }
+        let sb = sb.into_inner();
+        let n = u32::from_le_bytes([sb[0], sb[1], sb[2], sb[3]]);
+        let sph = sb[16..16 + 32 * n as usize].to_vec();
+        // Vec<MaterialGPU>: M x 32 B (ray_trace_materials.rs:33-43)
+        let mut mb = encase::StorageBuffer::new(Vec::<u8>::new());
+        if mb.write(world.resource::<MaterialGPUStorage>().buffer.get()).is_err() {
+            error!("scene upload: cannot pack the materials");
+            return;
+        }
+        let mat = mb.into_inner();
+        let m = (mat.len() / 32) as u32;
+        let (old_s, old_m) = (&self.uploaded.spheres, &self.uploaded.materials);
+        let ok = self.uploaded.scene_ok;
+        if ok && sph == *old_s && mat == *old_m {
+            return;
+        }
+        let ctx = self.ctx.0;
+        let rc = if ok && old_s.len() == sph.len() && old_m.len() == mat.len() {
+            let mut rc = 0;
+            if let Some((i0, i1)) = dirty_range(old_m, &mat, 32) {
+                let p = mat[32 * i0 as usize..].as_ptr() as *const _;
+                rc = unsafe { rt_update_materials(ctx, i0, p, i1 - i0) };
+            }
+            if rc == 0 {
+                if let Some((i0, i1)) = dirty_range(old_s, &sph, 32) {
+                    let p = sph[32 * i0 as usize..].as_ptr() as *const _;
+                    rc = unsafe { rt_update_spheres(ctx, i0, p, i1 - i0) };
+                }
+            }
+            rc
+        } else {
+            unsafe { rt_set_scene(ctx, sph.as_ptr() as *const _, n, mat.as_ptr() as *const _, m) }
         };
-        match ctx.check(unsafe { rt_reserve(ctx.0, &params, 1) }) {
-            Ok(()) => state.reserved = size,
-            Err(e) => error!("rt_reserve: {e}"),
+        match self.ctx.check(rc) {
+            Ok(()) => {
+                self.uploaded.spheres = sph;
+                self.uploaded.materials = mat;
+                self.uploaded.scene_ok = true;
+            }
+            Err(e) => {
+                // a failed rt_set_scene leaves no scene: upload in full next frame
+                self.uploaded = Uploaded::default();
+                error!("scene upload: {e}");
+            }
+        }
+    }
+
+    /// CameraGPU exactly as ray_trace_camera.rs:50-63 packs it (std140, 128 B).
+    fn pack_camera(&mut self, camera: &RayTraceCamera) {
+        let t = camera.transform;
+        let mut cb = encase::UniformBuffer::new(Vec::<u8>::new());
+        let ok = cb
+            .write(&CameraGPU {
+                transform: t.compute_matrix(),
+                forward: t.forward(),
+                up: t.up(),
+                right: t.right(),
+                position: t.translation,
+                fov: 1.5708,
+                image_plane_distance: 10.0,
+                lens_focal_length: 0.1,
+                fstop: 1.0 / 32.0,
+            })
+            .is_ok();
+        if ok {
+            self.camera = cb.into_inner();
         }
     }
 }
@@ -132,13 +198,45 @@ fn dirty_range(old: &[u8], new: &[u8], rec: usize) -> Option<(u32, u32)> {
     lo.map(|l| (l as u32, hi as u32))
 }
 
-#[derive(Default)]
-pub struct RayTraceNode {
-    texels: std::sync::Mutex<Vec<f32>>,
-}
-
 impl render_graph::Node for RayTraceNode {
-    fn update(&mut self, _world: &mut World) {}
+    fn update(&mut self, world: &mut World) {
+        self.finish_pending();
+        self.upload_scene(world);
+        if !self.uploaded.scene_ok {
+            return; // no scene on the device: nothing to render
+        }
+        let camera = world.resource::<RayTraceCamera>().clone();
+        self.pack_camera(&camera);
+        if self.camera.len() != 128 {
+            return;
+        }
+        let size = (camera.render_width, camera.render_height);
+        // seed frame (ray_trace_globals.rs:56-68)
+        let frame = world.resource::<GlobalsGPUStorage>().buffer.get().frame;
+        let params = self.params(size, frame);
+        if size != self.uploaded.reserved {
+            match self.ctx.check(unsafe { rt_reserve(self.ctx.0, &params, 1) }) {
+                Ok(()) => self.uploaded.reserved = size,
+                Err(e) => error!("rt_reserve: {e}"),
+            }
+        }
+        // the buffer `run` does not show
+        let i = match self.ready {
+            Some(r) => 1 - r,
+            None => 0,
+        };
+        let buf = &mut self.frames[i];
+        buf.texels.resize((size.0 * size.1 * 4) as usize, 0.0);
+        buf.size = size;
+        let rc = unsafe {
+            rt_render_async(self.ctx.0, self.camera.as_ptr() as *const _, &params,
+                            buf.texels.as_mut_ptr())
+        };
+        match self.ctx.check(rc) {
+            Ok(()) => self.pending = Some(i),
+            Err(e) => error!("rt_render_async: {e}"),
+        }
+    }
 
     fn run(
         &self,
@@ -146,45 +244,37 @@ impl render_graph::Node for RayTraceNode {
         _render_context: &mut RenderContext,
         world: &World,
     ) -> Result<(), NodeRunError> {
-        let ctx = world.resource::<RtContext>();
-        let state = world.resource::<SceneUploadState>();
-        let camera = world.resource::<RayTraceCamera>();
-        // frame = RNG seed input (ray_trace_globals.rs:56-68)
-        let frame = world.resource::<GlobalsGPUStorage>().buffer.get().frame;
-
-        let (w, h) = (camera.render_width, camera.render_height);
-        let params = rt_params {
-            width: w,
-            height: h,
-            spp: SAMPLES_PER_RAY as u32,
-            max_depth: 3, // ray_trace_node.rs:213
-            frame0: frame,
-            row_block: 8,
-            shard_count: 1,
-            ..Default::default()
+        let f = match self.ready {
+            Some(i) => &self.frames[i],
+            None => return Ok(()),
         };
-        let mut texels = self.texels.lock().unwrap();
-        texels.resize((w * h * 4) as usize, 0.0);
-        let rc = unsafe {
-            rt_render(ctx.0, state.camera.as_ptr() as _, &params, texels.as_mut_ptr(),
-                      std::ptr::null_mut())
-        };
-        if let Err(e) = ctx.check(rc) {
-            error!("rt_render: {e}"); // keep showing the previous frame
+        // the target is created at RENDER_TARGET_SIZE (ray_trace_output.rs init_output)
+        if f.size != RENDER_TARGET_SIZE {
             return Ok(());
         }
         let images = world.resource::<RenderAssets<Image>>();
-        let output = &images[&world.resource::<RayTraceOutputImage>().0];
+        let output = match images.get(&world.resource::<RayTraceOutputImage>().0) {
+            Some(o) => o,
+            None => return Ok(()), // not prepared yet
+        };
         world.resource::<RenderQueue>().write_texture(
             output.texture.as_image_copy(),
-            bytemuck::cast_slice(&texels[..]),
+            bytemuck::cast_slice(&f.texels[..]),
             ImageDataLayout {
                 offset: 0,
-                bytes_per_row: NonZeroU32::new(w * 16),
+                bytes_per_row: NonZeroU32::new(f.size.0 * 16),
                 rows_per_image: None,
             },
-            Extent3d { width: w, height: h, depth_or_array_layers: 1 },
+            Extent3d { width: f.size.0, height: f.size.1, depth_or_array_layers: 1 },
         );
         Ok(())
+    }
+}
+
+impl Drop for RayTraceNode {
+    fn drop(&mut self) {
+        // the host buffer of a pending render must outlive it
+        self.finish_pending();
+        // self.ctx drops next: rt_destroy
     }
 }

@@ -41,6 +41,8 @@ pub const RT_FLAG_NO_PRIMARY_CACHE: u32 = 0x1;
 /// through the reference's thin_lens_ray (generate.wgsl:85-107).
 pub const RT_FLAG_JITTER: u32 = 0x2;
 pub const RT_FLAG_THIN_LENS: u32 = 0x4;
+/// Culled sphere list: identical hits, less filter work (rt_hip.h).
+pub const RT_FLAG_CULL: u32 = 0x8;
 
 extern "C" {
     pub fn rt_version() -> c_int;
@@ -61,6 +63,9 @@ extern "C" {
                                    stream: *mut c_void) -> c_int;
     // allocate a launch's work buffers up front (RayTraceNode setup, not run)
     pub fn rt_reserve(ctx: *mut rt_ctx, params: *const rt_params, nframes: u32) -> c_int;
+    // enqueue a frame into a HOST buffer; rt_wait completes it (copy + stats)
+    pub fn rt_render_async(ctx: *mut rt_ctx, camera: *const c_void, params: *const rt_params,
+                           out_rgba: *mut f32) -> c_int;
     pub fn rt_wait(ctx: *mut rt_ctx, stats: *mut rt_stats) -> c_int;
     pub fn rt_intersect(ctx: *mut rt_ctx, rays: *const f32, n: u32, hit_index: *mut i32,
                         hit_t: *mut f32) -> c_int;

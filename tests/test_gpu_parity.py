@@ -666,10 +666,10 @@ def test_failed_scene_upload_leaves_no_scene():
         with pytest.raises(abi.RayTraceError) as e:
             r.set_scene(big, bmt)
         assert e.value.status == abi.RT_ERR_OUT_OF_MEMORY
+        r.tune(None)
         with pytest.raises(abi.RayTraceError) as e:
             r.render(cam, 16, 9, 1, 2)
         assert e.value.status == abi.RT_ERR_NO_SCENE
-        r.tune(None)
         r.set_scene(big, bmt)
         for _ in range(2):  # both in-flight slots get their work buffers
             plain, _ = r.render(cam, 32, 18, 2, 4)

@@ -19,6 +19,17 @@ if [ "${BENCH:-1}" = 1 ]; then
   step bench $?
   cat gpurun_out/bench.json
 fi
+if [ -n "${AB:-}" ]; then  # extra bench lines: AB="--tune wg_per_cu=6;--config rtiow4k ..."
+  IFS=';' read -ra ABS <<< "$AB"
+  i=0
+  for a in "${ABS[@]}"; do
+    i=$((i+1))
+    timeout -k 10 400 python bench.py --no-cpu-baseline --reuse-steps 0 --cull-steps 0 $a \
+        > gpurun_out/ab_$i.json 2>> gpurun_out/ab.err
+    step "ab $i ($a)" $?
+    cat gpurun_out/ab_$i.json
+  done
+fi
 if [ "${VALU:-0}" = 1 ]; then
   timeout -k 10 120 tools/ubench/valu_busy > gpurun_out/valu_busy.log 2>&1
   step valu_busy $?
