@@ -53,6 +53,10 @@ CASES = [
     # W*H = 800: the reference's floor(800/128) = 6 workgroups trace the first
     # 768 pixels only (D1); the test compares those
     ("wgsl_config1_40x20_ragged", scene.config1_scene, 40, 20, (0, 2)),
+    # the headline scene (BASELINE configs[1]) at 64x36 (18 workgroups, no
+    # floor remainder), 5 frames incl. >= 1000: 11,520 pixels of the
+    # reference's own kernels on the dielectric / metal / Lambertian mix
+    ("wgsl_rtiow_64x36", scene.rtiow_final_scene, 64, 36, (0, 1, 17, 1000, 4096)),
 ]
 
 
@@ -103,6 +107,8 @@ ISECT_CASES = [
     ("wgsl_isect_config1", scene.config1_scene, 2048),
     ("wgsl_isect_reference", scene.reference_scene, 512),
     ("wgsl_isect_rtiow", scene.rtiow_final_scene, 256),
+    # BASELINE configs[4]'s 10,000-sphere list (streamed, not staged)
+    ("wgsl_isect_spheres10k", scene.ten_thousand_scene, 384),
 ]
 
 
@@ -128,24 +134,53 @@ def run_intersect_world(sh, sph_bytes, rays):
             for k, v in out.items()}
 
 
+_REF = "/root/reference"
+
+
+def _shaders(ref):
+    srcs = {k: open(os.path.join(ref, "assets", "shaders", k + ".wgsl")).read() for k in KERNELS}
+    return {k: W.Shader(srcs[k]) for k in KERNELS}
+
+
+def _frame_job(args):
+    """One frame of one case (a worker process: frames are independent)."""
+    ref, name, f = args
+    _, mk, w, h, _ = next(c for c in CASES if c[0] == name)
+    sc = mk()
+    sp, mt = sc.objects_gpu(), sc.materials_gpu()
+    t0 = time.time()
+    img = run_reference(_shaders(ref), default_camera_block().tobytes(), sp.tobytes(),
+                        mt.tobytes(), w, h, f)
+    print(f"{name} frame {f}: {time.time() - t0:.1f} s", flush=True)
+    return img
+
+
+def _isect_job(args):
+    """A slice of one intersect_world ray set (a worker process)."""
+    ref, name, lo, hi = args
+    _, mk, n = next(c for c in ISECT_CASES if c[0] == name)
+    from raygen import adversarial_rays
+    sp = mk().objects_gpu()
+    rays = adversarial_rays(sp, n, seed=7)[lo:hi]
+    return run_intersect_world(_shaders(ref)["intersect"], sp.tobytes(), rays)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--ref", default=_REF)
     ap.add_argument("--only", default="")
+    ap.add_argument("--jobs", type=int, default=1, help="worker processes")
     a = ap.parse_args()
-    srcs = {k: open(os.path.join(a.ref, "assets", "shaders", k + ".wgsl")).read() for k in KERNELS}
-    shaders = {k: W.Shader(srcs[k]) for k in KERNELS}
+    from multiprocessing import Pool
+    pool = Pool(a.jobs) if a.jobs > 1 else None
+    run = pool.map if pool else lambda fn, xs: [fn(x) for x in xs]
     cam = default_camera_block()
     for name, mk, w, h, frames in CASES:
         if a.only and a.only != name:
             continue
         sc = mk()
         sp, mt = sc.objects_gpu(), sc.materials_gpu()
-        imgs = []
-        for f in frames:
-            t0 = time.time()
-            imgs.append(run_reference(shaders, cam.tobytes(), sp.tobytes(), mt.tobytes(), w, h, f))
-            print(f"{name} frame {f}: {time.time() - t0:.1f} s", flush=True)
+        imgs = run(_frame_job, [(a.ref, name, f) for f in frames])
         np.savez_compressed(os.path.join(HERE, name + ".npz"),
                             spheres=np.frombuffer(sp.tobytes(), np.uint8),
                             materials=np.frombuffer(mt.tobytes(), np.uint8),
@@ -162,7 +197,9 @@ def main():
         sp, mt = sc.objects_gpu(), sc.materials_gpu()
         rays = adversarial_rays(sp, n, seed=7)
         t0 = time.time()
-        res = run_intersect_world(shaders["intersect"], sp.tobytes(), rays)
+        step = -(-n // max(1, a.jobs))
+        parts = run(_isect_job, [(a.ref, name, lo, min(n, lo + step)) for lo in range(0, n, step)])
+        res = {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
         print(f"{name}: {n} rays {time.time() - t0:.1f} s", flush=True)
         np.savez_compressed(os.path.join(HERE, name + ".npz"),
                             spheres=np.frombuffer(sp.tobytes(), np.uint8),
