@@ -75,6 +75,9 @@ def parse():
     ap.add_argument("--cull-steps", type=int, default=-1,
                     help="extra frames timed with the culled list, RT_FLAG_CULL (0 = skip; "
                          "default 12 at N=1, skipped at N>1)")
+    ap.add_argument("--lib", default=None,
+                    help="A/B only: another build of librt_hip.so (same ABI), e.g. a previous "
+                         "round's, to compare on one box")
     ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE",
                     help="A/B only: set a library knob (rt_debug_tune; the defaults are the "
                          "product), e.g. --tune wg_per_cu=6")
@@ -176,7 +179,7 @@ def main():
     rows = abi.shard_rows(H, B, world, rank)
     max_rows = max(len(abi.shard_rows(H, B, world, k)) for k in range(world))
 
-    r = Renderer(local)
+    r = Renderer(local, lib_path=args.lib)
     for kv in args.tune:
         r.tune(*kv.split("=", 1))
     r.set_scene(spheres, mats)
@@ -382,6 +385,8 @@ def main():
                         for i in range(last)}
     if args.tune:
         out["tune"] = args.tune
+    if args.lib:
+        out["lib"] = os.path.relpath(os.path.abspath(args.lib), ROOT)
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cam, spheres, mats, W, H, S, D, args.cpu_rows,
                                            image[0].cpu().numpy())

@@ -69,6 +69,7 @@ struct Tuning {
     bool split_all = false;       // without primary reuse, every block as single samples
     bool tail_split = true;       // single-sample tail items at the end of a launch
     double tail[3] = {0.0, 0.0, 12.0};  // tail regions (4-, 2-, 1-sample items) x D x lanes
+    double block_region = 12.0;   // single-block items before the tail, x D x lanes samples
     bool prefetch = true;         // waves prefetch their next work chunk
     uint32_t prio_mode = 1;       // s_setprio rotation: 0 off, 1 by iteration, 3 by wall time
     uint32_t prio_shift = 14;     // mode 3 step: 2^prio_shift ticks of 10 ns
@@ -201,6 +202,9 @@ static bool tune_set(Tuning& t, const char* name, const char* v) {
         t.split_all = x != 0;
     } else if (!strcmp(name, "tail_split")) {
         t.tail_split = x != 0;
+    } else if (!strcmp(name, "block_region")) {
+        if (x < 0) return false;
+        t.block_region = x;
     } else if (!strcmp(name, "prefetch")) {
         t.prefetch = x != 0;
     } else if (!strcmp(name, "prio_mode")) {
@@ -790,19 +794,30 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         const uint64_t L = (A4 + A2 + A1 + RT_SAMPLE_BLOCK - 1) / RT_SAMPLE_BLOCK;
         return L < 1 ? 1 : (L > pairs ? pairs : L);
     };
+    // Block-item region: the last ~a8*D samples per lane of the main part are
+    // dealt as single-block items (knob block_region = a8, default 12), so the
+    // lanes still holding a pixel item (up to spp*D iterations) when the main
+    // part runs out finish inside the block items and the tail. In pairs:
+    const uint64_t A8 = per_px(tn.block_region, 1);
+    auto block_pairs = [&](uint64_t qmain) -> uint64_t {
+        const uint64_t Q = (A8 + RT_SAMPLE_BLOCK - 1) / RT_SAMPLE_BLOCK;
+        return Q > qmain ? qmain : Q;
+    };
     // first launch-relative sample g = f*spp + s of pair q (block b of frame f)
     auto pair_g = [&](uint64_t q, uint64_t nb, uint64_t bb) -> uint64_t {
         const uint64_t fr = q / nb;
         return fr * p.spp + (bb + (q - fr * nb)) * RT_SAMPLE_BLOCK;
     };
     // slots per pixel of a launch of F frames x blocks [bb, bb + nb): one per
-    // frame with main blocks (its lane-folded sum) + one per tail sample
+    // frame with pixel-item blocks (its lane-folded sum), one per block item,
+    // one per tail sample
     auto launch_slots = [&](uint64_t F, uint64_t nb, uint64_t bb) -> uint64_t {
         const uint64_t pairs = F * nb, L = tail_pairs(pairs);
+        const uint64_t qmain = pairs - L, qpix = qmain - block_pairs(qmain);
         const uint64_t g_end = (F - 1) * p.spp +
                                std::min<uint64_t>(p.spp, (bb + nb) * RT_SAMPLE_BLOCK);
         const uint64_t g0 = L ? pair_g(pairs - L, nb, bb) : g_end;
-        return (pairs - L + nb - 1) / nb + (g_end - g0);
+        return (qpix + nb - 1) / nb + (qmain - qpix) + (g_end - g0);
     };
     if (npix) {
         uint64_t slots_cap = tn.scratch_bytes / per_block;
@@ -946,7 +961,9 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
                                                              RT_SAMPLE_BLOCK);
         const uint64_t g0 = L ? pair_g(pairs - L, ps.nblocks, ps.block_begin) : g_end;
         K_.qmain = (uint32_t)(pairs - L);
-        K_.main_all = (K_.qmain + ps.nblocks - 1) / ps.nblocks * npix;  // (frame, pixel) items
+        K_.qpix = K_.qmain - (uint32_t)block_pairs(K_.qmain);
+        K_.main_pix = (K_.qpix + ps.nblocks - 1) / ps.nblocks * npix;  // (frame, pixel) items
+        K_.main_all = K_.main_pix + (K_.qmain - K_.qpix) * npix;         // + (pair, pixel) items
         // tail regions from the end: single samples, 2-sample, 4-sample items
         const uint64_t g2 = g_end - std::min<uint64_t>(A1, g_end - g0);
         const uint64_t g1 = g2 - std::min<uint64_t>(A2, g2 - g0);
@@ -1272,7 +1289,7 @@ int rt_debug_counters(const rt_ctx* ctx, uint64_t* out16) {
 // Internal (not in include/rt_hip.h): set one A/B or fault-injection knob of
 // ctx (struct Tuning above; names: scratch_bytes, split_all, tail_split, tail
 // "a4,a2,a1", prefetch, prio_mode, prio_shift, wg_per_cu, wide_max,
-// fast_exact, fail_alloc_after). name == NULL restores every default. Used by
+// fast_exact, fail_alloc_after, block_region). name == NULL restores every default. Used by
 // the tests and tools/ only; the product path never calls it.
 int rt_debug_tune(rt_ctx* ctx, const char* name, const char* value) {
     if (!ctx) return RT_ERR_INVALID_ARG;

@@ -99,33 +99,49 @@ struct PixelEntry {
     float4 d;
 };
 
-// Work item -> samples, pixel. A main item (item < main_all) is (frame f,
-// pixel k) with all of f's main blocks (pairs q = f*nblocks + b < qmain) in
-// block order: the lane sums each block of RT_SAMPLE_BLOCK samples in
-// registers (st.s_end = the block's end), folds the block sums in block order
-// (acc = bsum_0; acc = acc + bsum_b -- rt_collect_kernel's fold), and stores the
-// fold once, at slot = its queue index. A tail item is z = 4, 2 or 1
-// consecutive samples of one pixel, each sample's colour stored on its own.
+// Work item -> samples, pixel. The launch's main pairs (q = f*nblocks + b <
+// qmain) are dealt in two regions. Pairs q < qpix as pixel items (item <
+// main_pix): (frame f, pixel k) with all of f's pairs below qpix, in block
+// order -- the lane sums each block of RT_SAMPLE_BLOCK samples in registers
+// (st.s_end = the block's end), folds the block sums in block order (acc =
+// bsum_0; acc = acc + bsum_b, rt_collect_kernel's fold) and stores the fold
+// once, at slot = its queue index. Pairs [qpix, qmain) as block items (item <
+// main_all): one block of one pixel, its sum stored at its slot -- short
+// items at the end of the main part, so no lane holds a long pixel item
+// when the queue runs dry. A tail item is z = 4, 2 or 1 consecutive samples
+// of one pixel, each sample's colour stored on its own.
 __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint32_t item,
                                            const PixelEntry* __restrict__ tab, ItemLds L) {
     uint32_t k, s0, s1;  // pixel in processing order; the (first block's) samples [s0, s1)
     if (item < P.main_all) {
-        const uint32_t f = fdiv(item, P.div_npix);
-        k = item - f * P.npix;
-        const uint32_t mb = min(P.nblocks, P.qmain - f * P.nblocks);  // main blocks of f
+        uint32_t f, b0, b1;  // frame, the item's blocks [b0, b1) (pass-relative)
+        float4 a0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (item < P.main_pix) {
+            f = fdiv(item, P.div_npix);
+            k = item - f * P.npix;
+            b0 = 0;
+            b1 = min(P.nblocks, P.qpix - f * P.nblocks);
+            // a later pass over the frame's blocks (frames above the scratch
+            // budget) continues the fold of the earlier passes (rt_collect_kernel
+            // left it in acc_in): ((acc + b0) + b1) ..., the single-pass order
+            if (P.block_begin) {
+                a0 = P.acc_in[order_to_pixel(P, k)];
+                a0.w = 1.0f;
+            }
+        } else {
+            const uint32_t j = item - P.main_pix;
+            const uint32_t r = fdiv(j, P.div_npix);
+            k = j - r * P.npix;
+            const uint32_t q = P.qpix + r;
+            f = fdiv(q, P.div_nblocks);
+            b0 = q - f * P.nblocks;
+            b1 = b0 + 1;
+        }
         const uint32_t base = P.sample_base + f * P.spp;
-        s0 = base + P.block_begin * RT_SAMPLE_BLOCK;
-        const uint32_t iend = base + min(P.spp, (P.block_begin + mb) * RT_SAMPLE_BLOCK);
+        s0 = base + (P.block_begin + b0) * RT_SAMPLE_BLOCK;
+        const uint32_t iend = base + min(P.spp, (P.block_begin + b1) * RT_SAMPLE_BLOCK);
         s1 = min(s0 + RT_SAMPLE_BLOCK, iend);
         L->iend = iend;
-        // a later pass over the frame's blocks (frames above the scratch
-        // budget) continues the fold of the earlier passes (rt_collect_kernel
-        // left it in acc_in): ((acc + b0) + b1) ..., the single-pass order
-        float4 a0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (P.block_begin) {
-            a0 = P.acc_in[order_to_pixel(P, k)];
-            a0.w = 1.0f;
-        }
         L->acc = a0;
     } else {  // tail item: z = 4, 2 or 1 consecutive samples, each stored on its own
         uint32_t j = item - P.main_all, z, gb, ge;

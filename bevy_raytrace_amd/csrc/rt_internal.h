@@ -40,17 +40,21 @@ struct KParams {
     // sample_base + f*spp + [0, spp) of launch frame f; the seed frame is
     // frame0 + that) x blocks [block_begin, block_begin + nblocks) of each.
     // Its (frame, block) pairs q = f*nblocks + b: pairs q < qmain are the main
-    // part, dealt as one item per (frame, pixel) -- items [0, main_all =
-    // ceil(qmain / nblocks) * npix), frame-major -- covering that frame's main
-    // blocks; the lane folds their block sums and stores the fold at slot =
-    // its queue index. The rest -- the launch's tail, launch samples
-    // g = f*spp + s in [g0, g_end) -- is dealt as shrinking items so no wave
-    // holds a long item when the queue runs dry: 4-sample items over [g0, g1),
-    // 2-sample over [g1, g2), single samples over [g2, g_end), each region
+    // part, dealt as pixel items for q < qpix -- one item per (frame, pixel),
+    // items [0, main_pix = ceil(qpix / nblocks) * npix), frame-major, covering
+    // that frame's pairs below qpix; the lane folds their block sums and
+    // stores the fold at slot = its queue index -- then as block items for
+    // q in [qpix, qmain): items [main_pix, main_all), one (pair, pixel) each,
+    // pair-major, storing the block's sum at slot = its queue index (short
+    // items, so no lane holds a long pixel item when the queue runs dry). The
+    // rest -- the launch's tail, launch samples g = f*spp + s in [g0, g_end)
+    // -- is dealt as shrinking items: 4-sample items over [g0, g1), 2-sample
+    // over [g1, g2), single samples over [g2, g_end), each region
     // sample-major; a tail item stores every sample's colour at slot
     // main_all + (g - g0)*npix + k. rt_collect_kernel folds them per pixel in
     // block / sample order.
     uint32_t nframes, sample_base, qmain, main_all;
+    uint32_t qpix, main_pix;
     uint32_t g0, g1, g2, g_end;
     uint32_t ti1, ti2, tail_items;  // tail item offsets of the 2- and 1-sample regions, count
     FastDiv div_nblocks;

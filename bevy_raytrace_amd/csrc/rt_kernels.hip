@@ -456,13 +456,14 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_cull_kernel(
 // Fold one frame's results into acc (block order) and, on the frame's last
 // pass, write out = acc / spp with alpha 1 (collect.wgsl:115-125). One thread
 // per pixel of the processing order k (-> image pixel p = order_to_pixel).
-// Launch frame f = blockIdx.y. Its main blocks (pairs q = f*nblocks + b <
-// qmain) were folded by the lane that traced them (render loop: first block
-// as is -- or acc + it on a later pass -- then acc + block sum) and stored at
-// slot f*npix + k; each remaining
-// block is a tail block whose samples' colours sit at main_all + (g - g0)*npix
-// + k (g = f*spp + s), summed here exactly as a lane sums a block, ((0 + c0) +
-// c1) + ..., in sample order, then folded the same way.
+// Launch frame f = blockIdx.y, its blocks in order: those of its pixel item
+// (pairs q = f*nblocks + b < qpix), already folded by the lane that traced them
+// (first block as is -- or acc + it on a later pass -- then acc + block sum)
+// at slot f*npix + k; then its block items (qpix <= q < qmain), each sum at
+// main_pix + (q - qpix)*npix + k; then its tail blocks, whose samples' colours
+// sit at main_all + (g - g0)*npix + k (g = f*spp + s), summed here exactly as
+// a lane sums a block, ((0 + c0) + c1) + ..., in sample order. Each is folded
+// as the lane folds (first as is, then acc + it).
 // Progressive mode (rt_render_progressive): on the last pass the frame's sum
 // is folded into the running sum, prog = prog + sum (prog_mode 2) or
 // prog = sum (1, reset), and out = prog / total_spp.
@@ -482,13 +483,26 @@ __global__ void rt_collect_kernel(KParams P, const float4* __restrict__ block_su
         ax = v.x; ay = v.y; az = v.z;
     }
     const uint32_t q0 = f * P.nblocks;
-    const uint32_t mb = P.qmain > q0 ? min(P.nblocks, P.qmain - q0) : 0u;  // main blocks of f
-    if (mb) {  // the lane's fold already continued acc (start_item, later passes)
+    auto blocks_below = [&](uint32_t q) { return q > q0 ? min(P.nblocks, q - q0) : 0u; };
+    const uint32_t bp = blocks_below(P.qpix), bm = blocks_below(P.qmain);
+    auto fold = [&](float vx, float vy, float vz) {
+        if (have) {
+            ax = ax + vx; ay = ay + vy; az = az + vz;
+        } else {
+            ax = vx; ay = vy; az = vz;
+            have = true;
+        }
+    };
+    if (bp) {  // the lane's fold already continued acc (start_item, later passes)
         const float4 v = block_sums[(size_t)f * P.npix + k];
         ax = v.x; ay = v.y; az = v.z;
         have = true;
     }
-    for (uint32_t b = mb; b < P.nblocks; ++b) {  // tail blocks: their samples' colours
+    for (uint32_t b = bp; b < bm; ++b) {  // block items
+        const float4 v = block_sums[(size_t)P.main_pix + (size_t)(q0 + b - P.qpix) * P.npix + k];
+        fold(v.x, v.y, v.z);
+    }
+    for (uint32_t b = bm; b < P.nblocks; ++b) {  // tail blocks: their samples' colours
         const uint32_t sl = (P.block_begin + b) * RT_SAMPLE_BLOCK;
         const uint32_t g_end = f * P.spp + min(P.spp, sl + RT_SAMPLE_BLOCK);
         float vx = 0.0f, vy = 0.0f, vz = 0.0f;
@@ -496,12 +510,7 @@ __global__ void rt_collect_kernel(KParams P, const float4* __restrict__ block_su
             const float4 c = block_sums[(size_t)P.main_all + (size_t)(g - P.g0) * P.npix + k];
             vx = vx + c.x; vy = vy + c.y; vz = vz + c.z;
         }
-        if (have) {
-            ax = ax + vx; ay = ay + vy; az = az + vz;
-        } else {
-            ax = vx; ay = vy; az = vz;
-            have = true;
-        }
+        fold(vx, vy, vz);
     }
     if (!last_pass) {
         acc[p] = make_float4(ax, ay, az, 0.0f);

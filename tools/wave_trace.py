@@ -7,6 +7,7 @@ import torch
 from bevy_raytrace_amd import configs
 from bevy_raytrace_amd.camera import default_camera_block
 from bevy_raytrace_amd.renderer import Renderer
+import _knobs
 
 LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librt_hip_trace.so")
 wl = configs.WORKLOADS["rtiow1080"]
@@ -14,6 +15,7 @@ sc = wl.make_scene()
 cam = default_camera_block()
 r = Renderer(0, lib_path=LIB)
 r.lib.rt_debug_wave_trace.restype = ctypes.c_int
+_knobs.from_environ(r, os.environ)  # RT_WG_PER_CU=6 etc.
 r.set_scene(sc.objects_gpu(), sc.materials_gpu())
 W, H = wl.width, wl.height
 CASES = [tuple(int(v) for v in c.split(",")) for c in
