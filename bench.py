@@ -84,18 +84,43 @@ def parse():
     return ap.parse_args()
 
 
-def load_traffic(workload_key, frames_per_launch):
-    """HBM bytes per render launch from the committed rocprofv3 PMC summary
-    (measured over one launch of the fixture's frames_per_launch frames; per
-    frame it does not depend on the launch size: block sums and tail samples
-    are per frame), scaled to this run's average launch."""
+def load_pmc(workload_key):
+    """The committed rocprofv3 PMC record of the render kernel for this
+    workload (profiles/pmc_traffic.json, tools/pmc_round.sh +
+    tools/pmc_summary.py): HBM bytes and the VALU counters of one launch of
+    `frames_per_launch` frames, measured in separate --pmc passes."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            e = json.load(f).get(workload_key, {})
-        return int(e["hbm_bytes_per_launch"] / e["frames_per_launch"] * frames_per_launch)
-    except (OSError, ValueError, KeyError, ZeroDivisionError):
+            return json.load(f).get(workload_key)
+    except (OSError, ValueError):
         return None
+
+
+def load_traffic(e, frames_per_launch):
+    """HBM bytes per render launch from the PMC record, scaled per frame to
+    this run's average launch (block sums and tail samples are per frame)."""
+    try:
+        return int(e["hbm_bytes_per_launch"] / e["frames_per_launch"] * frames_per_launch)
+    except (TypeError, KeyError, ZeroDivisionError):
+        return None
+
+
+def valu_report(e):
+    """VALU busy of the render kernel from the PMC record, both forms (see
+    tools/pmc_summary.py): AMD's VALUBusy prices every VALU instruction at 4
+    cycles (one quad-cycle of SQ_ACTIVE_INST_VALU); the issue form prices
+    32-bit integer ops at their measured 2 cycles (tools/ubench/valu_busy)."""
+    v = (e or {}).get("valu")
+    if not v:
+        return None
+    out = {"amd_valubusy": round(v["valubusy_amd"], 4), "amd_formula": v["formula_amd"]}
+    if "valubusy_issue" in v:
+        out["issue_weighted"] = round(v["valubusy_issue"], 4)
+        out["issue_formula"] = v["formula_issue"]
+    out["source"] = "profiles/pmc_traffic.json (rocprofv3 --pmc, one launch of %d frames)" % (
+        e["frames_per_launch"])
+    return out
 
 
 def spawn_ranks(args):
@@ -338,7 +363,9 @@ def main():
     # duration (HIP events on the stream the kernel runs on)
     flops_total = traced_local * FLOPS_PER_SPHERE_TEST * nsph
     achieved = flops_total / (kernel_ms_total * 1e-3) / 1e12
-    traffic = load_traffic(wl.key, args.steps / max(1, len(sizes)))
+    pmc = load_pmc(wl.key)
+    traffic = load_traffic(pmc, args.steps / max(1, len(sizes)))
+    kms_launch = kernel_ms_total / launches
 
     out = {
         "metric": METRIC,
@@ -363,8 +390,14 @@ def main():
         "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
                      "traffic": traffic,
+                     # HBM GB/s of the render kernel: PMC bytes per launch / this
+                     # run's HIP-event launch time (peak ~8,000 GB/s: not the bound)
+                     "hbm_gbps": (round(traffic / (kms_launch * 1e-3) / 1e9, 2)
+                                  if traffic else None),
+                     "hbm_peak_gbps": 8000.0,
+                     "valu_busy": valu_report(pmc),
                      "kernel": "rt_render_kernel",
-                     "kernel_ms_per_launch": round(kernel_ms_total / launches, 3),
+                     "kernel_ms_per_launch": round(kms_launch, 3),
                      "flops_per_launch": flops_total / launches,
                      "basis": "traced segments x 18 x N_spheres (fp32 VALU; no MFMA)"},
         "segments_per_frame": int(segs_all / args.steps),

@@ -69,7 +69,7 @@ struct Tuning {
     bool split_all = false;       // without primary reuse, every block as single samples
     bool tail_split = true;       // single-sample tail items at the end of a launch
     double tail[3] = {0.0, 0.0, 12.0};  // tail regions (4-, 2-, 1-sample items) x D x lanes
-    double block_region = 12.0;   // single-block items before the tail, x D x lanes samples
+    double block_region = 96.0;   // single-block items before the tail, x D x lanes samples
     bool prefetch = true;         // waves prefetch their next work chunk
     uint32_t prio_mode = 1;       // s_setprio rotation: 0 off, 1 by iteration, 3 by wall time
     uint32_t prio_shift = 14;     // mode 3 step: 2^prio_shift ticks of 10 ns
@@ -795,9 +795,14 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         return L < 1 ? 1 : (L > pairs ? pairs : L);
     };
     // Block-item region: the last ~a8*D samples per lane of the main part are
-    // dealt as single-block items (knob block_region = a8, default 12), so the
+    // dealt as single-block items (knob block_region = a8, default 96), so the
     // lanes still holding a pixel item (up to spp*D iterations) when the main
-    // part runs out finish inside the block items and the tail. In pairs:
+    // part runs out finish inside the block items and the tail. It has to be
+    // long: the SIMD arbiter issues by age, and the youngest waves of a SIMD
+    // iterate several times slower than the oldest, so their
+    // last pixel items end late. Measured at 1080p/64, 24-frame launches
+    // (kernel ms, one box): a8 = 12: 521, 24: 524, 48: 517, 96: 511.5 -- the
+    // round-1 all-block-items kernel 511.7. In pairs:
     const uint64_t A8 = per_px(tn.block_region, 1);
     auto block_pairs = [&](uint64_t qmain) -> uint64_t {
         const uint64_t Q = (A8 + RT_SAMPLE_BLOCK - 1) / RT_SAMPLE_BLOCK;

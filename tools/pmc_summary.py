@@ -55,8 +55,29 @@ if "FETCH_SIZE" in rk and "WRITE_SIZE" in rk:
              "write_bytes": int(write), "frames_per_launch": fpl,
              "source": f"profiles/{tag}_pmc_{wl}.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
                        "separate passes; FETCH_SIZE x2 per gfx950 correction, x1024 KB->B)",
-             "note": f"per {fpl}-frame render launch: block-sum / tail-sample writes dominate; "
-                     "the sphere list is cache-resident"}
+             "note": f"per {fpl}-frame render launch"}
+    # VALU issue occupancy of the same launch (separate --pmc pass). gfx950:
+    # SQ_ACTIVE_INST_VALU counts one quad-cycle per VALU instruction whatever
+    # its issue cost; v_pk_fma_f32 / v_fma_f32 / v_max3_f32 issue in ~4 cycles
+    # per wave64 instruction, 32-bit integer ops in ~2 (tools/ubench/valu_busy,
+    # profiles/r02_valu_calibration.txt), so AMD's VALUBusy (the first form)
+    # can exceed 1; the second prices INT32 ops at 2 cycles.
+    if rk.get("SQ_ACTIVE_INST_VALU") and rk.get("GRBM_GUI_ACTIVE"):
+        simd_cycles = 1024 * rk["GRBM_GUI_ACTIVE"] / 8
+        ent = d[wl]
+        ent["valu"] = {
+            "sq_active_inst_valu": rk["SQ_ACTIVE_INST_VALU"], "sq_insts_valu": rk.get("SQ_INSTS_VALU"),
+            "sq_insts_valu_int32": rk.get("SQ_INSTS_VALU_INT32"),
+            "grbm_gui_active": rk["GRBM_GUI_ACTIVE"],
+            "kernel_ms_under_pmc": summary["render_kernel_ms_under_pmc"],
+            "valubusy_amd": rk["SQ_ACTIVE_INST_VALU"] * 4 / simd_cycles,
+            "formula_amd": "SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs)",
+        }
+        if rk.get("SQ_INSTS_VALU_INT32") is not None and rk.get("SQ_INSTS_VALU"):
+            i32 = rk["SQ_INSTS_VALU_INT32"]
+            ent["valu"]["valubusy_issue"] = ((rk["SQ_INSTS_VALU"] - i32) * 4 + i32 * 2) / simd_cycles
+            ent["valu"]["formula_issue"] = ("((SQ_INSTS_VALU - SQ_INSTS_VALU_INT32) x 4 + "
+                                            "SQ_INSTS_VALU_INT32 x 2) / (1024 x GRBM_GUI_ACTIVE / 8)")
     json.dump(d, open(tp, "w"), indent=1)
 print(json.dumps({k: summary[k] for k in summary if k != "per_dispatch_mean"}, indent=1))
 print(json.dumps(rk, indent=1))

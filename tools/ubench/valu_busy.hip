@@ -80,6 +80,76 @@ __global__ __launch_bounds__(256) void k_mix(float* out, float a) {
     out[blockIdx.x * 256 + threadIdx.x] = s.x + s.y + y0 + y1 + y2 + y3;
 }
 
+// One VOP instruction form, 8 independent operands per iteration (x_i = op(x_i, k)).
+#define RT_VALU_KERNEL(NAME, INSN, T)                                                        \
+    __global__ __launch_bounds__(256) void NAME(float* out, float a) {                      \
+        T x0 = (T)threadIdx.x, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3, x4 = x0 + 4,           \
+          x5 = x0 + 5, x6 = x0 + 6, x7 = x0 + 7;                                             \
+        T k = (T)a;                                                                          \
+        for (int i = 0; i < ITERS; ++i) {                                                    \
+            asm volatile(INSN " %0, %0, %8\n\t" INSN " %1, %1, %8\n\t" INSN " %2, %2, %8\n\t" \
+                         INSN " %3, %3, %8\n\t" INSN " %4, %4, %8\n\t" INSN " %5, %5, %8\n\t" \
+                         INSN " %6, %6, %8\n\t" INSN " %7, %7, %8"                           \
+                         : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(x4), "+v"(x5),     \
+                           "+v"(x6), "+v"(x7)                                                \
+                         : "v"(k));                                                          \
+        }                                                                                    \
+        out[blockIdx.x * 256 + threadIdx.x] = (float)(x0 + x1 + x2 + x3 + x4 + x5 + x6 + x7); \
+    }
+RT_VALU_KERNEL(k_addf8, "v_add_f32", float)
+RT_VALU_KERNEL(k_mulf8, "v_mul_f32", float)
+RT_VALU_KERNEL(k_max8, "v_max_f32", float)
+RT_VALU_KERNEL(k_and8, "v_and_b32", unsigned)
+RT_VALU_KERNEL(k_mullo8, "v_mul_lo_u32", unsigned)
+
+// 8 independent v_cndmask_b32 on one SGPR-pair mask
+__global__ __launch_bounds__(256) void k_cnd8(float* out, float a) {
+    float x0 = threadIdx.x, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3, x4 = x0 + 4, x5 = x0 + 5,
+          x6 = x0 + 6, x7 = x0 + 7;
+    const bool c = threadIdx.x & 1;
+    for (int i = 0; i < ITERS; ++i) {
+        asm volatile(
+            "v_cndmask_b32_e64 %0, %0, %8, %9\n\tv_cndmask_b32_e64 %1, %1, %8, %9\n\t"
+            "v_cndmask_b32_e64 %2, %2, %8, %9\n\tv_cndmask_b32_e64 %3, %3, %8, %9\n\t"
+            "v_cndmask_b32_e64 %4, %4, %8, %9\n\tv_cndmask_b32_e64 %5, %5, %8, %9\n\t"
+            "v_cndmask_b32_e64 %6, %6, %8, %9\n\tv_cndmask_b32_e64 %7, %7, %8, %9"
+            : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(x4), "+v"(x5), "+v"(x6), "+v"(x7)
+            : "v"(a), "s"(__builtin_amdgcn_ballot_w64(c)));
+    }
+    out[blockIdx.x * 256 + threadIdx.x] = ((x0 + x1) + (x2 + x3)) + ((x4 + x5) + (x6 + x7));
+}
+
+// 8 v_cmp_ge_f32 into SGPR pairs (the filter's candidate mask compares)
+__global__ __launch_bounds__(256) void k_cmp8(float* out, float a) {
+    const float x = threadIdx.x;
+    uint64_t m0, m1, m2, m3, m4, m5, m6, m7;
+    uint64_t acc = 0;
+    for (int i = 0; i < ITERS; ++i) {
+        asm volatile(
+            "v_cmp_ge_f32_e64 %0, %8, %9\n\tv_cmp_ge_f32_e64 %1, %8, %9\n\t"
+            "v_cmp_ge_f32_e64 %2, %8, %9\n\tv_cmp_ge_f32_e64 %3, %8, %9\n\t"
+            "v_cmp_ge_f32_e64 %4, %8, %9\n\tv_cmp_ge_f32_e64 %5, %8, %9\n\t"
+            "v_cmp_ge_f32_e64 %6, %8, %9\n\tv_cmp_ge_f32_e64 %7, %8, %9"
+            : "=s"(m0), "=s"(m1), "=s"(m2), "=s"(m3), "=s"(m4), "=s"(m5), "=s"(m6), "=s"(m7)
+            : "v"(x), "v"(a));
+        acc ^= m0 ^ m1 ^ m2 ^ m3 ^ m4 ^ m5 ^ m6 ^ m7;
+    }
+    out[blockIdx.x * 256 + threadIdx.x] = (float)(acc & 0xFF);
+}
+
+// 8 independent v_sqrt_f32 (transcendental unit)
+__global__ __launch_bounds__(256) void k_sqrt8(float* out, float a) {
+    float x0 = threadIdx.x + a, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3, x4 = x0 + 4,
+          x5 = x0 + 5, x6 = x0 + 6, x7 = x0 + 7;
+    for (int i = 0; i < ITERS; ++i) {
+        asm volatile(
+            "v_sqrt_f32 %0, %0\n\tv_sqrt_f32 %1, %1\n\tv_sqrt_f32 %2, %2\n\tv_sqrt_f32 %3, %3\n\t"
+            "v_sqrt_f32 %4, %4\n\tv_sqrt_f32 %5, %5\n\tv_sqrt_f32 %6, %6\n\tv_sqrt_f32 %7, %7"
+            : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(x4), "+v"(x5), "+v"(x6), "+v"(x7));
+    }
+    out[blockIdx.x * 256 + threadIdx.x] = ((x0 + x1) + (x2 + x3)) + ((x4 + x5) + (x6 + x7));
+}
+
 int main() {
     int cus = 0;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
@@ -91,7 +161,9 @@ int main() {
     hipEventCreate(&e1);
     struct K { const char* name; void (*fn)(float*, float); } ks[] = {
         {"pk_fma x8", k_pk8}, {"fma x8", k_fma8}, {"add_u32 x8", k_add8},
-        {"pk_fma x4 + max3 x4", k_mix}};
+        {"pk_fma x4 + max3 x4", k_mix}, {"add_f32 x8", k_addf8}, {"mul_f32 x8", k_mulf8},
+        {"max_f32 x8", k_max8}, {"and_b32 x8", k_and8}, {"mul_lo_u32 x8", k_mullo8},
+        {"cndmask_b32 x8", k_cnd8}, {"cmp_ge_f32 x8", k_cmp8}, {"sqrt_f32 x8", k_sqrt8}};
     for (int rep = 0; rep < 2; ++rep)
         for (const K& k : ks) {
             float ms = 0.0f;
