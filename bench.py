@@ -31,6 +31,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -441,10 +442,13 @@ def cpu_baseline(cam, spheres, mats, W, H, S, D, nrows, gpu_image):
     """Time the C oracle (scalar port of the WGSL) on a bounded row sample."""
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
-    # every host core this process may run on (no cap); the cgroup CPU quota,
-    # when there is one, is reported beside it
-    cores = len(os.sched_getaffinity(0)) or 1
+    # every host core this process may run on -- unless the cgroup grants
+    # fewer CPUs than that (the GPU box: 256 cores visible, a 16-CPU quota),
+    # where more threads than the quota only time-slice (measured: 11.8
+    # Mrays/s with 256 threads vs ~20 with 16); both counts are reported
+    host = len(os.sched_getaffinity(0)) or 1
     quota = cpu_quota()
+    cores = min(host, max(1, int(math.ceil(quota)))) if quota else host
     # calibrate on `cores` spread rows (one row per thread), then size the
     # sample for ~10 s of wall time
     rows = [int(i * H / cores) for i in range(cores)]
@@ -460,7 +464,7 @@ def cpu_baseline(cam, spheres, mats, W, H, S, D, nrows, gpu_image):
     dt = time.perf_counter() - t0
     exact = bool(np.array_equal(img, gpu_image[rows], equal_nan=True))
     return {"value": round(segs / dt / 1e6, 3), "unit": "Mrays/s", "cores": cores,
-            "cpu_quota_cores": quota, "kind": "port",
+            "host_cores": host, "cpu_quota_cores": quota, "kind": "port",
             "sample": f"{len(rows)} rows (every {stride}th) of the same {W}x{H} {S}spp frame, "
                       f"{segs} segments in {dt:.2f} s",
             "gpu_rows_bit_exact": exact}
