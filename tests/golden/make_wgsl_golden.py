@@ -57,10 +57,34 @@ CASES = [
     # floor remainder), 5 frames incl. >= 1000: 11,520 pixels of the
     # reference's own kernels on the dielectric / metal / Lambertian mix
     ("wgsl_rtiow_64x36", scene.rtiow_final_scene, 64, 36, (0, 1, 17, 1000, 4096)),
+    # consecutive frames 0..7: the reference renders one sample per frame
+    # (SAMPLES_PER_RAY = 1); an 8-spp render of this build is the blocked f32
+    # sum of exactly these frames / 8 (rt_hip.h RT_SAMPLE_BLOCK), which the
+    # accumulation tests check against these reference-executed frames
+    ("wgsl_rtiow_32x16_accum8", scene.rtiow_final_scene, 32, 16, tuple(range(8))),
 ]
 
+# Deeper schedules: the reference hard-codes 3 (intersect, shade) rounds
+# (ray_trace_node.rs:213) and the kill of a hit at bounce 2 (shade.wgsl:236,
+# `r.bounces == 2u`); this build's max_depth D generalises both. These
+# fixtures run the reference's own shaders with exactly that one constant
+# substituted (`2u` -> `D-1`, asserted to occur once) and D rounds -- the
+# reference code, generalised the way rt_params.max_depth is defined.
+DEEP_CASES = [
+    # name, scene, W, H, frames, D
+    ("wgsl_config1_32x16_d16", scene.config1_scene, 32, 16, (0, 5, 1000), 16),
+    ("wgsl_rtiow_32x16_d16", scene.rtiow_final_scene, 32, 16, (0, 2, 999), 16),
+]
+KILL_TEXT = "r.bounces == 2u"
 
-def run_reference(shaders, cam_bytes, sph_bytes, mat_bytes, width, height, frame):
+
+def deep_shade_source(src, depth):
+    assert src.count(KILL_TEXT) == 1, "shade.wgsl's bounce kill changed"
+    return src.replace(KILL_TEXT, f"r.bounces == {depth - 1}u")
+
+
+def run_reference(shaders, cam_bytes, sph_bytes, mat_bytes, width, height, frame,
+                  loops=BOUNCE_LOOPS):
     """One frame of RayTraceNode::run through the interpreted WGSL."""
     R = width * height
     groups = R // WORKGROUP  # ray_trace_node.rs:37-38 (floor)
@@ -94,7 +118,7 @@ def run_reference(shaders, cam_bytes, sph_bytes, mat_bytes, width, height, frame
         sh.bind(**res)
     shaders["clear"].dispatch("main", groups, WORKGROUP)
     shaders["generate"].dispatch("main", groups, WORKGROUP)
-    for _ in range(BOUNCE_LOOPS):
+    for _ in range(loops):
         shaders["prepass"].dispatch("main", 1, 1)
         shaders["intersect"].dispatch("main", groups, WORKGROUP)
         shaders["shade"].dispatch("main", groups, WORKGROUP)
@@ -137,20 +161,27 @@ def run_intersect_world(sh, sph_bytes, rays):
 _REF = "/root/reference"
 
 
-def _shaders(ref):
+def ALL_CASES():
+    """(name, scene, W, H, frames, depth) of every frame fixture."""
+    return [c + (BOUNCE_LOOPS,) for c in CASES] + list(DEEP_CASES)
+
+
+def _shaders(ref, depth=BOUNCE_LOOPS):
     srcs = {k: open(os.path.join(ref, "assets", "shaders", k + ".wgsl")).read() for k in KERNELS}
+    if depth != BOUNCE_LOOPS:
+        srcs["shade"] = deep_shade_source(srcs["shade"], depth)
     return {k: W.Shader(srcs[k]) for k in KERNELS}
 
 
 def _frame_job(args):
     """One frame of one case (a worker process: frames are independent)."""
     ref, name, f = args
-    _, mk, w, h, _ = next(c for c in CASES if c[0] == name)
+    _, mk, w, h, _, depth = next(c for c in ALL_CASES() if c[0] == name)
     sc = mk()
     sp, mt = sc.objects_gpu(), sc.materials_gpu()
     t0 = time.time()
-    img = run_reference(_shaders(ref), default_camera_block().tobytes(), sp.tobytes(),
-                        mt.tobytes(), w, h, f)
+    img = run_reference(_shaders(ref, depth), default_camera_block().tobytes(), sp.tobytes(),
+                        mt.tobytes(), w, h, f, loops=depth)
     print(f"{name} frame {f}: {time.time() - t0:.1f} s", flush=True)
     return img
 
@@ -175,7 +206,7 @@ def main():
     pool = Pool(a.jobs) if a.jobs > 1 else None
     run = pool.map if pool else lambda fn, xs: [fn(x) for x in xs]
     cam = default_camera_block()
-    for name, mk, w, h, frames in CASES:
+    for name, mk, w, h, frames, depth in ALL_CASES():
         if a.only and a.only != name:
             continue
         sc = mk()
@@ -185,7 +216,7 @@ def main():
                             spheres=np.frombuffer(sp.tobytes(), np.uint8),
                             materials=np.frombuffer(mt.tobytes(), np.uint8),
                             camera=np.frombuffer(cam.tobytes(), np.uint8),
-                            params=np.array([w, h, 1, BOUNCE_LOOPS], np.uint32),
+                            params=np.array([w, h, 1, depth], np.uint32),
                             frames=np.array(frames, np.uint32),
                             processed=np.array([(w * h) // WORKGROUP * WORKGROUP], np.uint32),
                             images=np.stack(imgs))

@@ -64,11 +64,15 @@ WGSL = sorted(p for p in glob.glob(os.path.join(os.path.dirname(os.path.abspath(
               if not os.path.basename(p).startswith("wgsl_isect_"))  # frames only
 
 
+WGSL_ACCUM = [p for p in WGSL if "_accum" in os.path.basename(p)]
+
+
 @pytest.mark.parametrize("flags", [0, NO_REUSE, CULL], ids=["reuse", "noreuse", "cull"])
 @pytest.mark.parametrize("path", WGSL, ids=[os.path.basename(p) for p in WGSL])
 def test_matches_interpreted_reference_wgsl(renderer, path, flags):
     """The HIP path against frames of the reference's own WGSL kernels,
-    executed by tests/golden/wgsl_exec.py (spp 1, depth 3), bit for bit."""
+    executed by tests/golden/wgsl_exec.py (spp 1; depth 3, or 16 for the
+    *_d16 fixtures whose bounce kill is generalised), bit for bit."""
     z = np.load(path, allow_pickle=False)
     sp = z["spheres"].view(abi.SPHERE_DTYPE)
     mt = z["materials"].view(abi.MATERIAL_DTYPE)
@@ -79,6 +83,23 @@ def test_matches_interpreted_reference_wgsl(renderer, path, flags):
     for f, ref in zip(z["frames"], z["images"]):
         img, _ = renderer.render(cam, W, H, S, D, frame0=int(f), flags=flags)
         check_exact(img.reshape(-1, 4)[:n], ref.reshape(-1, 4)[:n])
+
+
+@pytest.mark.parametrize("flags", [0, NO_REUSE, CULL], ids=["reuse", "noreuse", "cull"])
+@pytest.mark.parametrize("path", WGSL_ACCUM, ids=[os.path.basename(p) for p in WGSL_ACCUM])
+def test_spp_is_blocked_sum_of_reference_frames(renderer, path, flags):
+    """One S-spp render == the blocked f32 sum of the reference's S
+    one-sample frames (executed from its WGSL) / S, bit for bit."""
+    from test_oracle import blocked_mean
+    z = np.load(path, allow_pickle=False)
+    sp = z["spheres"].view(abi.SPHERE_DTYPE)
+    mt = z["materials"].view(abi.MATERIAL_DTYPE)
+    cam = z["camera"].view(abi.CAMERA_DTYPE).reshape(())
+    W, H, _, D = (int(v) for v in z["params"])
+    frames = [int(f) for f in z["frames"]]
+    renderer.set_scene(sp, mt)
+    img, _ = renderer.render(cam, W, H, len(frames), D, frame0=frames[0], flags=flags)
+    check_exact(img, blocked_mean(list(z["images"])))
 
 
 @pytest.mark.parametrize("flags", [0, NO_REUSE, CULL, CULL | NO_REUSE],
