@@ -996,7 +996,7 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         HIP_TRY_Q(hipEventRecord(f.ev[2 * i + 1], stream));
         const bool first_pass = ps.block_begin == 0;
         const bool last_pass = ps.block_begin + ps.nblocks == blocks_total;
-        HIP_TRY_Q(rt_launch_collect(&K_, f.d_pd, f.d_block_sums, f.d_acc, first_pass, last_pass,
+        HIP_TRY_Q(rt_launch_collect(&K_, f.d_block_sums, f.d_acc, first_pass, last_pass,
                                        (float)p.spp, d_out + (size_t)ps.frame_begin * npix,
                                        ctx->d_prog, prog_mode, prog_total, stream));
     }

@@ -105,7 +105,7 @@ hipError_t rt_launch_render(const KParams* P, const float4* grp, const float4* s
                             float4* block_sums,
                             uint32_t* work_counter, unsigned long long* seg_counter, uint32_t grid,
                             hipStream_t stream);
-hipError_t rt_launch_collect(const KParams* P, const float4* pd, const float4* block_sums,
+hipError_t rt_launch_collect(const KParams* P, const float4* block_sums,
                              float4* acc, int first_pass, int last_pass, float spp, float4* out,
                              float4* prog, int prog_mode, float prog_total, hipStream_t stream);
 hipError_t rt_launch_srgb8(const float4* in, uchar4* out, uint64_t npix, hipStream_t stream);

@@ -587,11 +587,10 @@ hipError_t rt_launch_primary(const KParams* P, float4* pd, hipStream_t stream) {
     return hipGetLastError();
 }
 
-hipError_t rt_launch_collect(const KParams* P, const float4* pd, const float4* block_sums,
+hipError_t rt_launch_collect(const KParams* P, const float4* block_sums,
                              float4* acc, int first_pass, int last_pass, float spp, float4* out,
                              float4* prog, int prog_mode, float prog_total, hipStream_t stream) {
     const uint32_t T = 256;
-    (void)pd;
     hipLaunchKernelGGL(rt_collect_kernel, dim3((P->npix + T - 1) / T, P->nframes), dim3(T), 0, stream, *P,
                        block_sums, acc, first_pass, last_pass, spp, out, prog, prog_mode,
                        prog_total);
