@@ -150,6 +150,67 @@ __global__ __launch_bounds__(256) void k_sqrt8(float* out, float a) {
     out[blockIdx.x * 256 + threadIdx.x] = ((x0 + x1) + (x2 + x3)) + ((x4 + x5) + (x6 + x7));
 }
 
+// forms considered for the candidate mask (sign bits of H - T instead of 8
+// compares into SGPRs): packed add, byte permute, shift-or, add-with-carry
+typedef float f2v __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(256) void k_pkadd8(float* out, float a) {
+    f2v x0 = {(float)threadIdx.x, 1.0f}, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3, x4 = x0 + 4,
+        x5 = x0 + 5, x6 = x0 + 6, x7 = x0 + 7;
+    const f2v k = {a, a};
+    for (int i = 0; i < ITERS; ++i) {
+        asm volatile(
+            "v_pk_add_f32 %0, %0, %8\n\tv_pk_add_f32 %1, %1, %8\n\t"
+            "v_pk_add_f32 %2, %2, %8\n\tv_pk_add_f32 %3, %3, %8\n\t"
+            "v_pk_add_f32 %4, %4, %8\n\tv_pk_add_f32 %5, %5, %8\n\t"
+            "v_pk_add_f32 %6, %6, %8\n\tv_pk_add_f32 %7, %7, %8"
+            : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(x4), "+v"(x5), "+v"(x6), "+v"(x7)
+            : "v"(k));
+    }
+    const f2v s2 = ((x0 + x1) + (x2 + x3)) + ((x4 + x5) + (x6 + x7));
+    out[blockIdx.x * 256 + threadIdx.x] = s2.x + s2.y;
+}
+#define RT_VOP3_KERNEL(NAME, INSN)                                                          \
+    __global__ __launch_bounds__(256) void NAME(float* out, float a) {                      \
+        unsigned x0 = threadIdx.x, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3, x4 = x0 + 4,       \
+                 x5 = x0 + 5, x6 = x0 + 6, x7 = x0 + 7;                                      \
+        const unsigned k = (unsigned)(a * 1000.0f), sel = 0x07030602u;                       \
+        for (int i = 0; i < ITERS; ++i) {                                                    \
+            asm volatile(INSN(0) "\n\t" INSN(1) "\n\t" INSN(2) "\n\t" INSN(3) "\n\t"     \
+                         INSN(4) "\n\t" INSN(5) "\n\t" INSN(6) "\n\t" INSN(7)              \
+                         : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(x4), "+v"(x5),     \
+                           "+v"(x6), "+v"(x7)                                                \
+                         : "v"(k), "v"(sel));                                                \
+        }                                                                                    \
+        out[blockIdx.x * 256 + threadIdx.x] = (float)(x0 ^ x1 ^ x2 ^ x3 ^ x4 ^ x5 ^ x6 ^ x7); \
+    }
+#define PERM_I(n) "v_perm_b32 %" #n ", %" #n ", %8, %9"
+#define LSHLOR_I(n) "v_lshl_or_b32 %" #n ", %" #n ", 1, %8"
+#define MOV_I(n) "v_mov_b32 %" #n ", %8"
+#define ANDOR_I(n) "v_and_or_b32 %" #n ", %" #n ", %9, %8"
+RT_VOP3_KERNEL(k_perm8, PERM_I)
+RT_VOP3_KERNEL(k_lshlor8, LSHLOR_I)
+RT_VOP3_KERNEL(k_mov8, MOV_I)
+RT_VOP3_KERNEL(k_andor8, ANDOR_I)
+
+// 8 v_addc_co_u32 (carry in/out in SGPR pairs), the current mask build
+__global__ __launch_bounds__(256) void k_addc8(float* out, float a) {
+    unsigned x0 = threadIdx.x, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3, x4 = x0 + 4, x5 = x0 + 5,
+             x6 = x0 + 6, x7 = x0 + 7;
+    const uint64_t c = __builtin_amdgcn_ballot_w64(threadIdx.x & 1);
+    uint64_t o0, o1, o2, o3, o4, o5, o6, o7;
+    for (int i = 0; i < ITERS; ++i) {
+        asm volatile(
+            "v_addc_co_u32_e64 %0, %8, %0, %0, %16\n\tv_addc_co_u32_e64 %1, %9, %1, %1, %16\n\t"
+            "v_addc_co_u32_e64 %2, %10, %2, %2, %16\n\tv_addc_co_u32_e64 %3, %11, %3, %3, %16\n\t"
+            "v_addc_co_u32_e64 %4, %12, %4, %4, %16\n\tv_addc_co_u32_e64 %5, %13, %5, %5, %16\n\t"
+            "v_addc_co_u32_e64 %6, %14, %6, %6, %16\n\tv_addc_co_u32_e64 %7, %15, %7, %7, %16"
+            : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(x4), "+v"(x5), "+v"(x6), "+v"(x7),
+              "=&s"(o0), "=&s"(o1), "=&s"(o2), "=&s"(o3), "=&s"(o4), "=&s"(o5), "=&s"(o6), "=&s"(o7)
+            : "s"(c));
+    }
+    out[blockIdx.x * 256 + threadIdx.x] = (float)(x0 ^ x1 ^ x2 ^ x3 ^ x4 ^ x5 ^ x6 ^ x7);
+}
+
 int main() {
     int cus = 0;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
@@ -163,7 +224,9 @@ int main() {
         {"pk_fma x8", k_pk8}, {"fma x8", k_fma8}, {"add_u32 x8", k_add8},
         {"pk_fma x4 + max3 x4", k_mix}, {"add_f32 x8", k_addf8}, {"mul_f32 x8", k_mulf8},
         {"max_f32 x8", k_max8}, {"and_b32 x8", k_and8}, {"mul_lo_u32 x8", k_mullo8},
-        {"cndmask_b32 x8", k_cnd8}, {"cmp_ge_f32 x8", k_cmp8}, {"sqrt_f32 x8", k_sqrt8}};
+        {"cndmask_b32 x8", k_cnd8}, {"cmp_ge_f32 x8", k_cmp8}, {"sqrt_f32 x8", k_sqrt8},
+        {"pk_add_f32 x8", k_pkadd8}, {"perm_b32 x8", k_perm8}, {"lshl_or_b32 x8", k_lshlor8},
+        {"mov_b32 x8", k_mov8}, {"and_or_b32 x8", k_andor8}, {"addc_co_u32 x8", k_addc8}};
     for (int rep = 0; rep < 2; ++rep)
         for (const K& k : ks) {
             float ms = 0.0f;
