@@ -46,3 +46,33 @@ def test_bench_launches_its_own_ranks():
     assert sum(b["ranks"]["segments"]) // 4 == a["segments_per_frame"]  # 4 timed frames
     assert a["check"] == b["check"]
     assert a["segments_per_frame"] == b["segments_per_frame"]
+
+
+@pytest.mark.gpu
+def test_bench_line_carries_the_contract_fields():
+    """The driver-facing line (small run of the default config shape on
+    config 1, a 2-row CPU sample): every contract key, the roofline block and
+    the CPU baseline, with self-consistent numbers."""
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "config1",
+                        "--steps", "2", "--warmup", "1", "--frames-per-launch", "2",
+                        "--reuse-steps", "0", "--cull-steps", "0", "--cpu-rows", "2"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=200)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = p.stdout.splitlines()
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+              "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1
+    assert d["higher_is_better"] is True and d["value"] > 0 and "workload" in d["config"]
+    rf = d["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in rf, k
+    assert rf["unit"] == "TFLOP/s" and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    cb = d["cpu_baseline"]
+    for k in ("value", "unit", "cores", "kind", "sample"):
+        assert k in cb, k
+    assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port"
+    assert cb.get("gpu_rows_bit_exact") is True
