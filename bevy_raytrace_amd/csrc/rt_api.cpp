@@ -110,6 +110,11 @@ struct rt_ctx {
     float4* d_bnd_c = nullptr;
     uint32_t* d_perm_c = nullptr;
     size_t grp_c_cap = 0, sph_c_cap = 0, rm_c_cap = 0, bnd_c_cap = 0, perm_c_cap = 0;
+    // matrix-core filter (RT_MFMA_FILTER builds, build_mfma): f16 A fragments
+    bool mf_dirty = true, mf_ok = false;
+    uint32_t mf_nblk = 0;
+    uint4* d_mfA = nullptr;
+    size_t mfA_cap = 0;
 
     // frames in flight: RT_MAX_PENDING slots of per-frame work buffers, each
     // with its own stream, so frame i+1 can start while frame i drains
@@ -301,6 +306,7 @@ void rt_destroy(rt_ctx* ctx) {
     hipFree(ctx->d_rm_c);
     hipFree(ctx->d_bnd_c);
     hipFree(ctx->d_perm_c);
+    hipFree(ctx->d_mfA);
     for (Frame& f : ctx->fr) {
         hipFree(f.d_block_sums);
         hipFree(f.d_acc);
@@ -646,6 +652,7 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n, const rt_mat
     // half-written or freed list behind stale counts).
     ctx->has_scene = false;
     ctx->cull_dirty = true;
+    ctx->mf_dirty = true;
     ctx->n = ctx->ngroups = ctx->m = 0;
     rc = ensure(ctx, &ctx->d_sph, &ctx->sph_cap, sizeof(float4) * nrec);
     if (rc) return rc;
@@ -682,6 +689,74 @@ static int cull_ready(rt_ctx* ctx) {
     return RT_OK;
 }
 
+#ifdef RT_MFMA_FILTER
+// ---- matrix-core filter fragments (rt_dev_intersect.h intersect_world_mfma) ----
+// Row j of the A operand (sphere j): [cx_hi, cx_lo, cx_hi, cy.., cz.., 1, 1,
+// S'_hi, S'_lo, 0, 0, 0], hi = RN_f16(c), lo = RN_f16(c - hi), S' = r^2 -
+// (1 - m - mu')|c|^2 from double. Block b (spheres 32b..32b+31), lane l: row
+// l & 31, elements k = 8 (l >> 5) .. + 8. Pad rows: c = 0, S'_hi = -inf (H is
+// -inf or NaN there: never a candidate). Only scenes whose centres and S' fit
+// the split's range take it (mf_ok); the rest keep the VALU filter.
+static uint16_t f16_bits(double x) {
+    const _Float16 h = (_Float16)x;
+    uint16_t u;
+    std::memcpy(&u, &h, 2);
+    return u;
+}
+
+static int build_mfma(rt_ctx* ctx) {
+    const uint32_t n = ctx->n;
+    ctx->mf_ok = false;
+    if (!n) return RT_OK;
+    const double kS = 1.0 - 0x1p-16 - 0x1p-14;  // 1 - m - mu' (RT_MF_MU)
+    const uint32_t nblk = (n + 31) / 32;
+    std::vector<uint16_t> h((size_t)nblk * 64 * 8);
+    for (uint32_t j = 0; j < n; ++j) {
+        const float4 q = ctx->h_sph[j];
+        if (!(std::fabs(q.x) <= 0x1p12f && std::fabs(q.y) <= 0x1p12f && std::fabs(q.z) <= 0x1p12f &&
+              q.w >= 0.0f && q.w <= 0x1p24f))
+            return RT_OK;  // outside the f16 split's range: VALU filter
+    }
+    for (uint32_t b = 0; b < nblk; ++b)
+        for (uint32_t l = 0; l < 64; ++l) {
+            const uint32_t j = 32 * b + (l & 31), hh = l >> 5;
+            uint16_t row[16] = {};
+            const uint16_t one = f16_bits(1.0);
+            if (j < n) {
+                const float4 q = ctx->h_sph[j];
+                const float c[3] = {q.x, q.y, q.z};
+                for (int a = 0; a < 3; ++a) {
+                    const uint16_t hi = f16_bits(c[a]);
+                    _Float16 hv;
+                    std::memcpy(&hv, &hi, 2);
+                    const uint16_t lo = f16_bits((double)c[a] - (double)hv);
+                    row[3 * a] = hi;
+                    row[3 * a + 1] = lo;
+                    row[3 * a + 2] = hi;
+                }
+                const double cc = (double)q.x * q.x + (double)q.y * q.y + (double)q.z * q.z;
+                const double S = (double)q.w - kS * cc;
+                if (!(std::fabs(S) <= 0x1p15)) return RT_OK;
+                const uint16_t sh = f16_bits(S);
+                _Float16 sv;
+                std::memcpy(&sv, &sh, 2);
+                row[11] = sh;
+                row[12] = f16_bits(S - (double)sv);
+            } else {
+                row[11] = f16_bits(-INFINITY);
+            }
+            row[9] = row[10] = one;
+            std::memcpy(&h[((size_t)b * 64 + l) * 8], &row[8 * hh], 16);
+        }
+    int rc = ensure(ctx, &ctx->d_mfA, &ctx->mfA_cap, h.size() * sizeof(uint16_t));
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpy(ctx->d_mfA, h.data(), h.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+    ctx->mf_nblk = nblk;
+    ctx->mf_ok = true;
+    return RT_OK;
+}
+#endif
+
 int rt_update_spheres(rt_ctx* ctx, uint32_t first, const rt_sphere* spheres, uint32_t count) {
     if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_update_spheres: ctx is NULL");
     if (!ctx->has_scene) return fail(ctx, RT_ERR_NO_SCENE, "rt_update_spheres before rt_set_scene");
@@ -705,6 +780,7 @@ int rt_update_spheres(rt_ctx* ctx, uint32_t first, const rt_sphere* spheres, uin
                            sizeof(float4) * RT_GROUP * (g1 - g0), hipMemcpyHostToDevice));
     ctx->scene_fast = scene_fast_ok(ctx);
     ctx->cull_dirty = true;  // the permutation and bounds follow at the next culled call
+    ctx->mf_dirty = true;
     return RT_OK;
 }
 
@@ -899,6 +975,19 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     }
     K_.scene_fast = ctx->scene_fast && tn.fast_exact ? 1u : 0u;
     K_.flags = p.flags;
+#ifdef RT_MFMA_FILTER
+    if (!cull) {
+        if (ctx->mf_dirty) {
+            int rc = build_mfma(ctx);
+            if (rc) return rc;
+            ctx->mf_dirty = false;
+        }
+        if (ctx->mf_ok) {
+            K_.mfA = ctx->d_mfA;
+            K_.mf_nblk = ctx->mf_nblk;
+        }
+    }
+#endif
     std::memcpy(K_.T, cam->transform, sizeof(K_.T));
     K_.tan_half = (float)std::tan((double)(cam->fov / 2.0f));                 // generate.wgsl:67
     K_.focus_plane = (cam->image_plane_distance * cam->lens_focal_length) /  // generate.wgsl:94-95

@@ -63,7 +63,9 @@ __device__ uint32_t g_prof_dummy;
 // (t, original index perm[idx]) -- the sequential strict-`<` scan's answer in
 // the original order (intersect.wgsl:137) whatever order the candidates come
 // in. perm is read only on an exact tie.
-template <bool FAST, bool CULL>
+// LEX (the matrix-core filter, candidates in any order): the lexicographic
+// minimum of (t, index), the sequential scan's answer without a permutation.
+template <bool FAST, bool CULL, bool LEX = false>
 __device__ __forceinline__ void exact_body(float4 s, int idx, v3 o, v3 d, float a, float ya,
                                            float& best_t, int& best_i,
                                            const uint32_t* perm EXACT_ARGS) {
@@ -100,6 +102,11 @@ __device__ __forceinline__ void exact_body(float4 s, int idx, v3 o, v3 d, float 
     if (CULL) {
         if (root <= best_t &&
             (root < best_t || (best_i >= 0 && perm[idx] < perm[best_i]))) {
+            best_t = root;
+            best_i = idx;
+        }
+    } else if (LEX) {
+        if (root < best_t || (root == best_t && idx < best_i)) {
             best_t = root;
             best_i = idx;
         }
@@ -589,5 +596,218 @@ __device__ __forceinline__ uint32_t lanemask_lt_count(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+
+
+#ifdef RT_MFMA_FILTER
+// ---- the filter on the matrix cores (RT_MFMA_FILTER builds) ----
+// Per 32-sphere block b and per 32-ray half t of the wave, two
+// v_mfma_f32_32x32x16_f16 give hb = k1 - dn.c and v = S' + o2.c for the 32 x 32
+// (sphere, ray) pairs from f16 hi/lo parts (A row of sphere j: [cx_hi, cx_lo,
+// cx_hi, cy.., cz.., 1, 1, S'_hi, S'_lo, 0, 0, 0]; B column of a ray: u =
+// [-dnx_hi, -dnx_hi, -dnx_lo, .., k1_hi, k1_lo, 0, 0, ..], v = [o2x_hi, o2x_hi,
+// o2x_lo, .., 0, 0, 1, 1, ..]), then H = hb^2 + v as the VALU filter, against
+// T' = (1 - m - mu')|o|^2 with the wider mu' of the split arithmetic. Output
+// layout (MI355X guide): lane l holds column (ray) l & 31 of the half, rows
+// (spheres) (i & 3) + 8 (i >> 2) + 4 (l >> 5) in register i: four whole groups
+// of 4 spheres per lane. A lane queues (group-of-4 index << 4 | 4-bit mask)
+// per half; the ray's lane drains the entries of its column's two lanes, in
+// any order, with the (t, index) tie-break (exact_body LEX).
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef float f16x __attribute__((ext_vector_type(16)));
+#define RT_MF_MU 0x1p-14f
+#define RT_MF_CAP 8  // queue entries per lane and half (LDS)
+
+__device__ __forceinline__ uint32_t bperm(uint32_t src_lane, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
+}
+
+__device__ __forceinline__ uint32_t pack2h(float x, float y) {
+    const _Float16 a = (_Float16)x, b = (_Float16)y;
+    uint16_t ua, ub;
+    __builtin_memcpy(&ua, &a, 2);
+    __builtin_memcpy(&ub, &b, 2);
+    return (uint32_t)ua | ((uint32_t)ub << 16);
+}
+// hi / lo f16 parts of x (lo = the rounding residual, itself rounded to f16)
+__device__ __forceinline__ void split_h(float x, float& hi, float& lo) {
+    hi = (float)(_Float16)x;
+    lo = (float)(_Float16)(x - hi);
+}
+
+// the wave may use the f16 filter: every live lane's |o| within the split's range
+__device__ __forceinline__ bool mfma_wave_ok(v3 o, bool live) {
+    const float om = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+    return rt_ballot(live && !(om <= 0x1p12f)) == 0;
+}
+
+template <bool FAST>
+__device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, uint32_t cnt1,
+                                           const float4* __restrict__ sph, v3 o, v3 d, float a,
+                                           float ya, float& best_t, int& best_i) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const uint32_t lane = __lane_id();
+    const uint32_t t = lane >> 5, j = lane & 31u;
+    // the two lanes holding this ray's column: j (rows 4h, h = 0) and j + 32
+    const uint32_t x0 = bperm(j, cnt0), x1 = bperm(j, cnt1);
+    const uint32_t y0 = bperm(j + 32u, cnt0), y1 = bperm(j + 32u, cnt1);
+    const uint32_t na = t ? x1 : x0, nb = t ? y1 : y0;
+    const uint32_t* q = cq + t * (RT_MF_CAP * 64u);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (uint32_t side = 0; side < 2; ++side) {
+        const uint32_t n = side ? nb : na, col = side ? j + 32u : j;
+        for (uint32_t k = 0; k < n; ++k) {
+            const uint32_t e = q[k * 64u + col];
+            uint32_t m = e & 15u;
+            const uint32_t base = (e >> 4) * 4u;
+            while (m) {
+                const uint32_t b = __builtin_ctz(m);
+                m &= m - 1;
+                exact_body<FAST, false, true>(sph[base + b], (int)(base + b), o, d, a, ya, best_t,
+                                              best_i, nullptr);
+            }
+        }
+    }
+}
+
+// Called by the whole wave (the MFMA operands span all 64 lanes): lanes
+// without a ray (live false) trace a dummy ray whose threshold is +inf.
+__device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mfA, uint32_t nblk,
+                                                    const float4* __restrict__ sph,
+                                                    uint32_t scene_fast, v3 o, v3 d, bool live,
+                                                    uint64_t live_mask, float& t_out,
+                                                    uint32_t* cq) {
+    if (!live) {
+        o = mk(0.0f, 0.0f, 0.0f);
+        d = mk(0.0f, 0.0f, 1.0f);
+    }
+    const float l = sqrt_x(dot(d, d));
+    const float a = l * l;  // sqr(length(r.dir)), intersect.wgsl:98
+    const bool fast = ray_fast(scene_fast, o, a);
+    const float ya = fast ? rt_recip_rn(a) : a;
+    const uint32_t lane = __lane_id();
+    const uint32_t h = lane >> 5;
+    // ray constants (ray_filter_consts, with the wider mu')
+    const float rs = __builtin_amdgcn_rsqf(dot(d, d));
+    const float dnx = d.x * rs, dny = d.y * rs, dnz = d.z * rs;
+    const float m_ = 0x1p-16f;
+    const float oo = __builtin_fmaf(o.z, o.z, __builtin_fmaf(o.y, o.y, o.x * o.x));
+    const float k1 = __builtin_fmaf(dnz, o.z, __builtin_fmaf(dny, o.y, dnx * o.x));
+    const float two = 2.0f * (1.0f - m_);
+    const float T = live ? (1.0f - m_ - RT_MF_MU) * oo : INFINITY;
+    float xh, xl, yh, yl, zh, zl, kh, kl;
+    split_h(-dnx, xh, xl);
+    split_h(-dny, yh, yl);
+    split_h(-dnz, zh, zl);
+    split_h(k1, kh, kl);
+    // u = [x_hi, x_hi, x_lo, y_hi, y_hi, y_lo, z_hi, z_hi | z_lo, k_hi, k_lo, 0, 0, 0, 0, 0]
+    const uint32_t ul0 = pack2h(xh, xh), ul1 = pack2h(xl, yh), ul2 = pack2h(yh, yl),
+                   ul3 = pack2h(zh, zh);
+    const uint32_t uh0 = pack2h(zl, kh), uh1 = pack2h(kl, 0.0f), uh2 = 0u, uh3 = 0u;
+    float ph, pl, qh, ql, rh, rl;
+    split_h(two * o.x, ph, pl);
+    split_h(two * o.y, qh, ql);
+    split_h(two * o.z, rh, rl);
+    // v = [p_hi, p_hi, p_lo, q_hi, q_hi, q_lo, r_hi, r_hi | r_lo, 0, 0, 1, 1, 0, 0, 0]
+    const uint32_t vl0 = pack2h(ph, ph), vl1 = pack2h(pl, qh), vl2 = pack2h(qh, ql),
+                   vl3 = pack2h(rh, rh);
+    const uint32_t vh0 = pack2h(rl, 0.0f), vh1 = pack2h(0.0f, 1.0f), vh2 = pack2h(1.0f, 0.0f),
+                   vh3 = 0u;
+    // B fragments: half 0 = rays 0..31 (lane l: column l & 31, k 8h..8h+7),
+    // half 1 = rays 32..63; a lane's own ray gives its K half, the partner
+    // (lane ^ 32) the other
+    const uint32_t partner = lane ^ 32u;
+    auto frag = [&](uint32_t lo, uint32_t hi, uint32_t& f0, uint32_t& f1) {
+        const uint32_t recv = bperm(partner, h ? lo : hi);
+        f0 = h ? recv : lo;
+        f1 = h ? hi : recv;
+    };
+    uint32_t u00, u01, u02, u03, u10, u11, u12, u13, v00, v01, v02, v03, v10, v11, v12, v13;
+    frag(ul0, uh0, u00, u10);
+    frag(ul1, uh1, u01, u11);
+    frag(ul2, uh2, u02, u12);
+    frag(ul3, uh3, u03, u13);
+    frag(vl0, vh0, v00, v10);
+    frag(vl1, vh1, v01, v11);
+    frag(vl2, vh2, v02, v12);
+    frag(vl3, vh3, v03, v13);
+    auto as_h8 = [](uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+        const uint4 q = make_uint4(w0, w1, w2, w3);
+        h8v r;
+        __builtin_memcpy(&r, &q, 16);
+        return r;
+    };
+    const h8v Bu0 = as_h8(u00, u01, u02, u03), Bu1 = as_h8(u10, u11, u12, u13);
+    const h8v Bv0 = as_h8(v00, v01, v02, v03), Bv1 = as_h8(v10, v11, v12, v13);
+    const float Tp = __uint_as_float(bperm(partner, __float_as_uint(T)));
+    const float T0 = h ? Tp : T, T1 = h ? T : Tp;
+
+    float best_t = VERY_FAR;
+    int best_i = -1;
+    uint32_t cnt0 = 0, cnt1 = 0;
+    const f16x zero = {};
+    // is the ray of this lane's column live, per half
+    const bool col0 = (live_mask >> (lane & 31u)) & 1u, col1 = (live_mask >> (32u + (lane & 31u))) & 1u;
+    const uint4* ap = mfA + lane;
+    uint4 a4 = ap[0];  // (RT_MF_PREFETCH: the next block's fragment loads during this one)
+    for (uint32_t b = 0; b < nblk; ++b) {
+        // a block adds at most 4 entries to each half's queue: make room first,
+        // while no tile result is live
+        if (rt_ballot(max(cnt0, cnt1) + 4u > RT_MF_CAP) != 0) {
+            if (fast)
+                mfma_drain<true>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i);
+            else
+                mfma_drain<false>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i);
+            cnt0 = cnt1 = 0;
+        }
+#ifdef RT_MF_PREFETCH
+        const uint4 an = ap[(size_t)(b + 1 < nblk ? b + 1 : b) * 64u];
+#else
+        a4 = ap[(size_t)b * 64u];
+#endif
+        h8v A;
+        __builtin_memcpy(&A, &a4, 16);
+#pragma nounroll
+        for (uint32_t t = 0; t < 2; ++t) {
+            const f16x U = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, t ? Bu1 : Bu0, zero, 0, 0, 0);
+            const f16x V = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, t ? Bv1 : Bv0, zero, 0, 0, 0);
+            const float Tt = t ? T1 : T0;
+            float H[16];
+#pragma unroll
+            for (int i = 0; i < 16; i += 2) {
+                const f2 hb = {U[i], U[i + 1]}, vs = {V[i], V[i + 1]};
+                const f2 hh = pk_fma(hb, hb, vs);
+                H[i] = hh.x;
+                H[i + 1] = hh.y;
+            }
+            float g = fmaxf(fmaxf(fmaxf(H[0], H[1]), fmaxf(H[2], H[3])),
+                            fmaxf(fmaxf(H[4], H[5]), fmaxf(H[6], H[7])));
+            g = fmaxf(g, fmaxf(fmaxf(fmaxf(H[8], H[9]), fmaxf(H[10], H[11])),
+                               fmaxf(fmaxf(H[12], H[13]), fmaxf(H[14], H[15]))));
+            if (rt_ballot(g >= Tt) != 0) {
+                uint32_t& cnt = t ? cnt1 : cnt0;
+                uint32_t* qt = cq + t * (RT_MF_CAP * 64u);
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q) {
+                    const uint32_t m4 = ge(H[4 * q], Tt) | (ge(H[4 * q + 1], Tt) << 1) |
+                                        (ge(H[4 * q + 2], Tt) << 2) | (ge(H[4 * q + 3], Tt) << 3);
+                    if (m4 && (t ? col1 : col0)) {
+                        qt[cnt * 64u + lane] = (((b * 8u) + q * 2u + h) << 4) | m4;
+                        ++cnt;
+                    }
+                }
+            }
+        }
+#ifdef RT_MF_PREFETCH
+        a4 = an;
+#endif
+    }
+    if (fast)
+        mfma_drain<true>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i);
+    else
+        mfma_drain<false>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i);
+    t_out = best_t;
+    return best_i;
+}
+#endif  // RT_MFMA_FILTER
 
 }  // namespace

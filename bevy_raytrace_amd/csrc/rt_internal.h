@@ -87,6 +87,11 @@ struct KParams {
     uint32_t nclusters;
     uint32_t cull_supers;   // 1: test the cluster bounds (many clusters); 0: walk every cluster
     const float4* acc_in;   // passes after the first (block_begin > 0): the fold so far, per pixel
+    // matrix-core filter (RT_MFMA_FILTER builds, brute-force walk): the list as
+    // f16 A fragments of v_mfma_f32_32x32x16_f16, per 32-sphere block 64 lanes
+    // x 16 B (rt_api.cpp build_mfma); null: the packed VALU filter
+    const uint4* mfA;
+    uint32_t mf_nblk;
 };
 
 // Row block b of the image -> owning shard (rt_params: serpentine deal).

@@ -118,6 +118,11 @@ __device__ __forceinline__ void render_body(
     __shared__ uint32_t s_cq[RT_BLOCK_THREADS * RT_CQ_CAP];  // per-lane candidate queues
     uint32_t* cq = s_cq + wave * (64u * RT_CQ_CAP);
     __shared__ LaneLds s_lane[RT_BLOCK_THREADS];  // per-lane item state (rt_dev_path.h)
+#ifdef RT_MFMA_FILTER
+    // the matrix-core filter's queues: per wave 2 halves x RT_MF_CAP x 64 lanes
+    __shared__ uint32_t s_cqm[(RT_BLOCK_THREADS / 64) * 2 * RT_MF_CAP * 64];
+    uint32_t* cqm = s_cqm + wave * (2u * RT_MF_CAP * 64u);
+#endif
     const ItemLds lds = s_lane + wave * 64u + lane;
 #ifdef RT_SPHERES_LDS
     // Experiment variant: the filter reads the sphere groups from LDS (staged
@@ -268,6 +273,13 @@ __device__ __forceinline__ void render_body(
         const uint64_t live = rt_ballot(has_item);
         if ((uint32_t)__popcll(live) <= P.wide_max) {  // nearly empty wave: sphere-parallel
             intersect_wide<CULL>(sph, P.nspheres, P.scene_fast, live, st.o, st.d, hi, t, P.perm);
+#ifdef RT_MFMA_FILTER
+        } else if (!CULL && P.mfA && mfma_wave_ok(st.o, has_item)) {  // the whole wave
+            const int h2 = intersect_world_mfma(P.mfA, P.mf_nblk, sph, P.scene_fast, st.o, st.d,
+                                                has_item, live, t, cqm);
+            if (has_item) hi = h2;
+            else t = VERY_FAR;
+#endif
         } else if (has_item) {
             hi = intersect_world<CULL>(grp, sph, P.ngroups, P.scene_fast, st.o, st.d, t, cq,
 #ifdef RT_PROFILE
