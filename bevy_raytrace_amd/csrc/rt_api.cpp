@@ -83,7 +83,8 @@ struct rt_ctx {
     int device = 0;
     std::string err;
     int cu_count = 0;
-    int blocks_per_cu = 0;
+    int blocks_per_cu = 0;          // resident workgroups per CU, brute-force kernel
+    int blocks_per_cu_c = 0;        // ... culled kernel
     Tuning tune;
     uint64_t allocs = 0;            // device allocations made (rt_debug_alloc_count)
 
@@ -111,7 +112,7 @@ struct rt_ctx {
     uint32_t* d_perm_c = nullptr;
     size_t grp_c_cap = 0, sph_c_cap = 0, rm_c_cap = 0, bnd_c_cap = 0, perm_c_cap = 0;
     // matrix-core filter (RT_MFMA_FILTER builds, build_mfma): f16 A fragments
-    bool mf_dirty = true, mf_ok = false;
+    bool mf_ok = false;
     uint32_t mf_nblk = 0;
     uint4* d_mfA = nullptr;
     size_t mfA_cap = 0;
@@ -269,7 +270,7 @@ int rt_create(int device, rt_ctx** out_ctx) {
         if ((e = hipDeviceGetAttribute(&ctx->cu_count, hipDeviceAttributeMultiprocessorCount,
                                        device)) != hipSuccess)
             break;
-        if ((e = rt_render_occupancy(&ctx->blocks_per_cu)) != hipSuccess) break;
+        if ((e = rt_render_occupancy(&ctx->blocks_per_cu, &ctx->blocks_per_cu_c)) != hipSuccess) break;
         for (Frame& f : ctx->fr) {
             if ((e = hipStreamCreateWithFlags(&f.stream, hipStreamNonBlocking)) != hipSuccess) break;
             if ((e = hipHostMalloc((void**)&f.h_segs, 18 * sizeof(unsigned long long))) != hipSuccess)
@@ -285,6 +286,7 @@ int rt_create(int device, rt_ctx** out_ctx) {
         return rc;
     }
     if (ctx->blocks_per_cu < 1) ctx->blocks_per_cu = 1;
+    if (ctx->blocks_per_cu_c < 1) ctx->blocks_per_cu_c = 1;
     *out_ctx = ctx;
     return RT_OK;
 }
@@ -626,69 +628,6 @@ static int quiesce(rt_ctx* ctx) {  // no kernel may be reading the scene while i
     return RT_OK;
 }
 
-int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n, const rt_material* materials,
-                 uint32_t m) {
-    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_set_scene: ctx is NULL");
-    if (n && !spheres) return fail(ctx, RT_ERR_INVALID_ARG, "rt_set_scene: spheres is NULL, n=%u", n);
-    if (m && !materials)
-        return fail(ctx, RT_ERR_INVALID_ARG, "rt_set_scene: materials is NULL, m=%u", m);
-    int rc = check_materials(ctx, materials, 0, m);
-    if (rc) return rc;
-    rc = check_spheres(ctx, spheres, 0, n, m);
-    if (rc) return rc;
-    const uint32_t ngroups = (n + RT_GROUP - 1) / RT_GROUP;
-    const size_t nrec = (size_t)(ngroups + 1) * RT_GROUP;
-    ctx->h_sph.assign(nrec, make_float4(0.0f, 0.0f, 0.0f, -INFINITY));
-    ctx->h_S.assign(nrec, -INFINITY);
-    ctx->h_rm.assign(n ? n : 1, make_float2(0.0f, 0.0f));
-    ctx->h_grp.assign(nrec, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-    for (uint32_t i = 0; i < n; ++i) pack_record(ctx, i, spheres[i]);
-    for (size_t g = 0; g < nrec / RT_GROUP; ++g) pack_group(ctx, g);
-    ctx->h_mats.assign(materials, materials + m);
-    rc = quiesce(ctx);
-    if (rc) return rc;
-    // From here on the device buffers change: until every upload succeeded
-    // there is no scene (a failed call leaves RT_ERR_NO_SCENE, never a
-    // half-written or freed list behind stale counts).
-    ctx->has_scene = false;
-    ctx->cull_dirty = true;
-    ctx->mf_dirty = true;
-    ctx->n = ctx->ngroups = ctx->m = 0;
-    rc = ensure(ctx, &ctx->d_sph, &ctx->sph_cap, sizeof(float4) * nrec);
-    if (rc) return rc;
-    rc = ensure(ctx, &ctx->d_grp, &ctx->grp_cap, sizeof(float4) * nrec);
-    if (rc) return rc;
-    rc = ensure(ctx, &ctx->d_sph_rm, &ctx->sph_rm_cap, sizeof(float2) * ctx->h_rm.size());
-    if (rc) return rc;
-    rc = ensure(ctx, &ctx->d_mats, &ctx->mat_cap, sizeof(rt_material) * (size_t)m);
-    if (rc) return rc;
-    HIP_TRY(ctx, hipMemcpy(ctx->d_sph, ctx->h_sph.data(), sizeof(float4) * nrec, hipMemcpyHostToDevice));
-    HIP_TRY(ctx, hipMemcpy(ctx->d_grp, ctx->h_grp.data(), sizeof(float4) * nrec, hipMemcpyHostToDevice));
-    HIP_TRY(ctx, hipMemcpy(ctx->d_sph_rm, ctx->h_rm.data(), sizeof(float2) * ctx->h_rm.size(),
-                           hipMemcpyHostToDevice));
-    if (m)
-        HIP_TRY(ctx, hipMemcpy(ctx->d_mats, materials, sizeof(rt_material) * m, hipMemcpyHostToDevice));
-    ctx->n = n;
-    ctx->ngroups = ngroups;
-    ctx->m = m;
-    ctx->scene_fast = scene_fast_ok(ctx);
-    ctx->has_scene = true;  // the culled list follows lazily (cull_ready)
-    return RT_OK;
-}
-
-// The culled list of the current scene, (re)built on the first RT_FLAG_CULL
-// call after rt_set_scene / rt_update_spheres. No kernel can be reading the
-// old one: those calls quiesce, and the first culled call after them builds
-// before it enqueues. A failed build leaves it dirty (the next call retries).
-static int cull_ready(rt_ctx* ctx) {
-    if (!ctx->cull_dirty) return RT_OK;
-    ctx->n_c = ctx->ngroups_c = ctx->nclusters_c = 0;
-    int rc = build_cull(ctx);
-    if (rc) return rc;
-    ctx->cull_dirty = false;
-    return RT_OK;
-}
-
 #ifdef RT_MFMA_FILTER
 // ---- matrix-core filter fragments (rt_dev_intersect.h intersect_world_mfma) ----
 // Row j of the A operand (sphere j): [cx_hi, cx_lo, cx_hi, cy.., cz.., 1, 1,
@@ -708,7 +647,7 @@ static int build_mfma(rt_ctx* ctx) {
     const uint32_t n = ctx->n;
     ctx->mf_ok = false;
     if (!n) return RT_OK;
-    const double kS = 1.0 - 0x1p-16 - 0x1p-14;  // 1 - m - mu' (RT_MF_MU)
+    const double kS = 1.0 - 0x1p-16 - 0x1p-16;  // 1 - m - mu' (RT_MF_MU)
     const uint32_t nblk = (n + 31) / 32;
     std::vector<uint16_t> h((size_t)nblk * 64 * 8);
     for (uint32_t j = 0; j < n; ++j) {
@@ -757,6 +696,77 @@ static int build_mfma(rt_ctx* ctx) {
 }
 #endif
 
+int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n, const rt_material* materials,
+                 uint32_t m) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_set_scene: ctx is NULL");
+    if (n && !spheres) return fail(ctx, RT_ERR_INVALID_ARG, "rt_set_scene: spheres is NULL, n=%u", n);
+    if (m && !materials)
+        return fail(ctx, RT_ERR_INVALID_ARG, "rt_set_scene: materials is NULL, m=%u", m);
+    int rc = check_materials(ctx, materials, 0, m);
+    if (rc) return rc;
+    rc = check_spheres(ctx, spheres, 0, n, m);
+    if (rc) return rc;
+    const uint32_t ngroups = (n + RT_GROUP - 1) / RT_GROUP;
+    const size_t nrec = (size_t)(ngroups + 1) * RT_GROUP;
+    ctx->h_sph.assign(nrec, make_float4(0.0f, 0.0f, 0.0f, -INFINITY));
+    ctx->h_S.assign(nrec, -INFINITY);
+    ctx->h_rm.assign(n ? n : 1, make_float2(0.0f, 0.0f));
+    ctx->h_grp.assign(nrec, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    for (uint32_t i = 0; i < n; ++i) pack_record(ctx, i, spheres[i]);
+    for (size_t g = 0; g < nrec / RT_GROUP; ++g) pack_group(ctx, g);
+    ctx->h_mats.assign(materials, materials + m);
+    rc = quiesce(ctx);
+    if (rc) return rc;
+    // From here on the device buffers change: until every upload succeeded
+    // there is no scene (a failed call leaves RT_ERR_NO_SCENE, never a
+    // half-written or freed list behind stale counts).
+    ctx->has_scene = false;
+    ctx->cull_dirty = true;
+    ctx->mf_ok = false;
+    ctx->n = ctx->ngroups = ctx->m = 0;
+    rc = ensure(ctx, &ctx->d_sph, &ctx->sph_cap, sizeof(float4) * nrec);
+    if (rc) return rc;
+    rc = ensure(ctx, &ctx->d_grp, &ctx->grp_cap, sizeof(float4) * nrec);
+    if (rc) return rc;
+    rc = ensure(ctx, &ctx->d_sph_rm, &ctx->sph_rm_cap, sizeof(float2) * ctx->h_rm.size());
+    if (rc) return rc;
+    rc = ensure(ctx, &ctx->d_mats, &ctx->mat_cap, sizeof(rt_material) * (size_t)m);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpy(ctx->d_sph, ctx->h_sph.data(), sizeof(float4) * nrec, hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(ctx->d_grp, ctx->h_grp.data(), sizeof(float4) * nrec, hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(ctx->d_sph_rm, ctx->h_rm.data(), sizeof(float2) * ctx->h_rm.size(),
+                           hipMemcpyHostToDevice));
+    if (m)
+        HIP_TRY(ctx, hipMemcpy(ctx->d_mats, materials, sizeof(rt_material) * m, hipMemcpyHostToDevice));
+    ctx->n = n;
+    ctx->ngroups = ngroups;
+    ctx->m = m;
+    ctx->scene_fast = scene_fast_ok(ctx);
+#ifdef RT_MFMA_FILTER
+    rc = build_mfma(ctx);  // with the scene, so a reserved render allocates nothing
+    if (rc) {
+        ctx->n = ctx->ngroups = ctx->m = 0;
+        return rc;
+    }
+#endif
+    ctx->has_scene = true;  // the culled list follows lazily (cull_ready)
+    return RT_OK;
+}
+
+// The culled list of the current scene, (re)built on the first RT_FLAG_CULL
+// call after rt_set_scene / rt_update_spheres. No kernel can be reading the
+// old one: those calls quiesce, and the first culled call after them builds
+// before it enqueues. A failed build leaves it dirty (the next call retries).
+static int cull_ready(rt_ctx* ctx) {
+    if (!ctx->cull_dirty) return RT_OK;
+    ctx->n_c = ctx->ngroups_c = ctx->nclusters_c = 0;
+    int rc = build_cull(ctx);
+    if (rc) return rc;
+    ctx->cull_dirty = false;
+    return RT_OK;
+}
+
+
 int rt_update_spheres(rt_ctx* ctx, uint32_t first, const rt_sphere* spheres, uint32_t count) {
     if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_update_spheres: ctx is NULL");
     if (!ctx->has_scene) return fail(ctx, RT_ERR_NO_SCENE, "rt_update_spheres before rt_set_scene");
@@ -780,7 +790,10 @@ int rt_update_spheres(rt_ctx* ctx, uint32_t first, const rt_sphere* spheres, uin
                            sizeof(float4) * RT_GROUP * (g1 - g0), hipMemcpyHostToDevice));
     ctx->scene_fast = scene_fast_ok(ctx);
     ctx->cull_dirty = true;  // the permutation and bounds follow at the next culled call
-    ctx->mf_dirty = true;
+#ifdef RT_MFMA_FILTER
+    rc = build_mfma(ctx);
+    if (rc) return rc;
+#endif
     return RT_OK;
 }
 
@@ -854,7 +867,8 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     // finished when the queue runs dry, and an item taken in the tail leaves
     // at most one short path per lane to drain. In samples per pixel:
     const Tuning& tn = ctx->tune;
-    const uint64_t lanes = (uint64_t)ctx->cu_count * ctx->blocks_per_cu * RT_BLOCK_THREADS;
+    const int bpc = (p.flags & RT_FLAG_CULL) ? ctx->blocks_per_cu_c : ctx->blocks_per_cu;
+    const uint64_t lanes = (uint64_t)ctx->cu_count * bpc * RT_BLOCK_THREADS;
     bool tail_on = tn.tail_split;
     const double* ta = tn.tail;
     auto per_px = [&](double a, uint64_t mult) -> uint64_t {
@@ -976,16 +990,9 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     K_.scene_fast = ctx->scene_fast && tn.fast_exact ? 1u : 0u;
     K_.flags = p.flags;
 #ifdef RT_MFMA_FILTER
-    if (!cull) {
-        if (ctx->mf_dirty) {
-            int rc = build_mfma(ctx);
-            if (rc) return rc;
-            ctx->mf_dirty = false;
-        }
-        if (ctx->mf_ok) {
-            K_.mfA = ctx->d_mfA;
-            K_.mf_nblk = ctx->mf_nblk;
-        }
+    if (!cull && ctx->mf_ok) {
+        K_.mfA = ctx->d_mfA;
+        K_.mf_nblk = ctx->mf_nblk;
     }
 #endif
     std::memcpy(K_.T, cam->transform, sizeof(K_.T));
@@ -1038,8 +1045,7 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     HIP_TRY_Q(hipMemsetAsync(f.d_counters, 0, words_pad * sizeof(uint32_t), stream));
     // wg_per_cu < occupancy: fewer co-resident waves per SIMD (A/B)
     const uint32_t wg_per_cu = std::min<uint32_t>(
-        ctx->tune.wg_per_cu ? ctx->tune.wg_per_cu : (uint32_t)ctx->blocks_per_cu,
-        (uint32_t)ctx->blocks_per_cu);
+        ctx->tune.wg_per_cu ? ctx->tune.wg_per_cu : (uint32_t)bpc, (uint32_t)bpc);
     const uint32_t grid_full = (uint32_t)(ctx->cu_count * (wg_per_cu ? wg_per_cu : 1));
     if (npix) HIP_TRY_Q(rt_launch_primary(&K_, f.d_pd, stream));
     for (size_t i = 0; i < passes.size(); ++i) {

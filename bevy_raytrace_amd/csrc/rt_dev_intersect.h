@@ -614,7 +614,20 @@ __device__ __forceinline__ uint32_t lanemask_lt_count(uint64_t m) {
 // any order, with the (t, index) tie-break (exact_body LEX).
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef float f16x __attribute__((ext_vector_type(16)));
-#define RT_MF_MU 0x1p-14f
+// Margins (the VALU filter's m; mu' and an absolute term for the split):
+// with x = hi + lo + e, |e| <= 2^-22|x| + 2^-25 (f16 11-bit significands, lo
+// possibly subnormal), each 3-product term is within 3 * 2^-22|x||y| +
+// 2^-25(|x| + |y|) of x*y, and the f32 sum of the 11 exact products within
+// 10 * 2^-24 of the sum of their magnitudes. So |hb' - hb~| <= 2^-19.5 (|o| +
+// |c|) + 2^-23 (1 + |c|) and |v' - v~| <= 2^-18.6 |o||c| + 2^-20.6 (r^2 + |c|^2)
+// + 2^-24 (|o| + |c|), hence with |hb~| <= (1 + 2^-20)(|o| + |c|) and the last
+// fma's rounding: |H' - H~| <= 1.0 * 2^-17 (|o|^2 + |c|^2) + 2^-20.3 r^2 +
+// 2^-21. The ray constants are the VALU filter's (their error, <= 25 * 2^-24
+// (|o|^2 + |c|^2), is in its mu = 2^-17); mu' = 2^-16 covers both terms in
+// |o|^2 + |c|^2, the m margin's slack (2^-16 - 35 * 2^-24) the r^2 term, and
+// T' carries 2^-20 for the absolute one.
+#define RT_MF_MU 0x1p-16f
+#define RT_MF_ABS 0x1p-20f
 #define RT_MF_CAP 8  // queue entries per lane and half (LDS)
 
 __device__ __forceinline__ uint32_t bperm(uint32_t src_lane, uint32_t v) {
@@ -647,10 +660,12 @@ __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, ui
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     const uint32_t lane = __lane_id();
     const uint32_t t = lane >> 5, j = lane & 31u;
-    // the two lanes holding this ray's column: j (rows 4h, h = 0) and j + 32
-    const uint32_t x0 = bperm(j, cnt0), x1 = bperm(j, cnt1);
-    const uint32_t y0 = bperm(j + 32u, cnt0), y1 = bperm(j + 32u, cnt1);
-    const uint32_t na = t ? x1 : x0, nb = t ? y1 : y0;
+    // the two lanes holding this ray's column: j (rows 4h, h = 0) and j + 32;
+    // v_permlane32_swap(x, x) gives (lane < 32 ? x[l] : x[l - 32], lane < 32 ?
+    // x[l + 32] : x[l]) (profiles/r02_permlane32_swap.log)
+    const auto c0 = __builtin_amdgcn_permlane32_swap(cnt0, cnt0, false, false);
+    const auto c1 = __builtin_amdgcn_permlane32_swap(cnt1, cnt1, false, false);
+    const uint32_t na = t ? c1[0] : c0[0], nb = t ? c1[1] : c0[1];
     const uint32_t* q = cq + t * (RT_MF_CAP * 64u);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     for (uint32_t side = 0; side < 2; ++side) {
@@ -693,7 +708,7 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
     const float oo = __builtin_fmaf(o.z, o.z, __builtin_fmaf(o.y, o.y, o.x * o.x));
     const float k1 = __builtin_fmaf(dnz, o.z, __builtin_fmaf(dny, o.y, dnx * o.x));
     const float two = 2.0f * (1.0f - m_);
-    const float T = live ? (1.0f - m_ - RT_MF_MU) * oo : INFINITY;
+    const float T = live ? (1.0f - m_ - RT_MF_MU) * oo - RT_MF_ABS : INFINITY;
     float xh, xl, yh, yl, zh, zl, kh, kl;
     split_h(-dnx, xh, xl);
     split_h(-dny, yh, yl);
@@ -713,13 +728,14 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
     const uint32_t vh0 = pack2h(rl, 0.0f), vh1 = pack2h(0.0f, 1.0f), vh2 = pack2h(1.0f, 0.0f),
                    vh3 = 0u;
     // B fragments: half 0 = rays 0..31 (lane l: column l & 31, k 8h..8h+7),
-    // half 1 = rays 32..63; a lane's own ray gives its K half, the partner
-    // (lane ^ 32) the other
-    const uint32_t partner = lane ^ 32u;
+    // half 1 = rays 32..63. v_permlane32_swap(lo, hi) swaps lo's upper 32
+    // lanes with hi's lower 32 (profiles/r02_permlane32_swap.log): its first
+    // result is half 0's fragment (lanes < 32 their own K 0..7, lanes >= 32
+    // K 8..15 of ray l - 32), its second half 1's.
     auto frag = [&](uint32_t lo, uint32_t hi, uint32_t& f0, uint32_t& f1) {
-        const uint32_t recv = bperm(partner, h ? lo : hi);
-        f0 = h ? recv : lo;
-        f1 = h ? hi : recv;
+        const auto r = __builtin_amdgcn_permlane32_swap(lo, hi, false, false);
+        f0 = r[0];
+        f1 = r[1];
     };
     uint32_t u00, u01, u02, u03, u10, u11, u12, u13, v00, v01, v02, v03, v10, v11, v12, v13;
     frag(ul0, uh0, u00, u10);
@@ -738,8 +754,8 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
     };
     const h8v Bu0 = as_h8(u00, u01, u02, u03), Bu1 = as_h8(u10, u11, u12, u13);
     const h8v Bv0 = as_h8(v00, v01, v02, v03), Bv1 = as_h8(v10, v11, v12, v13);
-    const float Tp = __uint_as_float(bperm(partner, __float_as_uint(T)));
-    const float T0 = h ? Tp : T, T1 = h ? T : Tp;
+    const auto Tw = __builtin_amdgcn_permlane32_swap(__float_as_uint(T), __float_as_uint(T), false, false);
+    const float T0 = __uint_as_float(Tw[0]), T1 = __uint_as_float(Tw[1]);  // of ray l & 31, 32 + (l & 31)
 
     float best_t = VERY_FAR;
     int best_i = -1;

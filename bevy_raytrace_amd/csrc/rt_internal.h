@@ -21,6 +21,9 @@
 #ifndef RT_MIN_WAVES_PER_SIMD
 #define RT_MIN_WAVES_PER_SIMD 6
 #endif
+#ifndef RT_MIN_WAVES_PER_SIMD_CULL
+#define RT_MIN_WAVES_PER_SIMD_CULL 6
+#endif
 
 // Unsigned 32-bit division by a run-time invariant d >= 1 as a multiply-high
 // (Granlund & Montgomery 1994, Fig. 4.1): exact for every 32-bit n.
@@ -121,6 +124,6 @@ hipError_t rt_launch_intersect(const float4* grp, const float4* sph, uint32_t ng
                                uint32_t scene_fast, const float* rays, uint32_t n, int* out_i, float* out_t,
                                const float4* bnd, const uint32_t* perm, uint32_t nclusters,
                                hipStream_t stream);
-hipError_t rt_render_occupancy(int* blocks_per_cu);
+hipError_t rt_render_occupancy(int* blocks_per_cu, int* blocks_per_cu_cull);
 hipError_t rt_launch_primary(const KParams* P, float4* pd, hipStream_t stream);
 }

@@ -400,7 +400,7 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
     render_body<false>(P, grp, sph, sph_rm, mats, tab, block_sums, work_counter, seg_counter, dbg);
 }
 
-__global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_render_cull_kernel(
+__global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD_CULL) void rt_render_cull_kernel(
     KParams P, const float4* grp, const float4* __restrict__ sph,
     const float2* __restrict__ sph_rm, const rt_material* __restrict__ mats,
     const PixelEntry* __restrict__ tab, float4* __restrict__ block_sums,
@@ -689,8 +689,13 @@ int rt_debug_math(int mode, const float* in_device, uint32_t n, float* out_devic
     return hipDeviceSynchronize() == hipSuccess ? 0 : -3;
 }
 
-hipError_t rt_render_occupancy(int* blocks_per_cu) {
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_render_kernel,
+// resident workgroups per CU of the brute-force and the culled kernel (their
+// register and LDS footprints differ: the matrix-core filter's tiles)
+hipError_t rt_render_occupancy(int* blocks_per_cu, int* blocks_per_cu_cull) {
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_render_kernel,
+                                                                RT_BLOCK_THREADS, 0);
+    if (e != hipSuccess) return e;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu_cull, rt_render_cull_kernel,
                                                         RT_BLOCK_THREADS, 0);
 }
 
