@@ -667,6 +667,9 @@ __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, ui
     const auto c1 = __builtin_amdgcn_permlane32_swap(cnt1, cnt1, false, false);
     const uint32_t na = t ? c1[0] : c0[0], nb = t ? c1[1] : c0[1];
     const uint32_t* q = cq + t * (RT_MF_CAP * 64u);
+#ifdef RT_PROFILE
+    uint32_t ecnt[2] = {0, 0};  // (exact-test counts are not reported for this path)
+#endif
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     for (uint32_t side = 0; side < 2; ++side) {
         const uint32_t n = side ? nb : na, col = side ? j + 32u : j;
@@ -678,7 +681,7 @@ __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, ui
                 const uint32_t b = __builtin_ctz(m);
                 m &= m - 1;
                 exact_body<FAST, false, true>(sph[base + b], (int)(base + b), o, d, a, ya, best_t,
-                                              best_i, nullptr);
+                                              best_i, nullptr EXACT_PASS);
             }
         }
     }
@@ -690,7 +693,11 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
                                                     const float4* __restrict__ sph,
                                                     uint32_t scene_fast, v3 o, v3 d, bool live,
                                                     uint64_t live_mask, float& t_out,
-                                                    uint32_t* cq) {
+                                                    uint32_t* cq
+#ifdef RT_PROFILE
+                                                    , Prof& prof_
+#endif
+                                                    ) {
     if (!live) {
         o = mk(0.0f, 0.0f, 0.0f);
         d = mk(0.0f, 0.0f, 1.0f);
@@ -817,10 +824,12 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
         a4 = an;
 #endif
     }
+    PROF_MARK(1);
     if (fast)
         mfma_drain<true>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i);
     else
         mfma_drain<false>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i);
+    PROF_MARK(2);
     t_out = best_t;
     return best_i;
 }

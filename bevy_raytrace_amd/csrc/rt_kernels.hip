@@ -276,7 +276,11 @@ __device__ __forceinline__ void render_body(
 #ifdef RT_MFMA_FILTER
         } else if (!CULL && P.mfA && mfma_wave_ok(st.o, has_item)) {  // the whole wave
             const int h2 = intersect_world_mfma(P.mfA, P.mf_nblk, sph, P.scene_fast, st.o, st.d,
-                                                has_item, live, t, cqm);
+                                                has_item, live, t, cqm
+#ifdef RT_PROFILE
+                                                , prof_
+#endif
+                                                );
             if (has_item) hi = h2;
             else t = VERY_FAR;
 #endif
