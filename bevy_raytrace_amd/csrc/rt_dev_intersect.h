@@ -789,8 +789,11 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
 #endif
         h8v A;
         __builtin_memcpy(&A, &a4, 16);
-#pragma nounroll
+        // the two halves unrolled (no per-tile operand selects) but kept apart
+        // (sched_barrier): one tile's 32 result registers live at a time
+#pragma unroll
         for (uint32_t t = 0; t < 2; ++t) {
+            if (t) __builtin_amdgcn_sched_barrier(0);
             const f16x U = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, t ? Bu1 : Bu0, zero, 0, 0, 0);
             const f16x V = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, t ? Bv1 : Bv0, zero, 0, 0, 0);
             const float Tt = t ? T1 : T0;
