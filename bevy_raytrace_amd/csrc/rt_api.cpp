@@ -990,7 +990,7 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     K_.scene_fast = ctx->scene_fast && tn.fast_exact ? 1u : 0u;
     K_.flags = p.flags;
 #ifdef RT_MFMA_FILTER
-    if (!cull && ctx->mf_ok) {
+    if (!cull && ctx->mf_ok && !(p.flags & RT_FLAG_VALU_FILTER)) {
         K_.mfA = ctx->d_mfA;
         K_.mf_nblk = ctx->mf_nblk;
     }
@@ -1334,6 +1334,16 @@ int rt_intersect_ex(rt_ctx* ctx, const float* rays, uint32_t n, uint32_t flags, 
     HIP_TRY(ctx, hipMalloc(&buf, rb + 2 * ob));
     char* b = (char*)buf;
     hipError_t e = hipMemcpyAsync(b, rays, rb, hipMemcpyHostToDevice, ctx->stream);
+    // the brute-force walk takes the render's filter: the matrix-core tiles
+    // when the scene fits them (unless RT_FLAG_VALU_FILTER)
+    const uint4* mfA = nullptr;
+    uint32_t mf_nblk = 0;
+#ifdef RT_MFMA_FILTER
+    if (!cull && ctx->mf_ok && !(flags & RT_FLAG_VALU_FILTER)) {
+        mfA = ctx->d_mfA;
+        mf_nblk = ctx->mf_nblk;
+    }
+#endif
     if (e == hipSuccess)
     {
         e = rt_launch_intersect(cull ? ctx->d_grp_c : ctx->d_grp, cull ? ctx->d_sph_c : ctx->d_sph,
@@ -1341,7 +1351,7 @@ int rt_intersect_ex(rt_ctx* ctx, const float* rays, uint32_t n, uint32_t flags, 
                                 ctx->scene_fast && ctx->tune.fast_exact ? 1u : 0u,
                                 (const float*)b, n, (int*)(b + rb), (float*)(b + rb + ob),
                                 cull ? ctx->d_bnd_c : nullptr, cull ? ctx->d_perm_c : nullptr,
-                                cull ? ctx->nclusters_c : 0u, ctx->stream);
+                                cull ? ctx->nclusters_c : 0u, mfA, mf_nblk, ctx->stream);
     }
     if (e == hipSuccess)
         e = hipMemcpyAsync(hit_index, b + rb, ob, hipMemcpyDeviceToHost, ctx->stream);

@@ -183,23 +183,26 @@ __device__ __forceinline__ f2 filter2(f2 cx, f2 cy, f2 cz, f2 S, const RayF& r) 
 }
 
 // The same filter for a whole group of 8 spheres in hand-scheduled VOP3P:
-// the ray constants live ONCE in 4 VGPR pairs (r0 = (-dnx, -dny),
-// r1 = (-dnz, k1), r2 = (o2x, o2y), r3 = (o2z, T)) and op_sel / op_sel_hi
-// broadcast one half to both packed lanes -- the compiler's form needs every
-// constant duplicated in a pair (7 VGPRs more at the 80-VGPR occupancy limit).
-// The four pair chains are interleaved, so dependent ops are 4 apart (no
+// the four pair chains are interleaved, so dependent ops are 4 apart (no
 // wait states, and a lone wave in the queue tail issues back to back). Op
-// order per pair is exactly filter2's.
+// order per pair is exactly filter2's. Every ray constant is held as a
+// duplicated VGPR pair: no op_sel / op_sel_hi broadcast of one half of a pair.
+// The broadcast form (4 pairs, 7 VGPRs fewer) gave wrong H values, on a few
+// waves of some launches only, in a kernel whose other waves ran the
+// matrix-core filter on the same SIMDs (tools/isect_diag.py: ~10-100 of
+// 400,000 adversarial rays per launch, every one in a VALU-walk wave; the
+// same asm without op_sel, or the compiler's filter2, exact over 8 launches;
+// DESIGN.md §4.7).
 struct RayP {
-    f2 r0, r1, r2, r3;
+    f2 dx, dy, dz, k1, ox, oy, oz;  // (-dn, k1, o2) duplicated in both halves
+    float T;
 };
 
 __device__ __forceinline__ RayP ray_pack(const RayF& r) {
     RayP p;
-    p.r0 = f2{r.dx.x, r.dy.x};
-    p.r1 = f2{r.dz.x, r.k1.x};
-    p.r2 = f2{r.o2x.x, r.o2y.x};
-    p.r3 = f2{r.o2z.x, r.T};
+    p.dx = r.dx; p.dy = r.dy; p.dz = r.dz; p.k1 = r.k1;
+    p.ox = r.o2x; p.oy = r.o2y; p.oz = r.o2z;
+    p.T = r.T;
     return p;
 }
 
@@ -209,35 +212,35 @@ __device__ __forceinline__ void filter8(const RayP& R, f2 cxa, f2 cxb, f2 cxc, f
                                         f2& hd, float& hmax) {
     asm volatile(
         // hb = k1 + (-dnx) cx + (-dny) cy + (-dnz) cz
-        "v_pk_fma_f32 %[ha], %[r0], %[cxa], %[r1] op_sel:[0,0,1] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[hb], %[r0], %[cxb], %[r1] op_sel:[0,0,1] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[hc], %[r0], %[cxc], %[r1] op_sel:[0,0,1] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[hd], %[r0], %[cxd], %[r1] op_sel:[0,0,1] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[ha], %[r0], %[cya], %[ha] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
-        "v_pk_fma_f32 %[hb], %[r0], %[cyb], %[hb] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
-        "v_pk_fma_f32 %[hc], %[r0], %[cyc], %[hc] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
-        "v_pk_fma_f32 %[hd], %[r0], %[cyd], %[hd] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
-        "v_pk_fma_f32 %[ha], %[r1], %[cza], %[ha] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[hb], %[r1], %[czb], %[hb] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[hc], %[r1], %[czc], %[hc] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[hd], %[r1], %[czd], %[hd] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[ha], %[dx], %[cxa], %[k1]\n\t"
+        "v_pk_fma_f32 %[hb], %[dx], %[cxb], %[k1]\n\t"
+        "v_pk_fma_f32 %[hc], %[dx], %[cxc], %[k1]\n\t"
+        "v_pk_fma_f32 %[hd], %[dx], %[cxd], %[k1]\n\t"
+        "v_pk_fma_f32 %[ha], %[dy], %[cya], %[ha]\n\t"
+        "v_pk_fma_f32 %[hb], %[dy], %[cyb], %[hb]\n\t"
+        "v_pk_fma_f32 %[hc], %[dy], %[cyc], %[hc]\n\t"
+        "v_pk_fma_f32 %[hd], %[dy], %[cyd], %[hd]\n\t"
+        "v_pk_fma_f32 %[ha], %[dz], %[cza], %[ha]\n\t"
+        "v_pk_fma_f32 %[hb], %[dz], %[czb], %[hb]\n\t"
+        "v_pk_fma_f32 %[hc], %[dz], %[czc], %[hc]\n\t"
+        "v_pk_fma_f32 %[hd], %[dz], %[czd], %[hd]\n\t"
         // H = hb^2 + S + o2z cz + o2y cy + o2x cx
         "v_pk_fma_f32 %[ha], %[ha], %[ha], %[sa]\n\t"
         "v_pk_fma_f32 %[hb], %[hb], %[hb], %[sb]\n\t"
         "v_pk_fma_f32 %[hc], %[hc], %[hc], %[sc]\n\t"
         "v_pk_fma_f32 %[hd], %[hd], %[hd], %[sd]\n\t"
-        "v_pk_fma_f32 %[ha], %[r3], %[cza], %[ha] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[hb], %[r3], %[czb], %[hb] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[hc], %[r3], %[czc], %[hc] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[hd], %[r3], %[czd], %[hd] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[ha], %[r2], %[cya], %[ha] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
-        "v_pk_fma_f32 %[hb], %[r2], %[cyb], %[hb] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
-        "v_pk_fma_f32 %[hc], %[r2], %[cyc], %[hc] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
-        "v_pk_fma_f32 %[hd], %[r2], %[cyd], %[hd] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
-        "v_pk_fma_f32 %[ha], %[r2], %[cxa], %[ha] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[hb], %[r2], %[cxb], %[hb] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[hc], %[r2], %[cxc], %[hc] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
-        "v_pk_fma_f32 %[hd], %[r2], %[cxd], %[hd] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %[ha], %[oz], %[cza], %[ha]\n\t"
+        "v_pk_fma_f32 %[hb], %[oz], %[czb], %[hb]\n\t"
+        "v_pk_fma_f32 %[hc], %[oz], %[czc], %[hc]\n\t"
+        "v_pk_fma_f32 %[hd], %[oz], %[czd], %[hd]\n\t"
+        "v_pk_fma_f32 %[ha], %[oy], %[cya], %[ha]\n\t"
+        "v_pk_fma_f32 %[hb], %[oy], %[cyb], %[hb]\n\t"
+        "v_pk_fma_f32 %[hc], %[oy], %[cyc], %[hc]\n\t"
+        "v_pk_fma_f32 %[hd], %[oy], %[cyd], %[hd]\n\t"
+        "v_pk_fma_f32 %[ha], %[ox], %[cxa], %[ha]\n\t"
+        "v_pk_fma_f32 %[hb], %[ox], %[cxb], %[hb]\n\t"
+        "v_pk_fma_f32 %[hc], %[ox], %[cxc], %[hc]\n\t"
+        "v_pk_fma_f32 %[hd], %[ox], %[cxd], %[hd]\n\t"
         // group max of the 8 H (v_max3 drops a quiet-NaN operand, as fmaxf)
         "v_max3_f32 %[hm], v40, v41, v42\n\t"
         "v_max3_f32 %[hm], %[hm], v43, v44\n\t"
@@ -245,10 +248,11 @@ __device__ __forceinline__ void filter8(const RayP& R, f2 cxa, f2 cxb, f2 cxc, f
         "v_max_f32 %[hm], %[hm], v47"
         : [ha] "={v[40:41]}"(ha), [hb] "={v[42:43]}"(hb), [hc] "={v[44:45]}"(hc),
           [hd] "={v[46:47]}"(hd), [hm] "=&v"(hmax)
-        : [r0] "v"(R.r0), [r1] "v"(R.r1), [r2] "v"(R.r2), [r3] "v"(R.r3), [cxa] "s"(cxa),
-          [cxb] "s"(cxb), [cxc] "s"(cxc), [cxd] "s"(cxd), [cya] "s"(cya), [cyb] "s"(cyb),
-          [cyc] "s"(cyc), [cyd] "s"(cyd), [cza] "s"(cza), [czb] "s"(czb), [czc] "s"(czc),
-          [czd] "s"(czd), [sa] "s"(sa), [sb] "s"(sb), [sc] "s"(sc), [sd] "s"(sd));
+        : [dx] "v"(R.dx), [dy] "v"(R.dy), [dz] "v"(R.dz), [k1] "v"(R.k1), [ox] "v"(R.ox),
+          [oy] "v"(R.oy), [oz] "v"(R.oz), [cxa] "s"(cxa), [cxb] "s"(cxb), [cxc] "s"(cxc),
+          [cxd] "s"(cxd), [cya] "s"(cya), [cyb] "s"(cyb), [cyc] "s"(cyc), [cyd] "s"(cyd),
+          [cza] "s"(cza), [czb] "s"(czb), [czc] "s"(czc), [czd] "s"(czd), [sa] "s"(sa),
+          [sb] "s"(sb), [sc] "s"(sc), [sd] "s"(sd));
 }
 
 __device__ __forceinline__ uint32_t ge(float h, float t) { return h >= t ? 1u : 0u; }
@@ -361,7 +365,7 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
     const bool fast = ray_fast(scene_fast, o, a);
 #if defined(RT_ASM_FILTER) && defined(__HIP_DEVICE_COMPILE__)
     const RayP RP = ray_pack(ray_filter_consts(o, d));
-    const float RT_T = RP.r3.y;
+    const float RT_T = RP.T;
 #else
     const RayF R = ray_filter_consts(o, d);
     const float RT_T = R.T;

@@ -123,7 +123,7 @@ hipError_t rt_launch_assemble(const float4* gathered, uint32_t max_rows, float4*
 hipError_t rt_launch_intersect(const float4* grp, const float4* sph, uint32_t ngroups,
                                uint32_t scene_fast, const float* rays, uint32_t n, int* out_i, float* out_t,
                                const float4* bnd, const uint32_t* perm, uint32_t nclusters,
-                               hipStream_t stream);
+                               const uint4* mfA, uint32_t mf_nblk, hipStream_t stream);
 hipError_t rt_render_occupancy(int* blocks_per_cu, int* blocks_per_cu_cull);
 hipError_t rt_launch_primary(const KParams* P, float4* pd, hipStream_t stream);
 }

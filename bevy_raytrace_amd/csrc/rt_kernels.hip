@@ -469,6 +469,61 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_cull_kernel(
     intersect_body<true>(grp, sph, ngroups, scene_fast, rays, n, out_i, out_t, bnd, perm, nclusters);
 }
 
+#ifdef RT_MFMA_FILTER
+// The same batch query through the render's matrix-core filter (rt_render_kernel
+// takes it for every wave whose rays fit the split's range): the whole wave
+// runs the tiles, lanes past n trace a dummy ray that never has a candidate; a
+// wave with a ray outside the range takes the VALU filter, as in the render.
+__global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_mfma_kernel(
+    const uint4* __restrict__ mfA, uint32_t nblk, const float4* __restrict__ grp,
+    const float4* __restrict__ sph, uint32_t ngroups, uint32_t scene_fast,
+    const float* __restrict__ rays, uint32_t n, int* __restrict__ out_i, float* __restrict__ out_t) {
+    __shared__ uint32_t s_cq[RT_BLOCK_THREADS * RT_CQ_CAP];
+    __shared__ uint32_t s_cqm[(RT_BLOCK_THREADS / 64) * 2 * RT_MF_CAP * 64];
+    const uint32_t wave = threadIdx.x / 64u;
+    PROF_DECL
+    PROF_START();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = i < n;
+    const uint64_t lm = rt_ballot(live);
+    if (lm == 0) return;  // wave-uniform: the whole wave is past n
+    v3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
+    if (live) {
+        const float* r = rays + (size_t)i * 6;
+        o = mk(r[0], r[1], r[2]);
+        d = mk(r[3], r[4], r[5]);
+    }
+    float t = VERY_FAR;
+    int hi = -1;
+#ifdef RT_ISECT_FORCE_VALU  // diagnostic build: the VALU walk for every wave
+    if (false) {
+#else
+    if (mfma_wave_ok(o, live)) {
+#endif
+        hi = intersect_world_mfma(mfA, nblk, sph, scene_fast, o, d, live, lm, t,
+                                  s_cqm + wave * (2u * RT_MF_CAP * 64u)
+#ifdef RT_PROFILE
+                                  , prof_
+#endif
+                                  );
+    } else if (live) {
+        hi = intersect_world<false>(grp, sph, ngroups, scene_fast, o, d, t,
+                                    s_cq + wave * (64u * RT_CQ_CAP),
+#ifdef RT_PROFILE
+                                    prof_,
+#endif
+                                    nullptr, nullptr, 0u);
+    }
+#ifdef RT_ISECT_PATHTAG  // diagnostic build: bit 24 of the index marks the matrix-core walk
+    if (mfma_wave_ok(o, live)) hi += 1 << 24;
+#endif
+    if (live) {
+        out_i[i] = hi;
+        out_t[i] = t;
+    }
+}
+#endif
+
 // Fold one frame's results into acc (block order) and, on the frame's last
 // pass, write out = acc / spp with alpha 1 (collect.wgsl:115-125). One thread
 // per pixel of the processing order k (-> image pixel p = order_to_pixel).
@@ -633,8 +688,19 @@ hipError_t rt_launch_assemble(const float4* gathered, uint32_t max_rows, float4*
 hipError_t rt_launch_intersect(const float4* grp, const float4* sph, uint32_t ngroups,
                                uint32_t scene_fast, const float* rays, uint32_t n, int* out_i,
                                float* out_t, const float4* bnd, const uint32_t* perm,
-                               uint32_t nclusters, hipStream_t stream) {
+                               uint32_t nclusters, const uint4* mfA, uint32_t mf_nblk,
+                               hipStream_t stream) {
     const uint32_t T = RT_BLOCK_THREADS;
+#ifdef RT_MFMA_FILTER
+    if (mfA && !bnd) {
+        hipLaunchKernelGGL(rt_intersect_mfma_kernel, dim3((n + T - 1) / T), dim3(T), 0, stream, mfA,
+                           mf_nblk, grp, sph, ngroups, scene_fast, rays, n, out_i, out_t);
+        return hipGetLastError();
+    }
+#else
+    (void)mfA;
+    (void)mf_nblk;
+#endif
     if (bnd)
         hipLaunchKernelGGL(rt_intersect_cull_kernel, dim3((n + T - 1) / T), dim3(T), 0, stream, grp,
                            sph, ngroups, scene_fast, rays, n, out_i, out_t, bnd, perm, nclusters);

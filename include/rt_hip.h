@@ -157,6 +157,14 @@ typedef struct rt_params {
  * intersect.wgsl:133-143 (ties still go to the lower sphere index); only the
  * work differs, so it is opt-in like the other non-reference modes. */
 #define RT_FLAG_CULL      0x8u
+/* RT_FLAG_VALU_FILTER: run the brute-force walk's conservative sphere filter
+ * as packed fp32 FMAs on the vector ALUs instead of the default f16 hi/lo
+ * tiles on the matrix cores (the matrix-core filter is used
+ * whenever the scene fits its range). Both filters only decide which spheres
+ * get the reference's exact test, so hits, segment counts and images are
+ * identical; the flag exists for A/B timing and for checking one filter
+ * against the other (rt_render*, rt_intersect_ex). */
+#define RT_FLAG_VALU_FILTER 0x10u
 #define RT_JITTER_HASH_MUL 0x9E3779B1u
 #define RT_LENS_HASH_MUL   0x85EBCA77u
 

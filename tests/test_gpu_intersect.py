@@ -1,7 +1,10 @@
 """Intersection parity: the GPU's filtered closest-hit loop (rt_intersect ->
 intersect_world) against the oracle's brute-force reference loop
 (intersect.wgsl:94-143), bit-exact index and t, on adversarial rays aimed at
-the filter's decision boundary (tests/raygen.py)."""
+the filter's decision boundary (tests/raygen.py). Each walk is checked: the
+default brute-force walk (the matrix-core filter whenever the scene and the
+wave's rays fit its f16 split, else the packed VALU filter), the VALU filter
+forced (RT_FLAG_VALU_FILTER) and the culled list (RT_FLAG_CULL)."""
 import glob
 import os
 import zlib
@@ -10,7 +13,7 @@ import numpy as np
 import pytest
 
 from bevy_raytrace_amd import scene
-from bevy_raytrace_amd.abi import RT_FLAG_CULL
+from bevy_raytrace_amd.abi import RT_FLAG_CULL, RT_FLAG_VALU_FILTER
 from oracle import oracle as O
 from raygen import adversarial_rays
 
@@ -50,10 +53,13 @@ SCENES = {  # name -> (spheres, translation applied to spheres and rays)
 }
 
 
-@pytest.mark.parametrize("cull", [False, True], ids=["brute", "cull"])
+WALKS = {"brute": 0, "brute_valu": RT_FLAG_VALU_FILTER, "cull": RT_FLAG_CULL}
+
+
+@pytest.mark.parametrize("walk", sorted(WALKS))
 @pytest.mark.parametrize("fast", [True, False], ids=["short_math", "ieee"])
 @pytest.mark.parametrize("name", sorted(SCENES))
-def test_intersect_bit_exact(renderer, name, fast, cull):
+def test_intersect_bit_exact(renderer, name, fast, walk):
     """fast=False forces the IEEE exact tests (knob fast_exact=0): both forms
     must give the oracle's bits."""
     if not fast:
@@ -68,7 +74,7 @@ def test_intersect_bit_exact(renderer, name, fast, cull):
         sp["center"] += np.asarray(off, np.float32)
         rays[:, :3] += np.asarray(off, np.float32)
     renderer.set_scene(sp, mt)
-    gi, gt = renderer.intersect(rays, flags=RT_FLAG_CULL if cull else 0)
+    gi, gt = renderer.intersect(rays, flags=WALKS[walk])
     ci, ct = O.intersect_batch(sp, rays)
     bad = np.nonzero((gi != ci) | (gt.view(np.uint32) != ct.view(np.uint32)))[0]
     assert bad.size == 0, f"{bad.size} rays differ, e.g. {bad[:5].tolist()}: gpu {gi[bad[:5]]} {gt[bad[:5]]} cpu {ci[bad[:5]]} {ct[bad[:5]]}"
@@ -93,7 +99,7 @@ def test_cull_tie_goes_to_lower_index(renderer):
     rays = np.hstack([o, d]).astype(np.float32)
     renderer.set_scene(sp, mt)
     ci, ct = O.intersect_batch(sp, rays)
-    for flags in (0, RT_FLAG_CULL):
+    for flags in WALKS.values():
         gi, gt = renderer.intersect(rays, flags=flags)
         assert np.array_equal(gi, ci) and np.array_equal(gt.view(np.uint32), ct.view(np.uint32))
     # the ties really occur: with the order reversed the oracle picks sphere 1
@@ -105,7 +111,7 @@ WGSL_ISECT = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__fil
                                            "wgsl_isect_*.npz")))
 
 
-@pytest.mark.parametrize("flags", [0, RT_FLAG_CULL], ids=["brute", "cull"])
+@pytest.mark.parametrize("flags", list(WALKS.values()), ids=list(WALKS))
 @pytest.mark.parametrize("path", WGSL_ISECT, ids=[os.path.basename(p) for p in WGSL_ISECT])
 def test_matches_reference_intersect_world(renderer, path, flags):
     """rt_intersect against intersect.wgsl's own intersect_world (executed by

@@ -19,6 +19,7 @@ pytestmark = pytest.mark.gpu
 
 NO_REUSE = abi.RT_FLAG_NO_PRIMARY_CACHE
 CULL = abi.RT_FLAG_CULL
+VALU = abi.RT_FLAG_VALU_FILTER  # the packed-fp32 filter instead of the matrix-core one
 
 
 def arrays(sc):
@@ -67,7 +68,7 @@ WGSL = sorted(p for p in glob.glob(os.path.join(os.path.dirname(os.path.abspath(
 WGSL_ACCUM = [p for p in WGSL if "_accum" in os.path.basename(p)]
 
 
-@pytest.mark.parametrize("flags", [0, NO_REUSE, CULL], ids=["reuse", "noreuse", "cull"])
+@pytest.mark.parametrize("flags", [0, NO_REUSE, CULL, VALU], ids=["reuse", "noreuse", "cull", "valu"])
 @pytest.mark.parametrize("path", WGSL, ids=[os.path.basename(p) for p in WGSL])
 def test_matches_interpreted_reference_wgsl(renderer, path, flags):
     """The HIP path against frames of the reference's own WGSL kernels,
@@ -85,7 +86,7 @@ def test_matches_interpreted_reference_wgsl(renderer, path, flags):
         check_exact(img.reshape(-1, 4)[:n], ref.reshape(-1, 4)[:n])
 
 
-@pytest.mark.parametrize("flags", [0, NO_REUSE, CULL], ids=["reuse", "noreuse", "cull"])
+@pytest.mark.parametrize("flags", [0, NO_REUSE, CULL, VALU], ids=["reuse", "noreuse", "cull", "valu"])
 @pytest.mark.parametrize("path", WGSL_ACCUM, ids=[os.path.basename(p) for p in WGSL_ACCUM])
 def test_spp_is_blocked_sum_of_reference_frames(renderer, path, flags):
     """One S-spp render == the blocked f32 sum of the reference's S
@@ -102,8 +103,8 @@ def test_spp_is_blocked_sum_of_reference_frames(renderer, path, flags):
     check_exact(img, blocked_mean(list(z["images"])))
 
 
-@pytest.mark.parametrize("flags", [0, NO_REUSE, CULL, CULL | NO_REUSE],
-                         ids=["reuse", "noreuse", "cull", "cull_noreuse"])
+@pytest.mark.parametrize("flags", [0, NO_REUSE, CULL, CULL | NO_REUSE, VALU, VALU | NO_REUSE],
+                         ids=["reuse", "noreuse", "cull", "cull_noreuse", "valu", "valu_noreuse"])
 @pytest.mark.parametrize("name,mk,W,H,S,D,f0", CASES, ids=[c[0] for c in CASES])
 def test_bit_exact(renderer, name, mk, W, H, S, D, f0, flags):
     sp, mt = arrays(mk())
