@@ -29,6 +29,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o ru
     > "$R/gpurun_out/prof.log" 2>&1
 step rocprof $?
 cd "$R"
+if [ "${CALIB:-0}" = 1 ]; then  # VALU issue calibration (tools/ubench/valu_busy, built by hand)
 timeout -k 10 120 tools/ubench/valu_busy > gpurun_out/valu_busy.log 2>&1
 step valu_busy $?
 cd /tmp
@@ -41,6 +42,7 @@ timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $CLS -d "$R/gpurun_out/rk_cls
     --no-cpu-baseline --reuse-steps 0 --cull-steps 0 > "$R/gpurun_out/rk_cls.log" 2>&1
 step rk_cls $?
 cd "$R"
+fi
 timeout -k 10 900 tools/pmc_round.sh
 step pmc_round $?
 echo ROUND_OK

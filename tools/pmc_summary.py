@@ -78,6 +78,19 @@ if "FETCH_SIZE" in rk and "WRITE_SIZE" in rk:
             ent["valu"]["valubusy_issue"] = ((rk["SQ_INSTS_VALU"] - i32) * 4 + i32 * 2) / simd_cycles
             ent["valu"]["formula_issue"] = ("((SQ_INSTS_VALU - SQ_INSTS_VALU_INT32) x 4 + "
                                             "SQ_INSTS_VALU_INT32 x 2) / (1024 x GRBM_GUI_ACTIVE / 8)")
+    # matrix-core filter (f16 MFMA tiles) of the same launch: executed MFMA
+    # flops (MOPS x 512) and the matrix pipe's busy share of the SIMD cycles
+    if rk.get("SQ_INSTS_VALU_MFMA_MOPS_F16") and rk.get("GRBM_GUI_ACTIVE"):
+        simd_cycles = 1024 * rk["GRBM_GUI_ACTIVE"] / 8
+        d[wl]["mfma"] = {
+            "mfma_f16_flops": rk["SQ_INSTS_VALU_MFMA_MOPS_F16"] * 512,
+            "sq_insts_mfma": rk.get("SQ_INSTS_MFMA"),
+            "sq_valu_mfma_busy_cycles": rk.get("SQ_VALU_MFMA_BUSY_CYCLES"),
+            "mfma_busy": (rk["SQ_VALU_MFMA_BUSY_CYCLES"] / simd_cycles
+                          if rk.get("SQ_VALU_MFMA_BUSY_CYCLES") else None),
+            "formula_busy": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs)",
+            "formula_flops": "SQ_INSTS_VALU_MFMA_MOPS_F16 x 512",
+        }
     json.dump(d, open(tp, "w"), indent=1)
 print(json.dumps({k: summary[k] for k in summary if k != "per_dispatch_mean"}, indent=1))
 print(json.dumps(rk, indent=1))
