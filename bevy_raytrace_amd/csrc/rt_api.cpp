@@ -114,6 +114,8 @@ struct rt_ctx {
     // matrix-core filter (RT_MFMA_FILTER builds, build_mfma): f16 A fragments
     bool mf_ok = false;
     uint32_t mf_nblk = 0;
+    float mf_qs = 1.0f;   // 2^sq: the ray side's scale of the quadratic features
+    float mf_abs = 0.0f;  // absolute margin of the threshold, 2^(sq - 20)
     uint4* d_mfA = nullptr;
     size_t mfA_cap = 0;
 
@@ -630,12 +632,21 @@ static int quiesce(rt_ctx* ctx) {  // no kernel may be reading the scene while i
 
 #ifdef RT_MFMA_FILTER
 // ---- matrix-core filter fragments (rt_dev_intersect.h intersect_world_mfma) ----
-// Row j of the A operand (sphere j): [cx_hi, cx_lo, cx_hi, cy.., cz.., 1, 1,
-// S'_hi, S'_lo, 0, 0, 0], hi = RN_f16(c), lo = RN_f16(c - hi), S' = r^2 -
-// (1 - m - mu')|c|^2 from double. Block b (spheres 32b..32b+31), lane l: row
-// l & 31, elements k = 8 (l >> 5) .. + 8. Pad rows: c = 0, S'_hi = -inf (H is
-// -inf or NaN there: never a candidate). Only scenes whose centres and S' fit
-// the split's range take it (mf_ok); the rest keep the VALU filter.
+// The filter value less the ray's k1^2, H0 = S' + L.c + sum_ab Q_ab c_a c_b, is
+// one 32-term dot product of a sphere row and a ray column (K = 32: two
+// chained v_mfma_f32_32x32x16_f16). Sphere row j, each feature as f16 hi/lo:
+//   K 0..8   c_a          [hi, hi, lo] for a = x, y, z
+//   K 9..26  c_a c_b 2^-sq [hi, hi, lo] for ab = xx, yy, zz, xy, xz, yz
+//   K 27, 28 S' = r^2 - (1 - m - mu')|c|^2  [hi, lo]
+//   K 29..31 0
+// (the ray column holds the partner parts [hi, lo, hi], and 1, 1 against S').
+// hi = RN_f16(x), lo = RN_f16(x - hi), all from double. sq scales the
+// quadratic features into f16 range (max |c_a c_b| 2^-sq <= 2^14); the ray
+// side carries 2^sq. Block b (spheres 32b..32b+31): two uint4 per lane, A0
+// (K 0..15) then A1 (K 16..31), 64 lanes each; lane l: row l & 31, elements
+// k = 8 (l >> 5) .. + 8 of that half. Pad rows: 0, S'_hi = -inf (H0 = -inf or
+// NaN: never a candidate). Only scenes with |c_i| <= 2^12 and |S'| <= 2^15
+// take it (mf_ok); the rest keep the VALU filter.
 static uint16_t f16_bits(double x) {
     const _Float16 h = (_Float16)x;
     uint16_t u;
@@ -643,54 +654,70 @@ static uint16_t f16_bits(double x) {
     return u;
 }
 
+static void f16_split(double x, uint16_t& hi, uint16_t& lo) {
+    hi = f16_bits(x);
+    _Float16 hv;
+    std::memcpy(&hv, &hi, 2);
+    lo = f16_bits(x - (double)hv);
+}
+
 static int build_mfma(rt_ctx* ctx) {
     const uint32_t n = ctx->n;
     ctx->mf_ok = false;
     if (!n) return RT_OK;
     const double kS = 1.0 - 0x1p-16 - 0x1p-16;  // 1 - m - mu' (RT_MF_MU)
-    const uint32_t nblk = (n + 31) / 32;
-    std::vector<uint16_t> h((size_t)nblk * 64 * 8);
+    double qmax = 1.0;
     for (uint32_t j = 0; j < n; ++j) {
         const float4 q = ctx->h_sph[j];
         if (!(std::fabs(q.x) <= 0x1p12f && std::fabs(q.y) <= 0x1p12f && std::fabs(q.z) <= 0x1p12f &&
               q.w >= 0.0f && q.w <= 0x1p24f))
             return RT_OK;  // outside the f16 split's range: VALU filter
+        const double c[3] = {q.x, q.y, q.z};
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) qmax = std::max(qmax, std::fabs(c[a] * c[b]));
     }
+    int sq = 0;
+    while (qmax * std::ldexp(1.0, -sq) > 0x1p14) ++sq;  // <= 10 for |c| <= 2^12
+    const uint32_t nblk = (n + 31) / 32;
+    std::vector<uint16_t> h((size_t)nblk * 2 * 64 * 8);
+    static const int QA[6] = {0, 1, 2, 0, 0, 1}, QB[6] = {0, 1, 2, 1, 2, 2};
     for (uint32_t b = 0; b < nblk; ++b)
         for (uint32_t l = 0; l < 64; ++l) {
             const uint32_t j = 32 * b + (l & 31), hh = l >> 5;
-            uint16_t row[16] = {};
-            const uint16_t one = f16_bits(1.0);
+            uint16_t row[32] = {};
             if (j < n) {
                 const float4 q = ctx->h_sph[j];
-                const float c[3] = {q.x, q.y, q.z};
+                const double c[3] = {q.x, q.y, q.z};
+                uint16_t hi, lo;
                 for (int a = 0; a < 3; ++a) {
-                    const uint16_t hi = f16_bits(c[a]);
-                    _Float16 hv;
-                    std::memcpy(&hv, &hi, 2);
-                    const uint16_t lo = f16_bits((double)c[a] - (double)hv);
+                    f16_split(c[a], hi, lo);
                     row[3 * a] = hi;
-                    row[3 * a + 1] = lo;
-                    row[3 * a + 2] = hi;
+                    row[3 * a + 1] = hi;
+                    row[3 * a + 2] = lo;
                 }
-                const double cc = (double)q.x * q.x + (double)q.y * q.y + (double)q.z * q.z;
-                const double S = (double)q.w - kS * cc;
+                for (int f = 0; f < 6; ++f) {
+                    f16_split(std::ldexp(c[QA[f]] * c[QB[f]], -sq), hi, lo);
+                    row[9 + 3 * f] = hi;
+                    row[9 + 3 * f + 1] = hi;
+                    row[9 + 3 * f + 2] = lo;
+                }
+                const double S = (double)q.w - kS * (c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
                 if (!(std::fabs(S) <= 0x1p15)) return RT_OK;
-                const uint16_t sh = f16_bits(S);
-                _Float16 sv;
-                std::memcpy(&sv, &sh, 2);
-                row[11] = sh;
-                row[12] = f16_bits(S - (double)sv);
+                f16_split(S, hi, lo);
+                row[27] = hi;
+                row[28] = lo;
             } else {
-                row[11] = f16_bits(-INFINITY);
+                row[27] = f16_bits(-INFINITY);
             }
-            row[9] = row[10] = one;
-            std::memcpy(&h[((size_t)b * 64 + l) * 8], &row[8 * hh], 16);
+            for (int half = 0; half < 2; ++half)  // A0: K 0..15, A1: K 16..31
+                std::memcpy(&h[(((size_t)b * 2 + half) * 64 + l) * 8], &row[16 * half + 8 * hh], 16);
         }
     int rc = ensure(ctx, &ctx->d_mfA, &ctx->mfA_cap, h.size() * sizeof(uint16_t));
     if (rc) return rc;
     HIP_TRY(ctx, hipMemcpy(ctx->d_mfA, h.data(), h.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
     ctx->mf_nblk = nblk;
+    ctx->mf_qs = (float)std::ldexp(1.0, sq);
+    ctx->mf_abs = (float)std::ldexp(1.0, sq - 20);
     ctx->mf_ok = true;
     return RT_OK;
 }
@@ -993,6 +1020,8 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     if (!cull && ctx->mf_ok && !(p.flags & RT_FLAG_VALU_FILTER)) {
         K_.mfA = ctx->d_mfA;
         K_.mf_nblk = ctx->mf_nblk;
+        K_.mf_qs = ctx->mf_qs;
+        K_.mf_abs = ctx->mf_abs;
     }
 #endif
     std::memcpy(K_.T, cam->transform, sizeof(K_.T));
@@ -1338,10 +1367,13 @@ int rt_intersect_ex(rt_ctx* ctx, const float* rays, uint32_t n, uint32_t flags, 
     // when the scene fits them (unless RT_FLAG_VALU_FILTER)
     const uint4* mfA = nullptr;
     uint32_t mf_nblk = 0;
+    float mf_qs = 1.0f, mf_abs = 0.0f;
 #ifdef RT_MFMA_FILTER
     if (!cull && ctx->mf_ok && !(flags & RT_FLAG_VALU_FILTER)) {
         mfA = ctx->d_mfA;
         mf_nblk = ctx->mf_nblk;
+        mf_qs = ctx->mf_qs;
+        mf_abs = ctx->mf_abs;
     }
 #endif
     if (e == hipSuccess)
@@ -1351,7 +1383,8 @@ int rt_intersect_ex(rt_ctx* ctx, const float* rays, uint32_t n, uint32_t flags, 
                                 ctx->scene_fast && ctx->tune.fast_exact ? 1u : 0u,
                                 (const float*)b, n, (int*)(b + rb), (float*)(b + rb + ob),
                                 cull ? ctx->d_bnd_c : nullptr, cull ? ctx->d_perm_c : nullptr,
-                                cull ? ctx->nclusters_c : 0u, mfA, mf_nblk, ctx->stream);
+                                cull ? ctx->nclusters_c : 0u, mfA, mf_nblk, mf_qs, mf_abs,
+                                ctx->stream);
     }
     if (e == hipSuccess)
         e = hipMemcpyAsync(hit_index, b + rb, ob, hipMemcpyDeviceToHost, ctx->stream);

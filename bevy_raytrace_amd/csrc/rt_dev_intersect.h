@@ -603,52 +603,45 @@ __device__ __forceinline__ uint32_t lanemask_lt_count(uint64_t m) {
 
 
 #ifdef RT_MFMA_FILTER
-// ---- the filter on the matrix cores (RT_MFMA_FILTER builds; DESIGN.md §9) ----
-// Per 32-sphere block b and per 32-ray half t of the wave, two
-// v_mfma_f32_32x32x16_f16 give hb = k1 - dn.c and v = S' + o2.c for the 32 x 32
-// (sphere, ray) pairs from f16 hi/lo parts (A row of sphere j: [cx_hi, cx_lo,
-// cx_hi, cy.., cz.., 1, 1, S'_hi, S'_lo, 0, 0, 0]; B column of a ray: u =
-// [-dnx_hi, -dnx_hi, -dnx_lo, .., k1_hi, k1_lo, 0, 0, ..], v = [o2x_hi, o2x_hi,
-// o2x_lo, .., 0, 0, 1, 1, ..]), then H = hb^2 + v as the VALU filter, against
-// T' = (1 - m - mu')|o|^2 with the wider mu' of the split arithmetic. Output
-// layout (MI355X guide): lane l holds column (ray) l & 31 of the half, rows
-// (spheres) (i & 3) + 8 (i >> 2) + 4 (l >> 5) in register i: four whole groups
-// of 4 spheres per lane. A lane queues (group-of-4 index << 4 | 4-bit mask)
-// per half; the ray's lane drains the entries of its column's two lanes, in
-// any order, with the (t, index) tie-break (exact_body LEX).
+// ---- the filter on the matrix cores (RT_MFMA_FILTER builds; DESIGN.md §4.7) ----
+// The VALU filter's value H = hb^2 + S + o2.c (hb = k1 + e.c, e = -dn) is a
+// quadratic form in the sphere centre, so with the ray's k1^2 moved into its
+// threshold it is ONE dot product of a sphere row and a ray column:
+//   H - k1^2 = H0 = S' + L.c + sum_ab Q_ab c_a c_b,
+//   L_a = 2 k1 e_a + o2_a,  Q_aa = e_a^2,  Q_ab = 2 e_a e_b (a < b),
+// candidate iff H0 >= T0 = (1 - m - mu')|o|^2 - k1^2 - abs'. Each of the 10
+// features is split into f16 hi/lo parts (x = hi + lo + err): 3 products
+// (hi.hi + hi.lo + lo.hi) per feature, 2 for S' against an exact 1 -- 29 of
+// K = 32 (rt_api.cpp build_mfma: the A rows and their layout). Per 32-sphere
+// block b and 32-ray half t of the wave, two chained v_mfma_f32_32x32x16_f16
+// give H0 for the 32 x 32 (sphere, ray) pairs straight into VGPRs; the VALU
+// only takes maxima and compares. Output layout (MI355X guide): lane l holds
+// column (ray) l & 31 of the half, rows (spheres) (i & 3) + 8 (i >> 2) +
+// 4 (l >> 5) in register i: four whole groups of 4 spheres per lane. A lane
+// queues (group-of-4 index << 4 | 4-bit mask) per half; the ray's lane drains
+// the entries of its column's two lanes, in any order, with the (t, index)
+// tie-break (exact_body LEX).
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef float f16x __attribute__((ext_vector_type(16)));
-// Margins (the VALU filter's m; mu' and an absolute term for the split):
-// with x = hi + lo + e, |e| <= 2^-22|x| + 2^-25 (f16 11-bit significands, lo
-// possibly subnormal), each 3-product term is within 3 * 2^-22|x||y| +
-// 2^-25(|x| + |y|) of x*y, and the f32 sum of the 11 exact products within
-// 10 * 2^-24 of the sum of their magnitudes. So |hb' - hb~| <= 2^-19.5 (|o| +
-// |c|) + 2^-23 (1 + |c|) and |v' - v~| <= 2^-18.6 |o||c| + 2^-20.6 (r^2 + |c|^2)
-// + 2^-24 (|o| + |c|), hence with |hb~| <= (1 + 2^-20)(|o| + |c|) and the last
-// fma's rounding: |H' - H~| <= 1.0 * 2^-17 (|o|^2 + |c|^2) + 2^-20.3 r^2 +
-// 2^-21. The ray constants are the VALU filter's (their error, <= 25 * 2^-24
-// (|o|^2 + |c|^2), is in its mu = 2^-17); mu' = 2^-16 covers both terms in
-// |o|^2 + |c|^2, the m margin's slack (2^-16 - 35 * 2^-24) the r^2 term, and
-// T' carries 2^-20 for the absolute one.
+// Margins. Split: |x - hi - lo| <= 2^-22|x| + 2^-25 (lo may be subnormal), so
+// a feature product is within 3 * 2^-22|a||b| + 2^-25(|a| + |b|) of a b, and
+// sum_f |a_f||b_f| <= 4|o||c| + |c|^2 + |S'| (|L| <= 4|o|, sum |Q c c| =
+// (sum |e_a c_a|)^2 <= |c|^2): <= 2^-18.8 (|o|^2 + |c|^2) + 2^-20.4 |S'|. The
+// f32 sums of the 29 exact products (two chained MFMAs, 31 roundings at most)
+// add <= 31 * 2^-24 of the same magnitudes: <= 2^-17.4 (|o|^2 + |c|^2) +
+// 2^-19 |S'|. The ray features' own roundings (one fma for L, two products for
+// Q, the fma of T0) add <= 2^-21 (|o|^2 + |c|^2), and the ray constants dn, k1,
+// o2 are the VALU filter's (<= 25 * 2^-24 (|o|^2 + |c|^2), ray_filter_consts).
+// Total <= 2^-16.3 (|o|^2 + |c|^2) < mu' = 2^-16 in |o|^2 + |c|^2; the |S'| <=
+// r^2 + |c|^2 part goes to the m margin's slack (2^-16 - 35 * 2^-24) and mu';
+// the absolute parts, 2^-25 x (the ray features scaled by 2^sq <= 2^(sq+1),
+// the linear ones <= 4|o|), to abs' = 2^(sq - 20) (rt_api.cpp: mf_abs).
+// tests/test_mfma_filter.py restates this arithmetic and checks it.
 #define RT_MF_MU 0x1p-16f
-#define RT_MF_ABS 0x1p-20f
 #define RT_MF_CAP 8  // queue entries per lane and half (LDS)
 
 __device__ __forceinline__ uint32_t bperm(uint32_t src_lane, uint32_t v) {
     return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
-}
-
-__device__ __forceinline__ uint32_t pack2h(float x, float y) {
-    const _Float16 a = (_Float16)x, b = (_Float16)y;
-    uint16_t ua, ub;
-    __builtin_memcpy(&ua, &a, 2);
-    __builtin_memcpy(&ub, &b, 2);
-    return (uint32_t)ua | ((uint32_t)ub << 16);
-}
-// hi / lo f16 parts of x (lo = the rounding residual, itself rounded to f16)
-__device__ __forceinline__ void split_h(float x, float& hi, float& lo) {
-    hi = (float)(_Float16)x;
-    lo = (float)(_Float16)(x - hi);
 }
 
 // the wave may use the f16 filter: every live lane's |o| within the split's range
@@ -693,7 +686,9 @@ __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, ui
 
 // Called by the whole wave (the MFMA operands span all 64 lanes): lanes
 // without a ray (live false) trace a dummy ray whose threshold is +inf.
+// mf_qs = 2^sq, mf_abs = abs' (build_mfma).
 __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mfA, uint32_t nblk,
+                                                    float mf_qs, float mf_abs,
                                                     const float4* __restrict__ sph,
                                                     uint32_t scene_fast, v3 o, v3 d, bool live,
                                                     uint64_t live_mask, float& t_out,
@@ -712,59 +707,69 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
     const float ya = fast ? rt_recip_rn(a) : a;
     const uint32_t lane = __lane_id();
     const uint32_t h = lane >> 5;
-    // ray constants (ray_filter_consts, with the wider mu')
+    // ray constants (ray_filter_consts, with the wider mu'), then the features
     const float rs = __builtin_amdgcn_rsqf(dot(d, d));
-    const float dnx = d.x * rs, dny = d.y * rs, dnz = d.z * rs;
+    const float ex = -(d.x * rs), ey = -(d.y * rs), ez = -(d.z * rs);  // e = -dn
     const float m_ = 0x1p-16f;
     const float oo = __builtin_fmaf(o.z, o.z, __builtin_fmaf(o.y, o.y, o.x * o.x));
-    const float k1 = __builtin_fmaf(dnz, o.z, __builtin_fmaf(dny, o.y, dnx * o.x));
+    const float k1 = __builtin_fmaf(-ez, o.z, __builtin_fmaf(-ey, o.y, -ex * o.x));
     const float two = 2.0f * (1.0f - m_);
-    const float T = live ? (1.0f - m_ - RT_MF_MU) * oo - RT_MF_ABS : INFINITY;
-    float xh, xl, yh, yl, zh, zl, kh, kl;
-    split_h(-dnx, xh, xl);
-    split_h(-dny, yh, yl);
-    split_h(-dnz, zh, zl);
-    split_h(k1, kh, kl);
-    // u = [x_hi, x_hi, x_lo, y_hi, y_hi, y_lo, z_hi, z_hi | z_lo, k_hi, k_lo, 0, 0, 0, 0, 0]
-    const uint32_t ul0 = pack2h(xh, xh), ul1 = pack2h(xl, yh), ul2 = pack2h(yh, yl),
-                   ul3 = pack2h(zh, zh);
-    const uint32_t uh0 = pack2h(zl, kh), uh1 = pack2h(kl, 0.0f), uh2 = 0u, uh3 = 0u;
-    float ph, pl, qh, ql, rh, rl;
-    split_h(two * o.x, ph, pl);
-    split_h(two * o.y, qh, ql);
-    split_h(two * o.z, rh, rl);
-    // v = [p_hi, p_hi, p_lo, q_hi, q_hi, q_lo, r_hi, r_hi | r_lo, 0, 0, 1, 1, 0, 0, 0]
-    const uint32_t vl0 = pack2h(ph, ph), vl1 = pack2h(pl, qh), vl2 = pack2h(qh, ql),
-                   vl3 = pack2h(rh, rh);
-    const uint32_t vh0 = pack2h(rl, 0.0f), vh1 = pack2h(0.0f, 1.0f), vh2 = pack2h(1.0f, 0.0f),
-                   vh3 = 0u;
-    // B fragments: half 0 = rays 0..31 (lane l: column l & 31, k 8h..8h+7),
-    // half 1 = rays 32..63. v_permlane32_swap(lo, hi) swaps lo's upper 32
-    // lanes with hi's lower 32 (profiles/r02_permlane32_swap.log): its first
-    // result is half 0's fragment (lanes < 32 their own K 0..7, lanes >= 32
-    // K 8..15 of ray l - 32), its second half 1's.
-    auto frag = [&](uint32_t lo, uint32_t hi, uint32_t& f0, uint32_t& f1) {
-        const auto r = __builtin_amdgcn_permlane32_swap(lo, hi, false, false);
-        f0 = r[0];
-        f1 = r[1];
-    };
-    uint32_t u00, u01, u02, u03, u10, u11, u12, u13, v00, v01, v02, v03, v10, v11, v12, v13;
-    frag(ul0, uh0, u00, u10);
-    frag(ul1, uh1, u01, u11);
-    frag(ul2, uh2, u02, u12);
-    frag(ul3, uh3, u03, u13);
-    frag(vl0, vh0, v00, v10);
-    frag(vl1, vh1, v01, v11);
-    frag(vl2, vh2, v02, v12);
-    frag(vl3, vh3, v03, v13);
-    auto as_h8 = [](uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
-        const uint4 q = make_uint4(w0, w1, w2, w3);
+    const float T = live ? __builtin_fmaf(-k1, k1, (1.0f - m_ - RT_MF_MU) * oo) - mf_abs : INFINITY;
+    const float k2 = 2.0f * k1;
+    float f[9];  // L_x, L_y, L_z, Q_xx, Q_yy, Q_zz, Q_xy, Q_xz, Q_yz
+    f[0] = __builtin_fmaf(k2, ex, two * o.x);
+    f[1] = __builtin_fmaf(k2, ey, two * o.y);
+    f[2] = __builtin_fmaf(k2, ez, two * o.z);
+    f[3] = (ex * ex) * mf_qs;
+    f[4] = (ey * ey) * mf_qs;
+    f[5] = (ez * ez) * mf_qs;
+    f[6] = ((2.0f * ex) * ey) * mf_qs;
+    f[7] = ((2.0f * ex) * ez) * mf_qs;
+    f[8] = ((2.0f * ey) * ez) * mf_qs;
+    // the ray column, K 0..31: per feature [hi, lo, hi] (the sphere row holds
+    // [hi, hi, lo]), then 1, 1 (against S'_hi, S'_lo), then 0, 0, 0
+    _Float16 col[32];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        const _Float16 hi = (_Float16)f[k];
+        const _Float16 lo = (_Float16)(f[k] - (float)hi);
+        col[3 * k] = hi;
+        col[3 * k + 1] = lo;
+        col[3 * k + 2] = hi;
+    }
+    col[27] = (_Float16)1.0f;
+    col[28] = (_Float16)1.0f;
+    col[29] = col[30] = col[31] = (_Float16)0.0f;
+    uint32_t w[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        uint16_t u0, u1;
+        __builtin_memcpy(&u0, &col[2 * k], 2);
+        __builtin_memcpy(&u1, &col[2 * k + 1], 2);
+        w[k] = (uint32_t)u0 | ((uint32_t)u1 << 16);
+    }
+    // B fragments of K group g (K 16g..16g+15), half t: lane l holds column
+    // l & 31, k = 8 (l >> 5) .. + 8. v_permlane32_swap(lo, hi) swaps lo's upper
+    // 32 lanes with hi's lower 32 (profiles/r02_permlane32_swap.log): from each
+    // lane's own K 16g..+7 (lo) and 16g+8..+15 (hi) its first result is half
+    // 0's fragment, its second half 1's.
+    uint32_t b0[2][4], b1[2][4];  // [K group][word] of half 0 / half 1
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const auto r = __builtin_amdgcn_permlane32_swap(w[8 * g + q], w[8 * g + 4 + q], false, false);
+            b0[g][q] = r[0];
+            b1[g][q] = r[1];
+        }
+    auto as_h8 = [](const uint32_t* v) {
+        const uint4 q = make_uint4(v[0], v[1], v[2], v[3]);
         h8v r;
         __builtin_memcpy(&r, &q, 16);
         return r;
     };
-    const h8v Bu0 = as_h8(u00, u01, u02, u03), Bu1 = as_h8(u10, u11, u12, u13);
-    const h8v Bv0 = as_h8(v00, v01, v02, v03), Bv1 = as_h8(v10, v11, v12, v13);
+    const h8v B00 = as_h8(b0[0]), B01 = as_h8(b0[1]);  // half 0: K 0..15, K 16..31
+    const h8v B10 = as_h8(b1[0]), B11 = as_h8(b1[1]);  // half 1
     const auto Tw = __builtin_amdgcn_permlane32_swap(__float_as_uint(T), __float_as_uint(T), false, false);
     const float T0 = __uint_as_float(Tw[0]), T1 = __uint_as_float(Tw[1]);  // of ray l & 31, 32 + (l & 31)
 
@@ -775,7 +780,7 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
     // is the ray of this lane's column live, per half
     const bool col0 = (live_mask >> (lane & 31u)) & 1u, col1 = (live_mask >> (32u + (lane & 31u))) & 1u;
     const uint4* ap = mfA + lane;
-    uint4 a4 = ap[0];
+    uint4 a0 = ap[0], a1 = ap[64];
     for (uint32_t b = 0; b < nblk; ++b) {
         // a block adds at most 4 entries to each half's queue: make room first,
         // while no tile result is live
@@ -787,26 +792,21 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
                 mfma_drain<false>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i);
             cnt0 = cnt1 = 0;
         }
-        // the next block's fragment loads during this one (-1.2 %)
-        const uint4 an = ap[(size_t)(b + 1 < nblk ? b + 1 : b) * 64u];
-        h8v A;
-        __builtin_memcpy(&A, &a4, 16);
+        // the next block's fragments load during this one
+        const size_t nb = (size_t)(b + 1 < nblk ? b + 1 : b) * 128u;
+        const uint4 n0 = ap[nb], n1 = ap[nb + 64];
+        h8v A0, A1;
+        __builtin_memcpy(&A0, &a0, 16);
+        __builtin_memcpy(&A1, &a1, 16);
         // the two halves unrolled (no per-tile operand selects) but kept apart
-        // (sched_barrier): one tile's 32 result registers live at a time
+        // (sched_barrier): one tile's 16 result registers live at a time
 #pragma unroll
         for (uint32_t t = 0; t < 2; ++t) {
             if (t) __builtin_amdgcn_sched_barrier(0);
-            const f16x U = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, t ? Bu1 : Bu0, zero, 0, 0, 0);
-            const f16x V = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, t ? Bv1 : Bv0, zero, 0, 0, 0);
+            const f16x H = __builtin_amdgcn_mfma_f32_32x32x16_f16(
+                A1, t ? B11 : B01,
+                __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, t ? B10 : B00, zero, 0, 0, 0), 0, 0, 0);
             const float Tt = t ? T1 : T0;
-            float H[16];
-#pragma unroll
-            for (int i = 0; i < 16; i += 2) {
-                const f2 hb = {U[i], U[i + 1]}, vs = {V[i], V[i + 1]};
-                const f2 hh = pk_fma(hb, hb, vs);
-                H[i] = hh.x;
-                H[i + 1] = hh.y;
-            }
             // per-group maxima (the lane's 4 groups of 4 spheres), then the tile's
             float gq[4];
 #pragma unroll
@@ -829,7 +829,8 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
                 }
             }
         }
-        a4 = an;
+        a0 = n0;
+        a1 = n1;
     }
     PROF_MARK(1);
     if (fast)

@@ -91,10 +91,11 @@ struct KParams {
     uint32_t cull_supers;   // 1: test the cluster bounds (many clusters); 0: walk every cluster
     const float4* acc_in;   // passes after the first (block_begin > 0): the fold so far, per pixel
     // matrix-core filter (RT_MFMA_FILTER builds, brute-force walk): the list as
-    // f16 A fragments of v_mfma_f32_32x32x16_f16, per 32-sphere block 64 lanes
-    // x 16 B (rt_api.cpp build_mfma); null: the packed VALU filter
+    // f16 A fragments of v_mfma_f32_32x32x16_f16, per 32-sphere block 2 x 64
+    // lanes x 16 B (rt_api.cpp build_mfma); null: the packed VALU filter
     const uint4* mfA;
     uint32_t mf_nblk;
+    float mf_qs, mf_abs;  // 2^sq (quadratic features' ray-side scale), threshold margin
 };
 
 // Row block b of the image -> owning shard (rt_params: serpentine deal).
@@ -123,7 +124,8 @@ hipError_t rt_launch_assemble(const float4* gathered, uint32_t max_rows, float4*
 hipError_t rt_launch_intersect(const float4* grp, const float4* sph, uint32_t ngroups,
                                uint32_t scene_fast, const float* rays, uint32_t n, int* out_i, float* out_t,
                                const float4* bnd, const uint32_t* perm, uint32_t nclusters,
-                               const uint4* mfA, uint32_t mf_nblk, hipStream_t stream);
+                               const uint4* mfA, uint32_t mf_nblk, float mf_qs, float mf_abs,
+                               hipStream_t stream);
 hipError_t rt_render_occupancy(int* blocks_per_cu, int* blocks_per_cu_cull);
 hipError_t rt_launch_primary(const KParams* P, float4* pd, hipStream_t stream);
 }

@@ -115,14 +115,22 @@ __device__ __forceinline__ void render_body(
     // the wave's slices of the workgroup's LDS arrays: wave-uniform bases
     // (SGPRs) indexed by the lane id, so no VGPR holds an LDS address
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
-    __shared__ uint32_t s_cq[RT_BLOCK_THREADS * RT_CQ_CAP];  // per-lane candidate queues
-    uint32_t* cq = s_cq + wave * (64u * RT_CQ_CAP);
-    __shared__ LaneLds s_lane[RT_BLOCK_THREADS];  // per-lane item state (rt_dev_path.h)
+    // per-lane candidate queues: RT_CQ_CAP entries per lane for the VALU walk,
+    // 2 halves x RT_MF_CAP for the matrix-core walk (RT_MFMA_FILTER); a wave
+    // drains the queue of one walk before it starts another, so both share
+    // one array (the brute-force kernel's LDS stays 28 KB per workgroup)
 #ifdef RT_MFMA_FILTER
-    // the matrix-core filter's queues: per wave 2 halves x RT_MF_CAP x 64 lanes
-    __shared__ uint32_t s_cqm[(RT_BLOCK_THREADS / 64) * 2 * RT_MF_CAP * 64];
-    uint32_t* cqm = s_cqm + wave * (2u * RT_MF_CAP * 64u);
+    constexpr uint32_t QW = CULL ? 64u * RT_CQ_CAP : 2u * RT_MF_CAP * 64u;  // words per wave
+    static_assert(2u * RT_MF_CAP >= RT_CQ_CAP, "the shared queue holds the VALU walk's");
+#else
+    constexpr uint32_t QW = 64u * RT_CQ_CAP;
 #endif
+    __shared__ uint32_t s_cq[(RT_BLOCK_THREADS / 64) * QW];
+    uint32_t* cq = s_cq + wave * QW;
+#ifdef RT_MFMA_FILTER
+    uint32_t* cqm = cq;
+#endif
+    __shared__ LaneLds s_lane[RT_BLOCK_THREADS];  // per-lane item state (rt_dev_path.h)
     const ItemLds lds = s_lane + wave * 64u + lane;
 #ifdef RT_SPHERES_LDS
     // Experiment variant: the filter reads the sphere groups from LDS (staged
@@ -275,7 +283,8 @@ __device__ __forceinline__ void render_body(
             intersect_wide<CULL>(sph, P.nspheres, P.scene_fast, live, st.o, st.d, hi, t, P.perm);
 #ifdef RT_MFMA_FILTER
         } else if (!CULL && P.mfA && mfma_wave_ok(st.o, has_item)) {  // the whole wave
-            const int h2 = intersect_world_mfma(P.mfA, P.mf_nblk, sph, P.scene_fast, st.o, st.d,
+            const int h2 = intersect_world_mfma(P.mfA, P.mf_nblk, P.mf_qs, P.mf_abs, sph,
+                                                P.scene_fast, st.o, st.d,
                                                 has_item, live, t, cqm
 #ifdef RT_PROFILE
                                                 , prof_
@@ -475,7 +484,8 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_cull_kernel(
 // runs the tiles, lanes past n trace a dummy ray that never has a candidate; a
 // wave with a ray outside the range takes the VALU filter, as in the render.
 __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_mfma_kernel(
-    const uint4* __restrict__ mfA, uint32_t nblk, const float4* __restrict__ grp,
+    const uint4* __restrict__ mfA, uint32_t nblk, float mf_qs, float mf_abs,
+    const float4* __restrict__ grp,
     const float4* __restrict__ sph, uint32_t ngroups, uint32_t scene_fast,
     const float* __restrict__ rays, uint32_t n, int* __restrict__ out_i, float* __restrict__ out_t) {
     __shared__ uint32_t s_cq[RT_BLOCK_THREADS * RT_CQ_CAP];
@@ -500,7 +510,7 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_mfma_kernel(
 #else
     if (mfma_wave_ok(o, live)) {
 #endif
-        hi = intersect_world_mfma(mfA, nblk, sph, scene_fast, o, d, live, lm, t,
+        hi = intersect_world_mfma(mfA, nblk, mf_qs, mf_abs, sph, scene_fast, o, d, live, lm, t,
                                   s_cqm + wave * (2u * RT_MF_CAP * 64u)
 #ifdef RT_PROFILE
                                   , prof_
@@ -689,17 +699,20 @@ hipError_t rt_launch_intersect(const float4* grp, const float4* sph, uint32_t ng
                                uint32_t scene_fast, const float* rays, uint32_t n, int* out_i,
                                float* out_t, const float4* bnd, const uint32_t* perm,
                                uint32_t nclusters, const uint4* mfA, uint32_t mf_nblk,
-                               hipStream_t stream) {
+                               float mf_qs, float mf_abs, hipStream_t stream) {
     const uint32_t T = RT_BLOCK_THREADS;
 #ifdef RT_MFMA_FILTER
     if (mfA && !bnd) {
         hipLaunchKernelGGL(rt_intersect_mfma_kernel, dim3((n + T - 1) / T), dim3(T), 0, stream, mfA,
-                           mf_nblk, grp, sph, ngroups, scene_fast, rays, n, out_i, out_t);
+                           mf_nblk, mf_qs, mf_abs, grp, sph, ngroups, scene_fast, rays, n, out_i,
+                           out_t);
         return hipGetLastError();
     }
 #else
     (void)mfA;
     (void)mf_nblk;
+    (void)mf_qs;
+    (void)mf_abs;
 #endif
     if (bnd)
         hipLaunchKernelGGL(rt_intersect_cull_kernel, dim3((n + T - 1) / T), dim3(T), 0, stream, grp,

@@ -1,18 +1,20 @@
 """The matrix-core filter's margin proof, checked numerically on the CPU.
 
 rt_dev_intersect.h intersect_world_mfma decides which spheres get the
-reference's exact test (intersect.wgsl:97-115) from two f16 hi/lo MFMA tiles:
-hb' = k1 - dn.c and v' = S' + o2.c, then H' = fma(hb', hb', v') against
-T' = (1 - m - mu')|o|^2 - 2^-20. The product is bit-exact only if that test
-is conservative: every sphere whose exact test accepts a root must have
-H' >= T'. This file restates the kernel's arithmetic in numpy -- the ray
-constants, the f16 splits, the A rows of rt_api.cpp build_mfma, the MFMA's
-16-product f32 sums in three summation orders (the hardware's is not
-documented) -- and checks that property on the adversarial ray sets of the
-GPU intersection tests (tests/raygen.py), for every (ray, sphere) pair whose
-ray lies inside the filter's range (|o_i| <= 2^12, the kernel's
-mfma_wave_ok). It also checks the error bound the proof states against the
-exact value of H.
+reference's exact test (intersect.wgsl:97-115) from one 32-term dot product
+per (sphere, ray) pair on the matrix cores: H0 = S' + L.c + sum_ab Q_ab c_a c_b
+(the VALU filter's hb^2 + S + o2.c less the ray's k1^2), every feature split
+into f16 hi/lo parts, against T0 = (1 - m - mu')|o|^2 - k1^2 - abs'. The
+product is bit-exact only if that test is conservative: every sphere whose
+exact test yields a root that can win must have H0 >= T0. This file restates
+the kernel's arithmetic in numpy -- the ray constants and features, the f16
+splits, the A rows of rt_api.cpp build_mfma (with its scale 2^sq of the
+quadratic features), the two chained MFMAs' 32-product f32 sums in four
+summation orders (the hardware's is not documented) -- and checks that
+property on the adversarial ray sets of the GPU intersection tests
+(tests/raygen.py), for every (ray, sphere) pair whose ray lies inside the
+filter's range (|o_i| <= 2^12, the kernel's mfma_wave_ok). It also checks the
+error bound the kernel's margins are built from against the exact value.
 """
 import zlib
 
@@ -23,86 +25,115 @@ from bevy_raytrace_amd import scene
 from raygen import adversarial_rays
 
 F, H16, D = np.float32, np.float16, np.float64
-M, MU, ABS = 2.0 ** -16, 2.0 ** -16, 2.0 ** -20  # rt_dev_intersect.h RT_MF_MU, RT_MF_ABS
+M, MU = 2.0 ** -16, 2.0 ** -16  # rt_dev_intersect.h m_, RT_MF_MU
 EPSILON, VERY_FAR = F(0.001), F(1e20)
+QUAD = [(0, 0), (1, 1), (2, 2), (0, 1), (0, 2), (1, 2)]
 
 
 def fma32(a, b, c):
     """f32 fma: the f64 product of two f32 is exact, one rounding to f32
-    after the add (double rounding cannot flip a comparison here by more than
-    the f64 ulp, far inside the margins)."""
+    after the add (the double rounding is far inside the margins)."""
     return (D(a) * D(b) + D(c)).astype(F)
 
 
 def split(x):
-    """split_h: hi = RN_f16(x), lo = RN_f16(x - hi) (x - hi exact in f32)."""
+    """The kernel's ray-side split: hi = RN_f16(x), lo = RN_f16(x - hi)
+    (x - hi exact in f32)."""
     x = np.asarray(x, F)
     hi = x.astype(H16).astype(F)
     lo = (x - hi).astype(H16).astype(F)
     return hi, lo
 
 
-def ray_columns(rays):
-    """The B columns u (hb) and v (v + S) of each ray, as the kernel builds
-    them; returns u, v (n, 16) f32 and T' (n,)."""
+def qscale(sp):
+    """build_mfma's sq: max |c_a c_b| 2^-sq <= 2^14."""
+    c = sp["center"].astype(F).astype(D)
+    mx = max(1.0, float(np.max(np.abs(c[:, :, None] * c[:, None, :]))))
+    sq = 0
+    while mx * 2.0 ** -sq > 2.0 ** 14:
+        sq += 1
+    return sq
+
+
+def sphere_rows(sp, sq):
+    """rt_api.cpp build_mfma: A row of each sphere (f32 values of the f16
+    parts), K = 32."""
+    c = sp["center"].astype(F).astype(D)
+    r2 = (sp["radius"] * sp["radius"]).astype(F).astype(D)  # the stored s.w = RN(r*r)
+    assert np.all(np.abs(c) <= 2.0 ** 12)  # mf_ok
+
+    def hl(x):
+        hi = x.astype(H16)
+        return hi, (x - hi.astype(D)).astype(H16)
+
+    cols = []
+    for a in range(3):
+        hi, lo = hl(c[:, a])
+        cols += [hi, hi, lo]
+    for a, b in QUAD:
+        hi, lo = hl(c[:, a] * c[:, b] * 2.0 ** -sq)
+        cols += [hi, hi, lo]
+    S = r2 - (1.0 - M - MU) * (c ** 2).sum(1)
+    assert np.all(np.abs(S) <= 2.0 ** 15)  # mf_ok
+    hi, lo = hl(S)
+    n = len(sp)
+    cols += [hi, lo] + [np.zeros(n, H16)] * 3
+    return np.stack(cols, 1).astype(F)
+
+
+def ray_constants(rays):
+    """ray_filter_consts' values as the kernel computes them: e = -dn, k1, o2,
+    |o|^2 (f32; v_rsq_f32 modelled as the correctly rounded 1/sqrt)."""
     o, d = rays[:, :3].astype(F), rays[:, 3:].astype(F)
     dd = (d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2]
-    with np.errstate(divide="ignore", invalid="ignore"):
-        rs = (1.0 / np.sqrt(D(dd))).astype(F)  # v_rsq_f32 (<= 1 ulp; covered by m)
-    dn = d * rs[:, None]
-    oo = fma32(o[:, 2], o[:, 2], fma32(o[:, 1], o[:, 1], o[:, 0] * o[:, 0]))
-    k1 = fma32(dn[:, 2], o[:, 2], fma32(dn[:, 1], o[:, 1], dn[:, 0] * o[:, 0]))
+    with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
+        rs = (1.0 / np.sqrt(D(dd))).astype(F)
+        e = -(d * rs[:, None])
+        oo = fma32(o[:, 2], o[:, 2], fma32(o[:, 1], o[:, 1], o[:, 0] * o[:, 0]))
+        k1 = fma32(-e[:, 2], o[:, 2], fma32(-e[:, 1], o[:, 1], -e[:, 0] * o[:, 0]))
     two = F(2.0) * (F(1.0) - F(M))
-    T = F(1.0 - M - MU) * oo - F(ABS)
-    z = np.zeros(len(rays), F)
-    one = np.ones(len(rays), F)
-    xh, xl = split(-dn[:, 0])
-    yh, yl = split(-dn[:, 1])
-    zh, zl = split(-dn[:, 2])
-    kh, kl = split(k1)
-    ph, pl = split(two * o[:, 0])
-    qh, ql = split(two * o[:, 1])
-    rh, rl = split(two * o[:, 2])
-    u = np.stack([xh, xh, xl, yh, yh, yl, zh, zh, zl, kh, kl, z, z, z, z, z], 1)
-    v = np.stack([ph, ph, pl, qh, qh, ql, rh, rh, rl, z, z, one, one, z, z, z], 1)
-    return u, v, T
+    return o, e, k1, oo, two * o
 
 
-def sphere_rows(sp):
-    """rt_api.cpp build_mfma: A row of sphere j (f32 values of the f16 parts)."""
-    c = sp["center"].astype(F)
-    r2 = (sp["radius"] * sp["radius"]).astype(F)  # the stored s.w = RN(r*r)
-    rows = []
-    for a in range(3):
-        hi = c[:, a].astype(H16)
-        lo = (D(c[:, a]) - D(hi)).astype(H16)
-        rows += [hi, lo, hi]
-    cc = (D(c) ** 2).sum(1)
-    S = D(r2) - (1.0 - 2.0 ** -16 - 2.0 ** -16) * cc
-    assert np.all(np.abs(S) <= 2.0 ** 15) and np.all(np.abs(c) <= 2.0 ** 12)  # mf_ok
-    sh = S.astype(H16)
-    sl = (S - D(sh)).astype(H16)
-    n = len(sp)
-    rows += [np.ones(n, H16), np.ones(n, H16), sh, sl] + [np.zeros(n, H16)] * 3
-    return np.stack(rows, 1).astype(F)  # (n, 16)
+def ray_columns(rays, sq, abs_margin):
+    """The ray column (n, 32) and threshold T0 (n,), as the kernel builds them."""
+    o, e, k1, oo, o2 = ray_constants(rays)
+    sc = F(2.0 ** sq)
+    with np.errstate(invalid="ignore", over="ignore"):
+        feats = [fma32(F(2.0) * k1, e[:, a], o2[:, a]) for a in range(3)]
+        feats += [((F(2.0) * e[:, a] if a != b else e[:, a]) * e[:, b]) * sc for a, b in QUAD]
+        T0 = (fma32(-k1, k1, F(1.0 - M - MU) * oo) - F(abs_margin)).astype(F)
+    cols = []
+    for x in feats:
+        hi, lo = split(x)
+        cols += [hi, lo, hi]
+    one, z = np.ones(len(rays), F), np.zeros(len(rays), F)
+    cols += [one, one, z, z, z]
+    return np.stack(cols, 1), T0
 
 
 def mfma_sum(A, B, order):
     """sum_k A[j,k] B[i,k] -> (rays, spheres) f32. Each product is exact in
-    f32 (two f16); the 16-term sum is rounded per the order."""
-    P = A[None, :, :].astype(D) * B[:, None, :].astype(D)  # (rays, spheres, 16) exact
+    f32 (two f16); the 32-term sum is rounded per the order ("chained": two
+    16-term sums, the second accumulating onto the first, as two MFMAs)."""
+    P = A[None, :, :].astype(D) * B[:, None, :].astype(D)
     if order == "exact":
         return P.sum(-1).astype(F)
+    if order == "chained":
+        return (P[..., :16].sum(-1).astype(F).astype(D) + P[..., 16:].sum(-1)).astype(F)
     if order == "pairwise":
         P = P.astype(F)
         while P.shape[-1] > 1:
             P = (P[..., 0::2] + P[..., 1::2]).astype(F)
         return P[..., 0]
-    ks = range(16) if order == "forward" else range(15, -1, -1)
+    ks = range(32) if order == "forward" else range(31, -1, -1)
     acc = np.zeros(P.shape[:2], F)
     for k in ks:
         acc = (acc + P[..., k].astype(F)).astype(F)
     return acc
+
+
+ORDERS = ("exact", "chained", "pairwise", "forward", "backward")
 
 
 def exact_hits(sp, rays):
@@ -140,62 +171,54 @@ SCENES = {
 }
 
 
+def _rays(sp, name, n):
+    rays = adversarial_rays(sp, n, seed=zlib.crc32(name.encode()) % 1000)
+    return rays[np.abs(rays[:, :3]).max(1) <= 2.0 ** 12]  # mfma_wave_ok
+
+
 @pytest.mark.parametrize("name", sorted(SCENES))
 def test_matrix_core_filter_is_conservative(name):
     sp = SCENES[name]()
-    n = 16_000 if len(sp) < 1000 else 4_000
-    rays = adversarial_rays(sp, n, seed=zlib.crc32(name.encode()) % 1000)
-    inside = np.abs(rays[:, :3]).max(1) <= 2.0 ** 12  # mfma_wave_ok
-    rays = rays[inside]
-    u, v, T = ray_columns(rays)
-    A = sphere_rows(sp)
+    rays = _rays(sp, name, 12_000 if len(sp) < 1000 else 3_000)
+    sq = qscale(sp)
+    B, T0 = ray_columns(rays, sq, 2.0 ** (sq - 20))
+    A = sphere_rows(sp, sq)
     hits = exact_hits(sp, rays)
     assert hits.sum() > 1000  # the set really has hits to lose
-    checked = 0
-    for order in ("exact", "pairwise", "forward", "backward"):
+    for order in ORDERS:
         for j0 in range(0, len(sp), 256):
-            Aj = A[j0:j0 + 256]
-            hb = mfma_sum(Aj, u, order)
-            vs = mfma_sum(Aj, v, order)
             with np.errstate(invalid="ignore", over="ignore"):
-                Hp = fma32(hb, hb, vs)
-                cand = Hp >= T[:, None]
+                cand = mfma_sum(A[j0:j0 + 256], B, order) >= T0[:, None]
             lost = hits[:, j0:j0 + 256] & ~cand
             assert not lost.any(), (
                 f"{order}: {int(lost.sum())} exact hits filtered out, e.g. ray "
                 f"{np.argwhere(lost)[0].tolist()}")
-            checked += int(hits[:, j0:j0 + 256].sum())
-    assert checked > 4000
 
 
 @pytest.mark.parametrize("name", ["rtiow", "spheres10k"])
-def test_split_error_within_stated_bound(name):
-    """|H' - H~| <= 2^-17 (|o|^2 + |c|^2) + 2^-20.3 r^2 + 2^-21, the bound the
-    kernel's margins are built from (rt_dev_intersect.h), where H~ is the
-    exact value of hb~^2 + S' + o2.c with the kernel's f32 ray constants."""
+def test_error_within_stated_bound(name):
+    """|(H0' - T0') - (H~ - T~)| <= 2^-16.3 (|o|^2 + |c|^2) + 2^-19 |S'| + abs',
+    the bound of rt_dev_intersect.h's margin comment, where H~ - T~ is the
+    exact value of hb^2 + S' + o2.c - (1 - m - mu')|o|^2 with the kernel's f32
+    ray constants e, k1, o2 (hb = k1 + e.c)."""
     sp = SCENES[name]()
-    rays = adversarial_rays(sp, 4_000, seed=7)
-    rays = rays[np.abs(rays[:, :3]).max(1) <= 2.0 ** 12]
+    rays = _rays(sp, "bound" + name, 3_000)
     rays = rays[np.isfinite(rays).all(1) & (np.abs(rays[:, 3:]).max(1) > 0)]
-    u, v, _ = ray_columns(rays)
-    # exact operands: the unsplit f32 ray constants and the f32 sphere values
-    xs = u[:, 0] + u[:, 2], u[:, 3] + u[:, 5], u[:, 6] + u[:, 8]
-    o2 = v[:, 0] + v[:, 2], v[:, 3] + v[:, 5], v[:, 6] + v[:, 8]
-    o = rays[:, :3].astype(D)
-    c = sp["center"].astype(D)
+    sq = qscale(sp)
+    absm = 2.0 ** (sq - 20)
+    B, T0 = ray_columns(rays, sq, absm)
+    o, e, k1, _, o2 = ray_constants(rays)
+    c = sp["center"].astype(F).astype(D)
     r2 = (sp["radius"] * sp["radius"]).astype(F).astype(D)
-    S = r2 - (1.0 - 2.0 ** -15) * (c ** 2).sum(1)
-    k1 = D(u[:, 9]) + D(u[:, 10])
-    hb_x = k1[:, None] + sum(D(xs[a])[:, None] * c[None, :, a] for a in range(3))
-    v_x = S[None, :] + sum(D(o2[a])[:, None] * c[None, :, a] for a in range(3))
-    H_x = hb_x * hb_x + v_x
-    A = sphere_rows(sp)
+    S = r2 - (1.0 - M - MU) * (c ** 2).sum(1)
+    oo = (o.astype(D) ** 2).sum(1)
+    hb = k1.astype(D)[:, None] + e.astype(D) @ c.T
+    exact = hb * hb + S[None, :] + o2.astype(D) @ c.T - (1.0 - M - MU) * oo[:, None]
+    bound = (2.0 ** -16.3 * (oo[:, None] + (c ** 2).sum(1)[None, :]) + 2.0 ** -19 * np.abs(S)[None, :]
+             + absm)
+    A = sphere_rows(sp, sq)
     worst = 0.0
-    for order in ("exact", "pairwise", "forward", "backward"):
-        hb = mfma_sum(A, u, order)
-        vs = mfma_sum(A, v, order)
-        Hp = fma32(hb, hb, vs).astype(D)
-        bound = (2.0 ** -17 * ((o ** 2).sum(1)[:, None] + (c ** 2).sum(1)[None, :])
-                 + 2.0 ** -20.3 * r2[None, :] + 2.0 ** -21)
-        worst = max(worst, float(np.max(np.abs(Hp - H_x) / bound)))
+    for order in ORDERS:
+        got = mfma_sum(A, B, order).astype(D) - T0.astype(D)[:, None]
+        worst = max(worst, float(np.max(np.abs(got - exact) / bound)))
     assert worst < 1.0, worst
