@@ -684,6 +684,32 @@ __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, ui
     }
 }
 
+// The four group maxima of a tile's 16 values and the tile's maximum, as
+// v_max3 / v_max (10 VALU): fmaxf on MFMA results makes the compiler
+// canonicalise every operand first (v_max x, x: 18 VALU), since it cannot
+// prove them canonical. v_max3 drops a quiet-NaN operand like fmaxf; a NaN
+// H0 is never a candidate either way (its compare is false). H comes straight
+// from the MFMAs and hipcc pads no hazard into inline asm, so the block opens
+// with the 12 wait states the compiler itself puts between the 8-pass
+// v_mfma_f32_32x32x16_f16 and a VALU reading its result (s_nop 11).
+__device__ __forceinline__ void tile_max(const f16x& H, float* gq, float& g) {
+    asm("s_nop 11\n\t"
+        "v_max3_f32 %0, %5, %6, %7\n\t"
+        "v_max3_f32 %1, %9, %10, %11\n\t"
+        "v_max3_f32 %2, %13, %14, %15\n\t"
+        "v_max3_f32 %3, %17, %18, %19\n\t"
+        "v_max_f32 %0, %0, %8\n\t"
+        "v_max_f32 %1, %1, %12\n\t"
+        "v_max_f32 %2, %2, %16\n\t"
+        "v_max_f32 %3, %3, %20\n\t"
+        "v_max3_f32 %4, %0, %1, %2\n\t"
+        "v_max_f32 %4, %4, %3"
+        : "=&v"(gq[0]), "=&v"(gq[1]), "=&v"(gq[2]), "=&v"(gq[3]), "=&v"(g)
+        : "v"(H[0]), "v"(H[1]), "v"(H[2]), "v"(H[3]), "v"(H[4]), "v"(H[5]), "v"(H[6]),
+          "v"(H[7]), "v"(H[8]), "v"(H[9]), "v"(H[10]), "v"(H[11]), "v"(H[12]), "v"(H[13]),
+          "v"(H[14]), "v"(H[15]));
+}
+
 // Called by the whole wave (the MFMA operands span all 64 lanes): lanes
 // without a ray (live false) trace a dummy ray whose threshold is +inf.
 // mf_qs = 2^sq, mf_abs = abs' (build_mfma).
@@ -808,11 +834,8 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
                 __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, t ? B10 : B00, zero, 0, 0, 0), 0, 0, 0);
             const float Tt = t ? T1 : T0;
             // per-group maxima (the lane's 4 groups of 4 spheres), then the tile's
-            float gq[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                gq[q] = fmaxf(fmaxf(H[4 * q], H[4 * q + 1]), fmaxf(H[4 * q + 2], H[4 * q + 3]));
-            const float g = fmaxf(fmaxf(gq[0], gq[1]), fmaxf(gq[2], gq[3]));
+            float gq[4], g;
+            tile_max(H, gq, g);
             if (rt_ballot(g >= Tt) != 0) {
                 PROF_ADD(5, 1);  // tiles with a candidate
                 uint32_t& cnt = t ? cnt1 : cnt0;
