@@ -1035,10 +1035,20 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     K_.div_npix = make_fastdiv(npix ? npix : 1);
     K_.div_width = make_fastdiv(p.width);
     K_.div_row_block = make_fastdiv(B);
-    K_.tile_full_rows = rows / 8;
-    K_.tile_full_cols = p.width / 8;
-    K_.tile_wrem = p.width % 8;
-    K_.div_8w = make_fastdiv(8 * p.width);
+    // processing order: tiles of tile_h x tile_w pixels (8 x 8 for a whole
+    // image; a shard's tiles are one row block high, so a tile's pixels stay
+    // neighbours in the image -- 8 packed shard rows would span two blocks
+    // shard_count x row_block rows apart). Only the work order changes: every
+    // pixel's result is its own.
+    const uint32_t th = (K > 1 && B < 8) ? B : 8, tw = (64 + th - 1) / th;
+    K_.tile_h = th;
+    K_.tile_w = tw;
+    K_.tile_full_rows = rows / th;
+    K_.tile_full_cols = p.width / tw;
+    K_.tile_wrem = p.width % tw;
+    K_.div_thw = make_fastdiv(th * p.width);
+    K_.div_tp = make_fastdiv(th * tw);
+    K_.div_tw = make_fastdiv(tw);
     K_.div_wrem = make_fastdiv(K_.tile_wrem ? K_.tile_wrem : 1);
     K_.prefetch = tn.prefetch ? 1u : 0u;
     K_.prio_mode = tn.prio_mode;

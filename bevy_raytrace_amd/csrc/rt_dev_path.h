@@ -63,32 +63,35 @@ __device__ __forceinline__ void pixel_xy(const KParams& P, uint32_t p, uint32_t&
 }
 
 // k-th pixel of a block in processing order -> shard-local pixel index
-// (row-major). Order: 8x8 tiles, so the 64 lanes of a wave trace a compact
-// patch of the image (coherent rays: fewer sphere groups with a candidate in
-// the wave); tile rows run bottom-up so the queue ends on the cheap sky rows.
+// (row-major). Order: tile_h x tile_w tiles (8 x 8; a shard's tiles one row
+// block high, rt_api.cpp), so the 64 lanes of a wave trace a compact patch of
+// the image (coherent rays: fewer sphere groups with a candidate in the wave);
+// tile rows run bottom-up so the queue ends on the cheap sky rows.
 __device__ __forceinline__ uint32_t order_to_pixel(const KParams& P, uint32_t k) {
     k = P.npix - 1 - k;
-    const uint32_t W = P.width;
-    const uint32_t tiled = P.tile_full_rows * 8 * W;
+    const uint32_t W = P.width, th = P.tile_h, tw = P.tile_w;
+    const uint32_t tiled = P.tile_full_rows * th * W;
     uint32_t x, r;
     if (k < tiled) {
-        const uint32_t tr = fdiv(k, P.div_8w);
-        const uint32_t rem = k - tr * 8 * W;
-        const uint32_t tx = rem >> 6;
+        const uint32_t tr = fdiv(k, P.div_thw);
+        const uint32_t rem = k - tr * th * W;
+        const uint32_t tx = fdiv(rem, P.div_tp);
         if (tx < P.tile_full_cols) {
-            x = tx * 8 + (rem & 7);
-            r = tr * 8 + ((rem >> 3) & 7);
+            const uint32_t j = rem - tx * th * tw;
+            const uint32_t jr = fdiv(j, P.div_tw);
+            x = tx * tw + (j - jr * tw);
+            r = tr * th + jr;
         } else {  // the narrow last tile of the tile row
-            const uint32_t j = rem - P.tile_full_cols * 64;
+            const uint32_t j = rem - P.tile_full_cols * th * tw;
             const uint32_t jr = fdiv(j, P.div_wrem);
-            x = P.tile_full_cols * 8 + (j - jr * P.tile_wrem);
-            r = tr * 8 + jr;
+            x = P.tile_full_cols * tw + (j - jr * P.tile_wrem);
+            r = tr * th + jr;
         }
     } else {
         const uint32_t j = k - tiled;
         const uint32_t jr = fdiv(j, P.div_width);
         x = j - jr * W;
-        r = P.tile_full_rows * 8 + jr;
+        r = P.tile_full_rows * th + jr;
     }
     return r * W + x;
 }

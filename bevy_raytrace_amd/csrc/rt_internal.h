@@ -73,12 +73,14 @@ struct KParams {
     float coc;             // lens_focal_length / (2 * fstop), generate.wgsl:97 (thin-lens flag)
     FastDiv div_npix, div_width, div_row_block;
     uint32_t tail_start;   // queue position from which waves take RT_WAVE_CHUNK_TAIL items
-    // processing order of a block's pixels: 8x8 tiles (rows of tiles), then the
-    // rows % 8 leftover rows row-major
-    uint32_t tile_full_rows;  // rows / 8
-    uint32_t tile_full_cols;  // width / 8
-    uint32_t tile_wrem;       // width % 8
-    FastDiv div_8w, div_wrem;
+    // processing order of a pass's pixels: tile_h x tile_w tiles (rows of
+    // tiles, each tile row-major inside), then the rows % tile_h leftover rows
+    // row-major (rt_dev_path.h order_to_pixel)
+    uint32_t tile_h, tile_w;
+    uint32_t tile_full_rows;  // rows / tile_h
+    uint32_t tile_full_cols;  // width / tile_w
+    uint32_t tile_wrem;       // width % tile_w
+    FastDiv div_thw, div_tp, div_tw, div_wrem;  // by tile_h * width, tile_h * tile_w, tile_w, tile_wrem
     uint32_t prefetch;  // 1: waves prefetch their next work chunk (knob prefetch)
     uint32_t prio_mode;   // s_setprio rotation (knob prio_mode): 0 off, 1 by iteration, 3 by wall time
     uint32_t prio_shift;  // mode 3: one step per 2^prio_shift ticks of 10 ns (knob prio_shift)
