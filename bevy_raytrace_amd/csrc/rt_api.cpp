@@ -68,7 +68,7 @@ struct Tuning {
     size_t scratch_bytes = (size_t)16 << 30;  // block sums per launch (of 288 GB HBM)
     bool split_all = false;       // without primary reuse, every block as single samples
     bool tail_split = true;       // single-sample tail items at the end of a launch
-    double tail[3] = {0.0, 0.0, 12.0};  // tail regions (4-, 2-, 1-sample items) x D x lanes
+    double tail[3] = {0.0, 0.0, 6.0};  // tail regions (4-, 2-, 1-sample items) x D x lanes
     double block_region = 96.0;   // single-block items before the tail, x D x lanes samples
     bool prefetch = true;         // waves prefetch their next work chunk
     uint32_t prio_mode = 1;       // s_setprio rotation: 0 off, 1 by iteration, 3 by wall time
@@ -889,8 +889,8 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     const size_t per_block = (size_t)npix * sizeof(float4);  // one slot per pixel
     // Tail: per lane ~a1*D single samples, and before them optionally a2*D
     // samples in 2-sample items and a4*D in 4-sample items (knob tail="a4,a2,a1";
-    // default 0,0,12 = single samples only, the measured best on the RTIOW
-    // frames): a block item (<= 8*D iterations) taken before the tail has
+    // default 0,0,6 = single samples only, the measured best on the RTIOW
+    // frames and N=8 shards with the matrix-core kernel; 0,0,12 before it): a block item (<= 8*D iterations) taken before the tail has
     // finished when the queue runs dry, and an item taken in the tail leaves
     // at most one short path per lane to drain. In samples per pixel:
     const Tuning& tn = ctx->tune;

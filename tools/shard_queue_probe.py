@@ -20,7 +20,7 @@ N = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 FPL = int(sys.argv[3]) if len(sys.argv) > 3 else 24
 REPS = int(sys.argv[4]) if len(sys.argv) > 4 else 4
-SETTINGS = sys.argv[5:] or ["br=96,tail=0:0:12"]
+SETTINGS = sys.argv[5:] or ["br=96,tail=0:0:6"]
 
 wl = configs.WORKLOADS[configs.HEADLINE]
 sc = wl.make_scene()
