@@ -43,6 +43,9 @@ pub const RT_FLAG_JITTER: u32 = 0x2;
 pub const RT_FLAG_THIN_LENS: u32 = 0x4;
 /// Culled sphere list: identical hits, less filter work (rt_hip.h).
 pub const RT_FLAG_CULL: u32 = 0x8;
+/// The packed-fp32 VALU filter instead of the matrix-core one: identical hits
+/// (rt_hip.h; A/B and cross-checks).
+pub const RT_FLAG_VALU_FILTER: u32 = 0x10;
 
 extern "C" {
     pub fn rt_version() -> c_int;

@@ -178,3 +178,21 @@ def test_bench_spawn_relays_rank0_line(monkeypatch, capsys):
     out = capsys.readouterr()
     assert out.out.strip() == '{"metric": "m", "value": 1.0}'
     assert "RCCL banner" in out.err
+
+
+def test_flag_constants_agree_across_bindings():
+    """Every RT_FLAG_* of include/rt_hip.h has the same value in the Python
+    binding (bevy_raytrace_amd/abi.py) and the Rust drop-in (bevy_shim/src/rt_hip.rs)."""
+    import re
+    from bevy_raytrace_amd import abi
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    hdr = open(os.path.join(root, "include", "rt_hip.h")).read()
+    flags = {m.group(1): int(m.group(2), 16) for m in
+             re.finditer(r"#define (RT_FLAG_\w+)\s+0x([0-9a-fA-F]+)u", hdr)}
+    rs = open(os.path.join(root, "bevy_shim", "src", "rt_hip.rs")).read()
+    rflags = {m.group(1): int(m.group(2), 16) for m in
+              re.finditer(r"pub const (RT_FLAG_\w+): u32 = 0x([0-9a-fA-F]+);", rs)}
+    assert len(flags) >= 5
+    for name, v in flags.items():
+        assert getattr(abi, name) == v, name
+        assert rflags.get(name) == v, name
