@@ -271,21 +271,23 @@ def main():
         if packed is not None:
             shard[:nf, :len(rows)].copy_(packed[:nf])
         if dist_on:
+            # rank k's nf frames land as slab k of a (world, nf, max_rows, W)
+            # view, the layout rt_assemble_shard_frames reads: one assembly
+            # launch for the launch's frames
+            g = (gathered.view(-1)[:world * nf * max_rows * W * 4].view(world, nf, max_rows, W, 4)
+                 if rank == 0 else None)
             if args.dist_backend == "nccl":
-                dist.gather(shard[:nf], [gathered[k, :nf] for k in range(world)] if rank == 0
-                            else None, dst=0)
+                dist.gather(shard[:nf], [g[k] for k in range(world)] if rank == 0 else None, dst=0)
             else:  # rehearsal: host-staged gather
                 host = shard[:nf].cpu()
                 parts = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
                 dist.gather(host, parts, dst=0)
                 if rank == 0:
                     for k in range(world):
-                        gathered[k, :nf].copy_(parts[k])
+                        g[k].copy_(parts[k])
             if rank == 0:
-                for fi in range(nf):
-                    slabs = gathered[:, fi].contiguous()
-                    r.assemble_shards(slabs.data_ptr(), max_rows, image[fi].data_ptr(), W, H, B,
-                                      world, stream=stream.cuda_stream)
+                r.assemble_shard_frames(g.data_ptr(), max_rows, nf, image.data_ptr(), W, H, B,
+                                        world, stream=stream.cuda_stream)
 
     def run(nsteps, flags):
         """nsteps frames in launches of <= FPL frames (near-equal sizes), two

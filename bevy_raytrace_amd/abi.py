@@ -127,6 +127,8 @@ _PROTOS = {
     "rt_render_async": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(RtParams), _VP]),
     "rt_wait": (ctypes.c_int, [_VP, ctypes.POINTER(RtStats)]),
     "rt_assemble_shards": (ctypes.c_int, [_VP, _VP, _U32, _VP, _U32, _U32, _U32, _U32, _VP]),
+    "rt_assemble_shard_frames": (ctypes.c_int,
+                                 [_VP, _VP, _U32, _U32, _VP, _U32, _U32, _U32, _U32, _VP]),
     "rt_intersect": (ctypes.c_int, [_VP, _VP, _U32, _VP, _VP]),
     "rt_intersect_ex": (ctypes.c_int, [_VP, _VP, _U32, _U32, _VP, _VP]),
     "rt_update_spheres": (ctypes.c_int, [_VP, _U32, _VP, _U32]),

@@ -638,14 +638,16 @@ static int quiesce(rt_ctx* ctx) {  // no kernel may be reading the scene while i
 //   K 0..8   c_a          [hi, hi, lo] for a = x, y, z
 //   K 9..26  c_a c_b 2^-sq [hi, hi, lo] for ab = xx, yy, zz, xy, xz, yz
 //   K 27, 28 S' = r^2 - (1 - m - mu')|c|^2  [hi, lo]
-//   K 29..31 0
-// (the ray column holds the partner parts [hi, lo, hi], and 1, 1 against S').
+//   K 29, 30 1, 1                         (against the ray's T0 hi, lo)
+//   K 31     0
+// (the ray column holds the negated partner parts [hi, lo, hi], -1, -1 against
+// S' and T0's parts: the MFMAs give T0 - H0, rt_dev_intersect.h).
 // hi = RN_f16(x), lo = RN_f16(x - hi), all from double. sq scales the
 // quadratic features into f16 range (max |c_a c_b| 2^-sq <= 2^14); the ray
 // side carries 2^sq. Block b (spheres 32b..32b+31): two uint4 per lane, A0
 // (K 0..15) then A1 (K 16..31), 64 lanes each; lane l: row l & 31, elements
-// k = 8 (l >> 5) .. + 8 of that half. Pad rows: 0, S'_hi = -inf (H0 = -inf or
-// NaN: never a candidate). Only scenes with |c_i| <= 2^12 and |S'| <= 2^15
+// k = 8 (l >> 5) .. + 8 of that half. Pad rows: 0, S'_hi = -inf (T0 - H0 =
+// +inf or NaN: never a candidate). Only scenes with |c_i| <= 2^12 and |S'| <= 2^15
 // take it (mf_ok); the rest keep the VALU filter.
 static uint16_t f16_bits(double x) {
     const _Float16 h = (_Float16)x;
@@ -709,6 +711,7 @@ static int build_mfma(rt_ctx* ctx) {
             } else {
                 row[27] = f16_bits(-INFINITY);
             }
+            row[29] = row[30] = f16_bits(1.0);  // against the ray's T0 hi, lo
             for (int half = 0; half < 2; ++half)  // A0: K 0..15, A1: K 16..31
                 std::memcpy(&h[(((size_t)b * 2 + half) * 64 + l) * 8], &row[16 * half + 8 * hh], 16);
         }
@@ -734,7 +737,10 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n, const rt_mat
     rc = check_spheres(ctx, spheres, 0, n, m);
     if (rc) return rc;
     const uint32_t ngroups = (n + RT_GROUP - 1) / RT_GROUP;
-    const size_t nrec = (size_t)(ngroups + 1) * RT_GROUP;
+    // + one pad group (the VALU walk's), and whole 32-sphere blocks: the
+    // matrix-core walk may queue a pad row of its last block (a NaN ray),
+    // whose record always misses
+    const size_t nrec = std::max((size_t)(ngroups + 1) * RT_GROUP, (size_t)(n + 31) / 32 * 32);
     ctx->h_sph.assign(nrec, make_float4(0.0f, 0.0f, 0.0f, -INFINITY));
     ctx->h_S.assign(nrec, -INFINITY);
     ctx->h_rm.assign(n ? n : 1, make_float2(0.0f, 0.0f));
@@ -1332,24 +1338,40 @@ int rt_encode_srgb8(rt_ctx* ctx, const float* rgba_device, uint8_t* rgba8_device
     return RT_OK;
 }
 
-int rt_assemble_shards(rt_ctx* ctx, const float* gathered_device, uint32_t max_rows,
-                       float* image_device, uint32_t width, uint32_t height, uint32_t row_block,
-                       uint32_t shard_count, void* stream) {
-    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_assemble_shards: ctx is NULL");
-    if (!gathered_device || !image_device || width == 0 || height == 0 || shard_count == 0)
-        return fail(ctx, RT_ERR_INVALID_ARG, "rt_assemble_shards: bad arguments");
+static int assemble(rt_ctx* ctx, const char* fn, const float* gathered_device, uint32_t max_rows,
+                    uint32_t frames, float* image_device, uint32_t width, uint32_t height,
+                    uint32_t row_block, uint32_t shard_count, void* stream) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "%s: ctx is NULL", fn);
+    if (!gathered_device || !image_device || width == 0 || height == 0 || shard_count == 0 ||
+        frames == 0 || frames > 65535)
+        return fail(ctx, RT_ERR_INVALID_ARG, "%s: bad arguments", fn);
     const uint32_t B = row_block ? row_block : 1;
     for (uint32_t k = 0; k < shard_count; ++k)
         if (rt_shard_rows(height, B, shard_count, k) > max_rows)
-            return fail(ctx, RT_ERR_INVALID_ARG, "rt_assemble_shards: shard %u has more than %u rows",
-                        k, max_rows);
+            return fail(ctx, RT_ERR_INVALID_ARG, "%s: shard %u has more than %u rows", fn, k,
+                        max_rows);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
     HIP_TRY(ctx, rt_launch_assemble(reinterpret_cast<const float4*>(gathered_device), max_rows,
-                                    reinterpret_cast<float4*>(image_device), width, height, B,
-                                    shard_count, s));
+                                    frames, reinterpret_cast<float4*>(image_device), width,
+                                    height, B, shard_count, s));
     if (!stream) HIP_TRY(ctx, hipStreamSynchronize(s));
     return RT_OK;
+}
+
+int rt_assemble_shards(rt_ctx* ctx, const float* gathered_device, uint32_t max_rows,
+                       float* image_device, uint32_t width, uint32_t height, uint32_t row_block,
+                       uint32_t shard_count, void* stream) {
+    return assemble(ctx, "rt_assemble_shards", gathered_device, max_rows, 1u, image_device, width,
+                    height, row_block, shard_count, stream);
+}
+
+int rt_assemble_shard_frames(rt_ctx* ctx, const float* gathered_device, uint32_t max_rows,
+                             uint32_t frames, float* image_device, uint32_t width,
+                             uint32_t height, uint32_t row_block, uint32_t shard_count,
+                             void* stream) {
+    return assemble(ctx, "rt_assemble_shard_frames", gathered_device, max_rows, frames,
+                    image_device, width, height, row_block, shard_count, stream);
 }
 
 int rt_intersect(rt_ctx* ctx, const float* rays, uint32_t n, int32_t* hit_index, float* hit_t) {

@@ -609,33 +609,43 @@ __device__ __forceinline__ uint32_t lanemask_lt_count(uint64_t m) {
 // threshold it is ONE dot product of a sphere row and a ray column:
 //   H - k1^2 = H0 = S' + L.c + sum_ab Q_ab c_a c_b,
 //   L_a = 2 k1 e_a + o2_a,  Q_aa = e_a^2,  Q_ab = 2 e_a e_b (a < b),
-// candidate iff H0 >= T0 = (1 - m - mu')|o|^2 - k1^2 - abs'. Each of the 10
-// features is split into f16 hi/lo parts (x = hi + lo + err): 3 products
-// (hi.hi + hi.lo + lo.hi) per feature, 2 for S' against an exact 1 -- 29 of
-// K = 32 (rt_api.cpp build_mfma: the A rows and their layout). Per 32-sphere
-// block b and 32-ray half t of the wave, two chained v_mfma_f32_32x32x16_f16
-// give H0 for the 32 x 32 (sphere, ray) pairs straight into VGPRs; the VALU
-// only takes maxima and compares. Output layout (MI355X guide): lane l holds
-// column (ray) l & 31 of the half, rows (spheres) (i & 3) + 8 (i >> 2) +
-// 4 (l >> 5) in register i: four whole groups of 4 spheres per lane. A lane
-// queues (group-of-4 index << 4 | 4-bit mask) per half; the ray's lane drains
-// the entries of its column's two lanes, in any order, with the (t, index)
-// tie-break (exact_body LEX).
+// candidate iff H0 >= T0 = (1 - m - mu')|o|^2 - k1^2 - abs'. The threshold is
+// one more term of the same dot product: the MFMAs give V = T0 - H0 straight
+// (the ray column holds the NEGATED features, -1 against S', and T0's own
+// hi/lo parts against two exact 1s in the sphere row), and a sphere is a
+// candidate iff V < 0. Each of the 10 features and T0 is split into f16
+// hi/lo parts (x = hi + lo + err): 3 products (hi.hi + hi.lo + lo.hi) per
+// feature, 2 for S' and 2 for T0 against exact 1s -- 31 of K = 32 (rt_api.cpp
+// build_mfma: the A rows and their layout). Per 32-sphere block b and 32-ray
+// half t of the wave, two chained v_mfma_f32_32x32x16_f16 give V for the
+// 32 x 32 (sphere, ray) pairs straight into VGPRs; the VALU only ORs them
+// (a tile or group with a candidate has a value with the sign bit set) and
+// compares. Output layout (MI355X guide): lane l holds column (ray) l & 31 of
+// the half, rows (spheres) (i & 3) + 8 (i >> 2) + 4 (l >> 5) in register i:
+// four whole groups of 4 spheres per lane. A lane queues (group-of-4 index
+// << 4 | 4-bit mask) per half; the ray's lane drains the entries of its
+// column's two lanes, in any order, with the (t, index) tie-break (exact_body
+// LEX).
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef float f16x __attribute__((ext_vector_type(16)));
 // Margins. Split: |x - hi - lo| <= 2^-22|x| + 2^-25 (lo may be subnormal), so
 // a feature product is within 3 * 2^-22|a||b| + 2^-25(|a| + |b|) of a b, and
 // sum_f |a_f||b_f| <= 4|o||c| + |c|^2 + |S'| (|L| <= 4|o|, sum |Q c c| =
-// (sum |e_a c_a|)^2 <= |c|^2): <= 2^-18.8 (|o|^2 + |c|^2) + 2^-20.4 |S'|. The
-// f32 sums of the 29 exact products (two chained MFMAs, 31 roundings at most)
-// add <= 31 * 2^-24 of the same magnitudes: <= 2^-17.4 (|o|^2 + |c|^2) +
-// 2^-19 |S'|. The ray features' own roundings (one fma for L, two products for
-// Q, the fma of T0) add <= 2^-21 (|o|^2 + |c|^2), and the ray constants dn, k1,
-// o2 are the VALU filter's (<= 25 * 2^-24 (|o|^2 + |c|^2), ray_filter_consts).
-// Total <= 2^-16.3 (|o|^2 + |c|^2) < mu' = 2^-16 in |o|^2 + |c|^2; the |S'| <=
-// r^2 + |c|^2 part goes to the m margin's slack (2^-16 - 35 * 2^-24) and mu';
-// the absolute parts, 2^-25 x (the ray features scaled by 2^sq <= 2^(sq+1),
-// the linear ones <= 4|o|), to abs' = 2^(sq - 20) (rt_api.cpp: mf_abs).
+// (sum |e_a c_a|)^2 <= |c|^2): <= 2^-18.8 (|o|^2 + |c|^2) + 2^-20.4 |S'|; T0's
+// split adds <= 2^-22 |o|^2 + 2^-25 (|T0| <= |o|^2). The f32 sums of the 31
+// exact products (two chained MFMAs, 33 roundings at most, each <= 2^-24 of
+// sum |p| <= 4.1 (|o|^2 + |c|^2) + |S'|) add <= 2^-16.9 (|o|^2 + |c|^2) +
+// 2^-19 |S'| (measured: <= 4.9 * 2^-24 sum |p|, profiles/r02_mfma_acc.log).
+// The ray features' own roundings (one fma for L, two products for Q, the
+// fma of T0) add <= 2^-21 (|o|^2 + |c|^2), and the ray constants dn, k1, o2
+// are the VALU filter's (<= 25 * 2^-24 (|o|^2 + |c|^2), ray_filter_consts).
+// Total <= 2^-16.02 (|o|^2 + |c|^2) < mu' = 2^-16 in |o|^2 + |c|^2, so a
+// sphere the exact test can hit has V <= -(slack) < 0 (never a signed zero);
+// the |S'| <= r^2 + |c|^2 part goes to the m margin's slack (2^-16 - 35 *
+// 2^-24) and mu'; the absolute parts, 2^-25 x (the ray features scaled by
+// 2^sq <= 2^(sq+1), the linear ones <= 4|o|, T0's lo), to abs' = 2^(sq - 20)
+// (rt_api.cpp: mf_abs). Range: |c_i| <= 2^12, |S'| <= 2^15 (build_mfma) and
+// per wave |o_i| <= 2^12, |o|^2 <= 2^15 (mfma_wave_ok: T0 in f16 range).
 // tests/test_mfma_filter.py restates this arithmetic and checks it.
 #define RT_MF_MU 0x1p-16f
 #define RT_MF_CAP 8  // queue entries per lane and half (LDS)
@@ -645,9 +655,11 @@ __device__ __forceinline__ uint32_t bperm(uint32_t src_lane, uint32_t v) {
 }
 
 // the wave may use the f16 filter: every live lane's |o| within the split's range
+// (and |o|^2 <= 2^15, so the threshold T0 <= |o|^2 splits into f16 parts)
 __device__ __forceinline__ bool mfma_wave_ok(v3 o, bool live) {
     const float om = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
-    return rt_ballot(live && !(om <= 0x1p12f)) == 0;
+    const float oo = __builtin_fmaf(o.z, o.z, __builtin_fmaf(o.y, o.y, o.x * o.x));
+    return rt_ballot(live && !(om <= 0x1p12f && oo <= 0x1p15f)) == 0;
 }
 
 template <bool FAST>
@@ -684,30 +696,39 @@ __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, ui
     }
 }
 
-// The four group maxima of a tile's 16 values and the tile's maximum, as
-// v_max3 / v_max (10 VALU): fmaxf on MFMA results makes the compiler
-// canonicalise every operand first (v_max x, x: 18 VALU), since it cannot
-// prove them canonical. v_max3 drops a quiet-NaN operand like fmaxf; a NaN
-// H0 is never a candidate either way (its compare is false). H comes straight
-// from the MFMAs and hipcc pads no hazard into inline asm, so the block opens
-// with the 12 wait states the compiler itself puts between the 8-pass
-// v_mfma_f32_32x32x16_f16 and a VALU reading its result (s_nop 11).
-__device__ __forceinline__ void tile_max(const f16x& H, float* gq, float& g) {
+// The ORs of a tile's 16 values V = T0 - H0 per group of 4 and over the tile
+// (10 VALU: v_or3 / v_or). A group or tile with a candidate (V < 0) has the
+// sign bit set in its OR. The per-value masks are sign bits too (sgn4), so a
+// -0 or a NaN with the sign bit set is queued as well: harmless, since a -0
+// never comes from a sphere the exact test can hit (the margins leave V <=
+// -slack) and a NaN only from a ray with a NaN/inf feature, whose exact tests
+// never hit; rows past the last sphere (whole 32-sphere blocks) read pad
+// records, r^2 = -inf, that always miss (rt_set_scene pads the list). V
+// comes straight from the MFMAs and hipcc pads no hazard into inline asm, so
+// the block opens with the 12 wait states the compiler itself puts between the
+// 8-pass v_mfma_f32_32x32x16_f16 and a VALU reading its result (s_nop 11).
+__device__ __forceinline__ void tile_or(const f16x& H, int* gq, int& g) {
     asm("s_nop 11\n\t"
-        "v_max3_f32 %0, %5, %6, %7\n\t"
-        "v_max3_f32 %1, %9, %10, %11\n\t"
-        "v_max3_f32 %2, %13, %14, %15\n\t"
-        "v_max3_f32 %3, %17, %18, %19\n\t"
-        "v_max_f32 %0, %0, %8\n\t"
-        "v_max_f32 %1, %1, %12\n\t"
-        "v_max_f32 %2, %2, %16\n\t"
-        "v_max_f32 %3, %3, %20\n\t"
-        "v_max3_f32 %4, %0, %1, %2\n\t"
-        "v_max_f32 %4, %4, %3"
+        "v_or3_b32 %0, %5, %6, %7\n\t"
+        "v_or3_b32 %1, %9, %10, %11\n\t"
+        "v_or3_b32 %2, %13, %14, %15\n\t"
+        "v_or3_b32 %3, %17, %18, %19\n\t"
+        "v_or_b32 %0, %0, %8\n\t"
+        "v_or_b32 %1, %1, %12\n\t"
+        "v_or_b32 %2, %2, %16\n\t"
+        "v_or_b32 %3, %3, %20\n\t"
+        "v_or3_b32 %4, %0, %1, %2\n\t"
+        "v_or_b32 %4, %4, %3"
         : "=&v"(gq[0]), "=&v"(gq[1]), "=&v"(gq[2]), "=&v"(gq[3]), "=&v"(g)
         : "v"(H[0]), "v"(H[1]), "v"(H[2]), "v"(H[3]), "v"(H[4]), "v"(H[5]), "v"(H[6]),
           "v"(H[7]), "v"(H[8]), "v"(H[9]), "v"(H[10]), "v"(H[11]), "v"(H[12]), "v"(H[13]),
           "v"(H[14]), "v"(H[15]));
+}
+
+// the sign bits of a group's four values as its 4-bit candidate mask
+__device__ __forceinline__ uint32_t sgn4(float a, float b, float c, float d) {
+    return (__float_as_uint(a) >> 31) | ((__float_as_uint(b) >> 30) & 2u) |
+           ((__float_as_uint(c) >> 29) & 4u) | ((__float_as_uint(d) >> 28) & 8u);
 }
 
 // Called by the whole wave (the MFMA operands span all 64 lanes): lanes
@@ -752,20 +773,29 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
     f[6] = ((2.0f * ex) * ey) * mf_qs;
     f[7] = ((2.0f * ex) * ez) * mf_qs;
     f[8] = ((2.0f * ey) * ez) * mf_qs;
-    // the ray column, K 0..31: per feature [hi, lo, hi] (the sphere row holds
-    // [hi, hi, lo]), then 1, 1 (against S'_hi, S'_lo), then 0, 0, 0
+    // the ray column, K 0..31: per NEGATED feature [hi, lo, hi] (the sphere
+    // row holds [hi, hi, lo]), then -1, -1 (against S'_hi, S'_lo), T0's hi, lo
+    // (against 1, 1), 0: the dot product is T0 - H0. A lane without a ray has
+    // T0 = +inf (hi +inf, lo 0): V = +inf, never a candidate.
     _Float16 col[32];
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
-        const _Float16 hi = (_Float16)f[k];
-        const _Float16 lo = (_Float16)(f[k] - (float)hi);
+        const float x = -f[k];
+        const _Float16 hi = (_Float16)x;
+        const _Float16 lo = (_Float16)(x - (float)hi);
         col[3 * k] = hi;
         col[3 * k + 1] = lo;
         col[3 * k + 2] = hi;
     }
-    col[27] = (_Float16)1.0f;
-    col[28] = (_Float16)1.0f;
-    col[29] = col[30] = col[31] = (_Float16)0.0f;
+    col[27] = (_Float16)-1.0f;
+    col[28] = (_Float16)-1.0f;
+    {
+        const _Float16 hi = (_Float16)T;
+        const float r = T - (float)hi;
+        col[29] = hi;
+        col[30] = (_Float16)(live ? r : 0.0f);
+    }
+    col[31] = (_Float16)0.0f;
     uint32_t w[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -796,8 +826,6 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
     };
     const h8v B00 = as_h8(b0[0]), B01 = as_h8(b0[1]);  // half 0: K 0..15, K 16..31
     const h8v B10 = as_h8(b1[0]), B11 = as_h8(b1[1]);  // half 1
-    const auto Tw = __builtin_amdgcn_permlane32_swap(__float_as_uint(T), __float_as_uint(T), false, false);
-    const float T0 = __uint_as_float(Tw[0]), T1 = __uint_as_float(Tw[1]);  // of ray l & 31, 32 + (l & 31)
 
     float best_t = VERY_FAR;
     int best_i = -1;
@@ -807,16 +835,21 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
     const bool col0 = (live_mask >> (lane & 31u)) & 1u, col1 = (live_mask >> (32u + (lane & 31u))) & 1u;
     const uint4* ap = mfA + lane;
     uint4 a0 = ap[0], a1 = ap[64];
+    // wave-uniform upper bounds of every lane's queue length per half (SGPRs):
+    // one per group some lane queued from since the last drain
+    uint32_t ub0 = 0, ub1 = 0;
     for (uint32_t b = 0; b < nblk; ++b) {
         // a block adds at most 4 entries to each half's queue: make room first,
-        // while no tile result is live
-        if (rt_ballot(max(cnt0, cnt1) + 4u > RT_MF_CAP) != 0) {
+        // while no tile result is live (the lanes' own counts are compared
+        // only when the scalar bound says the queue may be full)
+        if (max(ub0, ub1) + 4u > RT_MF_CAP && rt_ballot(max(cnt0, cnt1) + 4u > RT_MF_CAP) != 0) {
             PROF_ADD(11, 1);  // queue flushes
             if (fast)
                 mfma_drain<true>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i);
             else
                 mfma_drain<false>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i);
             cnt0 = cnt1 = 0;
+            ub0 = ub1 = 0;
         }
         // the next block's fragments load during this one
         const size_t nb = (size_t)(b + 1 < nblk ? b + 1 : b) * 128u;
@@ -832,19 +865,18 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
             const f16x H = __builtin_amdgcn_mfma_f32_32x32x16_f16(
                 A1, t ? B11 : B01,
                 __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, t ? B10 : B00, zero, 0, 0, 0), 0, 0, 0);
-            const float Tt = t ? T1 : T0;
-            // per-group maxima (the lane's 4 groups of 4 spheres), then the tile's
-            float gq[4], g;
-            tile_max(H, gq, g);
-            if (rt_ballot(g >= Tt) != 0) {
+            // per-group ORs (the lane's 4 groups of 4 spheres), then the tile's
+            int gq[4], g;
+            tile_or(H, gq, g);
+            if (rt_ballot(g < 0) != 0) {
                 PROF_ADD(5, 1);  // tiles with a candidate
                 uint32_t& cnt = t ? cnt1 : cnt0;
                 uint32_t* qt = cq + t * (RT_MF_CAP * 64u);
 #pragma unroll
                 for (uint32_t q = 0; q < 4; ++q) {
-                    if (rt_ballot(gq[q] >= Tt) == 0) continue;  // no lane has one in this group
-                    const uint32_t m4 = ge(H[4 * q], Tt) | (ge(H[4 * q + 1], Tt) << 1) |
-                                        (ge(H[4 * q + 2], Tt) << 2) | (ge(H[4 * q + 3], Tt) << 3);
+                    if (rt_ballot(gq[q] < 0) == 0) continue;  // no lane has one in this group
+                    ++(t ? ub1 : ub0);
+                    const uint32_t m4 = sgn4(H[4 * q], H[4 * q + 1], H[4 * q + 2], H[4 * q + 3]);
                     if (m4 && (t ? col1 : col0)) {
                         qt[cnt * 64u + lane] = (((b * 8u) + q * 2u + h) << 4) | m4;
                         ++cnt;

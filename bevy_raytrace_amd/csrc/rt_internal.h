@@ -120,8 +120,8 @@ hipError_t rt_launch_collect(const KParams* P, const float4* block_sums,
                              float4* acc, int first_pass, int last_pass, float spp, float4* out,
                              float4* prog, int prog_mode, float prog_total, hipStream_t stream);
 hipError_t rt_launch_srgb8(const float4* in, uchar4* out, uint64_t npix, hipStream_t stream);
-hipError_t rt_launch_assemble(const float4* gathered, uint32_t max_rows, float4* image,
-                              uint32_t width, uint32_t height, uint32_t row_block,
+hipError_t rt_launch_assemble(const float4* gathered, uint32_t max_rows, uint32_t frames,
+                              float4* image, uint32_t width, uint32_t height, uint32_t row_block,
                               uint32_t shard_count, hipStream_t stream);
 hipError_t rt_launch_intersect(const float4* grp, const float4* sph, uint32_t ngroups,
                                uint32_t scene_fast, const float* rays, uint32_t n, int* out_i, float* out_t,

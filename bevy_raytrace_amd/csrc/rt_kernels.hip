@@ -626,17 +626,20 @@ __global__ void rt_srgb8_kernel(const float4* __restrict__ in, uchar4* __restric
 }
 
 // gathered: shard_count slabs of max_rows*W float4; image: H*W float4.
+// (grid.y = frame: slab k holds shard k's `frames` frames of max_rows rows)
 __global__ void rt_assemble_kernel(const float4* __restrict__ gathered, uint32_t max_rows,
-                                   float4* __restrict__ image, uint32_t width, uint32_t height,
-                                   uint32_t row_block, uint32_t shard_count) {
+                                   uint32_t frames, float4* __restrict__ image, uint32_t width,
+                                   uint32_t height, uint32_t row_block, uint32_t shard_count) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (size_t)width * height) return;
+    const uint32_t f = blockIdx.y;
     const uint32_t y = (uint32_t)(i / width);
     const uint32_t x = (uint32_t)(i - (size_t)y * width);
     const uint32_t blk = y / row_block;
     const uint32_t k = rt_block_owner(blk, shard_count);
     const uint32_t r = (blk / shard_count) * row_block + (y % row_block);
-    image[i] = gathered[((size_t)k * max_rows + r) * width + x];
+    image[(size_t)f * width * height + i] =
+        gathered[(((size_t)k * frames + f) * max_rows + r) * width + x];
 }
 
 extern "C" {
@@ -685,13 +688,14 @@ hipError_t rt_launch_srgb8(const float4* in, uchar4* out, uint64_t npix, hipStre
     return hipGetLastError();
 }
 
-hipError_t rt_launch_assemble(const float4* gathered, uint32_t max_rows, float4* image,
-                              uint32_t width, uint32_t height, uint32_t row_block,
+hipError_t rt_launch_assemble(const float4* gathered, uint32_t max_rows, uint32_t frames,
+                              float4* image, uint32_t width, uint32_t height, uint32_t row_block,
                               uint32_t shard_count, hipStream_t stream) {
     const uint32_t T = 256;
     const size_t n = (size_t)width * height;
-    hipLaunchKernelGGL(rt_assemble_kernel, dim3((uint32_t)((n + T - 1) / T)), dim3(T), 0, stream,
-                       gathered, max_rows, image, width, height, row_block, shard_count);
+    hipLaunchKernelGGL(rt_assemble_kernel, dim3((uint32_t)((n + T - 1) / T), frames), dim3(T), 0,
+                       stream, gathered, max_rows, frames, image, width, height, row_block,
+                       shard_count);
     return hipGetLastError();
 }
 

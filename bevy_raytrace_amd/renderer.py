@@ -184,6 +184,16 @@ class Renderer:
         self.lib.rt_debug_counters(self.ctx, out)
         return list(out)
 
+    def assemble_shard_frames(self, gathered_ptr: int, max_rows, frames, image_ptr: int, width,
+                              height, row_block, shard_count, stream=None):
+        """rt_assemble_shard_frames: `frames` frames of (shard, frame)-ordered
+        slabs in one launch."""
+        rc = self.lib.rt_assemble_shard_frames(self.ctx, ctypes.c_void_p(int(gathered_ptr)),
+                                               max_rows, frames, ctypes.c_void_p(int(image_ptr)),
+                                               width, height, row_block, shard_count,
+                                               ctypes.c_void_p(int(stream)) if stream else None)
+        check(self.lib, self.ctx, rc)
+
     def assemble_shards(self, gathered_ptr: int, max_rows, image_ptr: int, width, height,
                         row_block, shard_count, stream=None):
         rc = self.lib.rt_assemble_shards(self.ctx, ctypes.c_void_p(int(gathered_ptr)), max_rows,

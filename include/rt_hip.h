@@ -300,6 +300,16 @@ int rt_assemble_shards(rt_ctx* ctx, const float* gathered_device, uint32_t max_r
                        float* image_device, uint32_t width, uint32_t height,
                        uint32_t row_block, uint32_t shard_count, void* stream);
 
+/* The same for `frames` (1..65535) consecutive frames in one launch, in the
+ * layout one gather of the shards' multi-frame launches lands: gathered =
+ * shard_count slabs of frames*max_rows*width*4 floats (slab k = shard k's
+ * frames in order, each padded to max_rows rows); image = frames*height*
+ * width*4 floats. rt_assemble_shards is frames = 1. */
+int rt_assemble_shard_frames(rt_ctx* ctx, const float* gathered_device, uint32_t max_rows,
+                             uint32_t frames, float* image_device, uint32_t width,
+                             uint32_t height, uint32_t row_block, uint32_t shard_count,
+                             void* stream);
+
 /* Message for the last failing call on ctx (or on the library when ctx is NULL). */
 const char* rt_last_error(const rt_ctx* ctx);
 

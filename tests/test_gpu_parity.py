@@ -224,6 +224,33 @@ def test_shards_and_device_assembly(renderer, K, B):
     assert segs == stf["segments"]
 
 
+@pytest.mark.parametrize("K,B,H", [(3, 2, 23), (8, 5, 1080), (1, 8, 17)])
+def test_assemble_shard_frames_matches_per_frame(renderer, K, B, H):
+    """rt_assemble_shard_frames (one launch over the (shard, frame) slabs one
+    gather of multi-frame launches lands) equals rt_assemble_shards frame by
+    frame, and the numpy statement of the mapping (distributed.assemble_host)."""
+    import torch
+    from bevy_raytrace_amd.distributed import ShardLayout, assemble_host
+    W, F = 40, 3
+    mr = max(len(abi.shard_rows(H, B, K, k)) for k in range(K))
+    g = torch.randn((K, F, mr, W, 4), dtype=torch.float32, device="cuda")
+    img = torch.full((F, H, W, 4), -7.0, dtype=torch.float32, device="cuda")
+    renderer.assemble_shard_frames(g.data_ptr(), mr, F, img.data_ptr(), W, H, B, K)
+    lay = ShardLayout(H, B, K)
+    for f in range(F):
+        slabs = g[:, f].contiguous()
+        one = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+        renderer.assemble_shards(slabs.data_ptr(), mr, one.data_ptr(), W, H, B, K)
+        torch.cuda.synchronize()
+        assert torch.equal(img[f], one)
+        assert np.array_equal(img[f].cpu().numpy(), assemble_host(slabs.cpu().numpy(), lay))
+    with pytest.raises(abi.RayTraceError):
+        renderer.assemble_shard_frames(g.data_ptr(), mr, 0, img.data_ptr(), W, H, B, K)
+    if K > 1:
+        with pytest.raises(abi.RayTraceError):  # slabs shorter than a shard
+            renderer.assemble_shard_frames(g.data_ptr(), mr - 1, F, img.data_ptr(), W, H, B, K)
+
+
 def test_full_1080p64_properties(renderer):
     """Headline config at full size: sampled-row parity (incl. NaN-path rows),
     determinism, reuse on/off identity."""

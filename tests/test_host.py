@@ -95,8 +95,8 @@ def test_library_exports_every_header_symbol():
     lib = abi.load()
     names = abi.header_symbols()
     assert {"rt_create", "rt_destroy", "rt_set_scene", "rt_render", "rt_render_device",
-            "rt_render_async", "rt_wait", "rt_assemble_shards", "rt_last_error", "rt_version",
-            "rt_shard_rows"} <= set(names)
+            "rt_render_async", "rt_wait", "rt_assemble_shards", "rt_assemble_shard_frames",
+            "rt_last_error", "rt_version", "rt_shard_rows"} <= set(names)
     for n in names:
         assert hasattr(lib, n), n
     assert lib.rt_version() == 1

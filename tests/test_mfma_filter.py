@@ -2,18 +2,19 @@
 
 rt_dev_intersect.h intersect_world_mfma decides which spheres get the
 reference's exact test (intersect.wgsl:97-115) from one 32-term dot product
-per (sphere, ray) pair on the matrix cores: H0 = S' + L.c + sum_ab Q_ab c_a c_b
-(the VALU filter's hb^2 + S + o2.c less the ray's k1^2), every feature split
-into f16 hi/lo parts, against T0 = (1 - m - mu')|o|^2 - k1^2 - abs'. The
-product is bit-exact only if that test is conservative: every sphere whose
-exact test yields a root that can win must have H0 >= T0. This file restates
+per (sphere, ray) pair on the matrix cores: V = T0 - H0, H0 = S' + L.c +
+sum_ab Q_ab c_a c_b (the VALU filter's hb^2 + S + o2.c less the ray's k1^2),
+T0 = (1 - m - mu')|o|^2 - k1^2 - abs' one more term of the dot product, every
+feature and T0 split into f16 hi/lo parts; a sphere is a candidate iff V < 0.
+The product is bit-exact only if that test is conservative: every sphere
+whose exact test yields a root that can win must have V < 0. This file restates
 the kernel's arithmetic in numpy -- the ray constants and features, the f16
 splits, the A rows of rt_api.cpp build_mfma (with its scale 2^sq of the
 quadratic features), the two chained MFMAs' 32-product f32 sums in four
 summation orders (the hardware's is not documented) -- and checks that
 property on the adversarial ray sets of the GPU intersection tests
 (tests/raygen.py), for every (ray, sphere) pair whose ray lies inside the
-filter's range (|o_i| <= 2^12, the kernel's mfma_wave_ok). It also checks the
+filter's range (|o_i| <= 2^12, |o|^2 <= 2^15, the kernel's mfma_wave_ok). It also checks the
 error bound the kernel's margins are built from against the exact value.
 """
 import zlib
@@ -77,7 +78,8 @@ def sphere_rows(sp, sq):
     assert np.all(np.abs(S) <= 2.0 ** 15)  # mf_ok
     hi, lo = hl(S)
     n = len(sp)
-    cols += [hi, lo] + [np.zeros(n, H16)] * 3
+    one = np.ones(n, H16)
+    cols += [hi, lo, one, one, np.zeros(n, H16)]  # K 29, 30: against T0's hi, lo
     return np.stack(cols, 1).astype(F)
 
 
@@ -96,7 +98,8 @@ def ray_constants(rays):
 
 
 def ray_columns(rays, sq, abs_margin):
-    """The ray column (n, 32) and threshold T0 (n,), as the kernel builds them."""
+    """The ray column (n, 32) and threshold T0 (n,), as the kernel builds them:
+    the negated features, -1, -1 against S', T0's hi, lo against 1, 1."""
     o, e, k1, oo, o2 = ray_constants(rays)
     sc = F(2.0 ** sq)
     with np.errstate(invalid="ignore", over="ignore"):
@@ -105,10 +108,12 @@ def ray_columns(rays, sq, abs_margin):
         T0 = (fma32(-k1, k1, F(1.0 - M - MU) * oo) - F(abs_margin)).astype(F)
     cols = []
     for x in feats:
-        hi, lo = split(x)
+        hi, lo = split(-x)
         cols += [hi, lo, hi]
-    one, z = np.ones(len(rays), F), np.zeros(len(rays), F)
-    cols += [one, one, z, z, z]
+    m1, z = -np.ones(len(rays), F), np.zeros(len(rays), F)
+    with np.errstate(invalid="ignore", over="ignore"):
+        thi, tlo = split(T0)
+    cols += [m1, m1, thi, tlo, z]
     return np.stack(cols, 1), T0
 
 
@@ -173,7 +178,9 @@ SCENES = {
 
 def _rays(sp, name, n):
     rays = adversarial_rays(sp, n, seed=zlib.crc32(name.encode()) % 1000)
-    return rays[np.abs(rays[:, :3]).max(1) <= 2.0 ** 12]  # mfma_wave_ok
+    o = rays[:, :3].astype(F)
+    oo = fma32(o[:, 2], o[:, 2], fma32(o[:, 1], o[:, 1], o[:, 0] * o[:, 0]))
+    return rays[(np.abs(o).max(1) <= 2.0 ** 12) & (oo <= 2.0 ** 15)]  # mfma_wave_ok
 
 
 @pytest.mark.parametrize("name", sorted(SCENES))
@@ -188,7 +195,7 @@ def test_matrix_core_filter_is_conservative(name):
     for order in ORDERS:
         for j0 in range(0, len(sp), 256):
             with np.errstate(invalid="ignore", over="ignore"):
-                cand = mfma_sum(A[j0:j0 + 256], B, order) >= T0[:, None]
+                cand = mfma_sum(A[j0:j0 + 256], B, order) < 0  # V = T0 - H0 < 0
             lost = hits[:, j0:j0 + 256] & ~cand
             assert not lost.any(), (
                 f"{order}: {int(lost.sum())} exact hits filtered out, e.g. ray "
@@ -197,7 +204,7 @@ def test_matrix_core_filter_is_conservative(name):
 
 @pytest.mark.parametrize("name", ["rtiow", "spheres10k"])
 def test_error_within_stated_bound(name):
-    """|(H0' - T0') - (H~ - T~)| <= 2^-16.3 (|o|^2 + |c|^2) + 2^-19 |S'| + abs',
+    """|-V' - (H~ - T~)| <= 2^-16.02 (|o|^2 + |c|^2) + 2^-19 |S'| + abs',
     the bound of rt_dev_intersect.h's margin comment, where H~ - T~ is the
     exact value of hb^2 + S' + o2.c - (1 - m - mu')|o|^2 with the kernel's f32
     ray constants e, k1, o2 (hb = k1 + e.c)."""
@@ -214,11 +221,11 @@ def test_error_within_stated_bound(name):
     oo = (o.astype(D) ** 2).sum(1)
     hb = k1.astype(D)[:, None] + e.astype(D) @ c.T
     exact = hb * hb + S[None, :] + o2.astype(D) @ c.T - (1.0 - M - MU) * oo[:, None]
-    bound = (2.0 ** -16.3 * (oo[:, None] + (c ** 2).sum(1)[None, :]) + 2.0 ** -19 * np.abs(S)[None, :]
+    bound = (2.0 ** -16.02 * (oo[:, None] + (c ** 2).sum(1)[None, :]) + 2.0 ** -19 * np.abs(S)[None, :]
              + absm)
     A = sphere_rows(sp, sq)
     worst = 0.0
     for order in ORDERS:
-        got = mfma_sum(A, B, order).astype(D) - T0.astype(D)[:, None]
+        got = -mfma_sum(A, B, order).astype(D)  # H0' - T0'
         worst = max(worst, float(np.max(np.abs(got - exact) / bound)))
     assert worst < 1.0, worst
