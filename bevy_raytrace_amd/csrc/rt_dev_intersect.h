@@ -833,12 +833,12 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
     const f16x zero = {};
     // is the ray of this lane's column live, per half
     const bool col0 = (live_mask >> (lane & 31u)) & 1u, col1 = (live_mask >> (32u + (lane & 31u))) & 1u;
-    const uint4* ap = mfA + lane;
-    uint4 a0 = ap[0], a1 = ap[64];
     // wave-uniform upper bounds of every lane's queue length per half (SGPRs):
     // one per group some lane queued from since the last drain
     uint32_t ub0 = 0, ub1 = 0;
-    for (uint32_t b = 0; b < nblk; ++b) {
+    // one 32-sphere block: both ray halves against A fragments x0 (K 0..15),
+    // x1 (K 16..31)
+    auto block = [&](uint32_t b, const uint4 x0, const uint4 x1) {
         // a block adds at most 4 entries to each half's queue: make room first,
         // while no tile result is live (the lanes' own counts are compared
         // only when the scalar bound says the queue may be full)
@@ -851,12 +851,9 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
             cnt0 = cnt1 = 0;
             ub0 = ub1 = 0;
         }
-        // the next block's fragments load during this one
-        const size_t nb = (size_t)(b + 1 < nblk ? b + 1 : b) * 128u;
-        const uint4 n0 = ap[nb], n1 = ap[nb + 64];
         h8v A0, A1;
-        __builtin_memcpy(&A0, &a0, 16);
-        __builtin_memcpy(&A1, &a1, 16);
+        __builtin_memcpy(&A0, &x0, 16);
+        __builtin_memcpy(&A1, &x1, 16);
         // the two halves unrolled (no per-tile operand selects) but kept apart
         // (sched_barrier): one tile's 16 result registers live at a time
 #pragma unroll
@@ -884,9 +881,22 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
                 }
             }
         }
-        a0 = n0;
-        a1 = n1;
+    };
+    // blocks in pairs: the next block's fragments load while this one runs,
+    // into the other register set (no fragment copies per block); block p's
+    // fragments at mfA + 128 p (uniform base) + lane
+    uint4 a0 = mfA[lane], a1 = mfA[64u + lane];
+    uint32_t b = 0;
+    for (; b + 2u <= nblk; b += 2u) {
+        const uint4* p1 = mfA + (size_t)(b + 1u) * 128u;
+        const uint4 n0 = p1[lane], n1 = p1[64u + lane];
+        block(b, a0, a1);
+        const uint4* p2 = mfA + (size_t)(b + 2u < nblk ? b + 2u : b + 1u) * 128u;
+        a0 = p2[lane];
+        a1 = p2[64u + lane];
+        block(b + 1u, n0, n1);
     }
+    if (b < nblk) block(b, a0, a1);
     PROF_MARK(1);
     if (fast)
         mfma_drain<true>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i);
