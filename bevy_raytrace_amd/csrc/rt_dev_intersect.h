@@ -662,10 +662,19 @@ __device__ __forceinline__ bool mfma_wave_ok(v3 o, bool live) {
     return rt_ballot(live && !(om <= 0x1p12f && oo <= 0x1p15f)) == 0;
 }
 
+#ifdef RT_PROFILE
+#define MF_ECNT , uint32_t& ecnt_
+#define MF_ECNT_PASS , ecnt_
+#define MF_ECNT_INC ++ecnt_
+#else
+#define MF_ECNT
+#define MF_ECNT_PASS
+#define MF_ECNT_INC
+#endif
 template <bool FAST>
 __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, uint32_t cnt1,
                                            const float4* __restrict__ sph, v3 o, v3 d, float a,
-                                           float ya, float& best_t, int& best_i) {
+                                           float ya, float& best_t, int& best_i MF_ECNT) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     const uint32_t lane = __lane_id();
     const uint32_t t = lane >> 5, j = lane & 31u;
@@ -689,6 +698,7 @@ __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, ui
             while (m) {
                 const uint32_t b = __builtin_ctz(m);
                 m &= m - 1;
+                MF_ECNT_INC;
                 exact_body<FAST, false, true>(sph[base + b], (int)(base + b), o, d, a, ya, best_t,
                                               best_i, nullptr EXACT_PASS);
             }
@@ -833,6 +843,9 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
     const f16x zero = {};
     // is the ray of this lane's column live, per half
     const bool col0 = (live_mask >> (lane & 31u)) & 1u, col1 = (live_mask >> (32u + (lane & 31u))) & 1u;
+#ifdef RT_PROFILE
+    uint32_t ecnt_ = 0;  // this lane's exact tests (c[13]: wave max, c[15]: lane sum)
+#endif
     // wave-uniform upper bounds of every lane's queue length per half (SGPRs):
     // one per group some lane queued from since the last drain
     uint32_t ub0 = 0, ub1 = 0;
@@ -845,9 +858,9 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
         if (max(ub0, ub1) + 4u > RT_MF_CAP && rt_ballot(max(cnt0, cnt1) + 4u > RT_MF_CAP) != 0) {
             PROF_ADD(11, 1);  // queue flushes
             if (fast)
-                mfma_drain<true>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i);
+                mfma_drain<true>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
             else
-                mfma_drain<false>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i);
+                mfma_drain<false>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
             cnt0 = cnt1 = 0;
             ub0 = ub1 = 0;
         }
@@ -899,10 +912,18 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
     if (b < nblk) block(b, a0, a1);
     PROF_MARK(1);
     if (fast)
-        mfma_drain<true>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i);
+        mfma_drain<true>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
     else
-        mfma_drain<false>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i);
+        mfma_drain<false>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
     PROF_MARK(2);
+#ifdef RT_PROFILE
+    {
+        PROF_ADD(13, wave_max_u32(ecnt_));
+        uint32_t sum0 = ecnt_;
+        for (int off = 32; off > 0; off >>= 1) sum0 += __shfl_xor(sum0, off);
+        PROF_ADD(15, sum0);
+    }
+#endif
     t_out = best_t;
     return best_i;
 }
