@@ -11,7 +11,7 @@ import _knobs
 wl = configs.WORKLOADS["rtiow1080"]
 sc = wl.make_scene()
 cam = default_camera_block()
-r = Renderer(0)
+r = Renderer(0, lib_path=os.environ.get("PROBE_LIB") or None)  # PROBE_LIB: another build (A/B)
 r.set_scene(sc.objects_gpu(), sc.materials_gpu())
 W, H, S, D = wl.width, wl.height, wl.spp, wl.max_depth
 FS = [int(x) for x in os.environ.get("PROBE_F", "4,8").split(",")]
