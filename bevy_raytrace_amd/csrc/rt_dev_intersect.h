@@ -648,7 +648,9 @@ typedef float f16x __attribute__((ext_vector_type(16)));
 // per wave |o_i| <= 2^12, |o|^2 <= 2^15 (mfma_wave_ok: T0 in f16 range).
 // tests/test_mfma_filter.py restates this arithmetic and checks it.
 #define RT_MF_MU 0x1p-16f
-#define RT_MF_CAP 8  // queue entries per lane and half (LDS)
+#ifndef RT_MF_CAP
+#define RT_MF_CAP 12  // queue entries per lane and half (LDS)
+#endif
 
 __device__ __forceinline__ uint32_t bperm(uint32_t src_lane, uint32_t v) {
     return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
