@@ -35,14 +35,16 @@ def test_rccl_gather_path_matches_single_gpu():
 
 
 @pytest.mark.gpu
-def test_bench_launches_its_own_ranks():
-    """`python bench.py --gpus 2` with no launcher around it (the driver's
-    scaling command) starts the two ranks itself and relays rank 0's line;
-    the assembled frames equal the single-GPU run's (both ranks on the one
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_launches_its_own_ranks(n):
+    """`python bench.py --gpus N` with no launcher around it (the driver's
+    scaling command) starts the N ranks itself and relays rank 0's line;
+    the assembled frames (rt_assemble_shard_frames over 2-frame launches;
+    225 rows split unevenly) equal the single-GPU run's (all ranks on the one
     GPU of this box, host-staged gloo gather)."""
     a = _bench()
-    b = _bench("--gpus", "2", "--same-device", "--dist-backend", "gloo")
-    assert b["n_gpus"] == 2 and len(b["ranks"]["segments"]) == 2
+    b = _bench("--gpus", str(n), "--same-device", "--dist-backend", "gloo")
+    assert b["n_gpus"] == n and len(b["ranks"]["segments"]) == n
     assert sum(b["ranks"]["segments"]) // 4 == a["segments_per_frame"]  # 4 timed frames
     assert a["check"] == b["check"]
     assert a["segments_per_frame"] == b["segments_per_frame"]
