@@ -7,8 +7,12 @@
 #include "../../include/rt_hip.h"
 
 #define RT_BLOCK_THREADS 256  // 4 waves per workgroup
+#ifndef RT_WAVE_CHUNK
 #define RT_WAVE_CHUNK 64      // work items a wave takes per atomic
+#endif
+#ifndef RT_WAVE_CHUNK_TAIL
 #define RT_WAVE_CHUNK_TAIL 16 // ... in the last 2 x 64 x waves items of the queue
+#endif
 // Counter block at the start of the ctx's counter buffer (u32 words):
 // [0,4) two u64 segment counters, [4,36) 16 u64 diagnostic counters
 // (RT_PROFILE builds), [36, ...) one u32 work counter per pass.
