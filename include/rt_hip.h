@@ -211,7 +211,9 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n,
  * the materials when their count changes, ray_trace_materials.rs:129-164).
  * Replace records [first, first+count) of the current scene; counts N and M
  * are unchanged. Only the touched sphere records and 8-sphere groups are
- * re-packed and uploaded; the culled list (RT_FLAG_CULL), which depends on
+ * re-packed and uploaded; the matrix-core filter's f16 sphere rows are
+ * rebuilt whole (their scale 2^-sq depends on every centre: O(N) on the host,
+ * 64 B per sphere uploaded); the culled list (RT_FLAG_CULL), which depends on
  * every sphere, is rebuilt once, at the next culled call. */
 int rt_update_spheres(rt_ctx* ctx, uint32_t first, const rt_sphere* spheres, uint32_t count);
 int rt_update_materials(rt_ctx* ctx, uint32_t first, const rt_material* materials,
