@@ -330,6 +330,10 @@ def main():
         return dt, stats, sizes
 
     dt, stats, sizes = timed(args.steps, NO_REUSE)
+    # the timed headline run's first frame of its last launch, kept for the
+    # parity check below before the reuse / cull runs overwrite the buffer
+    head_idx = args.steps - sizes[-1]
+    head_frame = image[0].clone() if (rank == 0 and world == 1) else None
     segs_local = sum(s["segments"] for s in stats)
     traced_local = sum(s["traced_segments"] for s in stats)
     kms = [s["kernel_ms"] for s in stats]
@@ -456,8 +460,18 @@ def main():
     if args.lib:
         out["lib"] = os.path.relpath(os.path.abspath(args.lib), ROOT)
     if world == 1 and not args.no_cpu_baseline:
+        def gpu_shard(K, j):
+            """Rows of shard j of K (one-row blocks, dealt serpentine: spread
+            over the whole frame) of the headline frame, rendered again on the
+            GPU with the headline's flags: (image rows, exact segment count)."""
+            rows_j = abi.shard_rows(H, 1, K, j)
+            buf = torch.empty((len(rows_j), W, 4), dtype=torch.float32, device="cuda")
+            r.render_device(cam, buf.data_ptr(), W, H, S, D, head_idx * S, 1, K, j, NO_REUSE,
+                            stream=stream.cuda_stream)
+            st = r.wait()
+            return rows_j, buf.cpu().numpy(), int(st["segments"])
         out["cpu_baseline"] = cpu_baseline(cam, spheres, mats, W, H, S, D, args.cpu_rows,
-                                           image[0].cpu().numpy())
+                                           head_frame.cpu().numpy(), head_idx, gpu_shard)
     os.write(json_fd, (json.dumps(out) + "\n").encode())
     if dist_on:
         dist.destroy_process_group()
@@ -472,8 +486,12 @@ def cpu_quota():
         return None
 
 
-def cpu_baseline(cam, spheres, mats, W, H, S, D, nrows, gpu_image):
-    """Time the C oracle (scalar port of the WGSL) on a bounded row sample."""
+def cpu_baseline(cam, spheres, mats, W, H, S, D, nrows, head_frame, head_idx, gpu_shard):
+    """Time the C oracle (scalar port of the WGSL) on a bounded row sample of
+    the timed headline frame and check it: the sample is shard j of K with
+    one-row blocks (rows spread over the frame, top to bottom), the oracle's
+    rows must equal the headline frame's rows bit for bit, and its segment
+    count the GPU's count for the same rows (the same shard rendered again)."""
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
     # every host core this process may run on -- unless the cgroup grants
@@ -483,25 +501,33 @@ def cpu_baseline(cam, spheres, mats, W, H, S, D, nrows, gpu_image):
     host = len(os.sched_getaffinity(0)) or 1
     quota = cpu_quota()
     cores = min(host, max(1, int(math.ceil(quota)))) if quota else host
+    frame0 = head_idx * S
     # calibrate on `cores` spread rows (one row per thread), then size the
     # sample for ~10 s of wall time
     rows = [int(i * H / cores) for i in range(cores)]
     t0 = time.perf_counter()
-    _, segs = O.render_rows(cam, spheres, mats, W, H, S, D, rows, nthreads=cores)
+    O.render_rows(cam, spheres, mats, W, H, S, D, rows, frame0=frame0, nthreads=cores)
     t1 = time.perf_counter() - t0
     if nrows <= 0:
         nrows = int(max(cores, min(H, cores * 10.0 / max(t1, 1e-3))))
-    stride = max(1, H // nrows)
-    rows = list(range(0, H, stride))[:nrows]
+    K = max(1, -(-H // max(1, nrows)))
+    j = K // 2
+    rows, gpu_rows, gpu_segs = gpu_shard(K, j)
     t0 = time.perf_counter()
-    img, segs = O.render_rows(cam, spheres, mats, W, H, S, D, rows, nthreads=cores)
+    img, segs = O.render_rows(cam, spheres, mats, W, H, S, D, rows, frame0=frame0, nthreads=cores)
     dt = time.perf_counter() - t0
-    exact = bool(np.array_equal(img, gpu_image[rows], equal_nan=True))
+    exact = bool(np.array_equal(img, head_frame[rows], equal_nan=True))
     return {"value": round(segs / dt / 1e6, 3), "unit": "Mrays/s", "cores": cores,
             "host_cores": host, "cpu_quota_cores": quota, "kind": "port",
-            "sample": f"{len(rows)} rows (every {stride}th) of the same {W}x{H} {S}spp frame, "
-                      f"{segs} segments in {dt:.2f} s",
-            "gpu_rows_bit_exact": exact}
+            "sample": f"{len(rows)} rows spread over the {W}x{H} {S}spp headline frame {head_idx} "
+                      f"(rows {rows[0]}..{rows[-1]}: shard {j} of {K}, one-row blocks dealt "
+                      f"serpentine), {segs} segments in {dt:.2f} s",
+            "frame": head_idx,
+            "gpu_rows_bit_exact": exact,
+            "segments_equal": bool(segs == gpu_segs),
+            "gpu_segments": gpu_segs,
+            "gpu_shard_equals_headline": bool(np.array_equal(gpu_rows, head_frame[rows],
+                                                             equal_nan=True))}
 
 
 if __name__ == "__main__":

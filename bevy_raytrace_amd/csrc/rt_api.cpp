@@ -113,6 +113,7 @@ struct rt_ctx {
     size_t grp_c_cap = 0, sph_c_cap = 0, rm_c_cap = 0, bnd_c_cap = 0, perm_c_cap = 0;
     // matrix-core filter (RT_MFMA_FILTER builds, build_mfma): f16 A fragments
     bool mf_ok = false;
+    bool mf_dirty = false;          // rt_update_spheres: fragments rebuilt by mfma_ready
     uint32_t mf_nblk = 0;
     float mf_qs = 1.0f;   // 2^sq: the ray side's scale of the quadratic features
     float mf_abs = 0.0f;  // absolute margin of the threshold, 2^(sq - 20)
@@ -741,6 +742,17 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n, const rt_mat
     // matrix-core walk may queue a pad row of its last block (a NaN ray),
     // whose record always misses
     const size_t nrec = std::max((size_t)(ngroups + 1) * RT_GROUP, (size_t)(n + 31) / 32 * 32);
+    rc = quiesce(ctx);
+    if (rc) return rc;  // nothing touched yet: the previous scene stays whole
+    // From here on the host mirrors and the device buffers change: until every
+    // upload succeeded there is no scene (a failed call leaves
+    // RT_ERR_NO_SCENE, never a half-written or freed list behind stale counts
+    // that a later update or culled build would index with).
+    ctx->has_scene = false;
+    ctx->cull_dirty = true;
+    ctx->mf_ok = false;
+    ctx->mf_dirty = false;
+    ctx->n = ctx->ngroups = ctx->m = 0;
     ctx->h_sph.assign(nrec, make_float4(0.0f, 0.0f, 0.0f, -INFINITY));
     ctx->h_S.assign(nrec, -INFINITY);
     ctx->h_rm.assign(n ? n : 1, make_float2(0.0f, 0.0f));
@@ -748,15 +760,6 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n, const rt_mat
     for (uint32_t i = 0; i < n; ++i) pack_record(ctx, i, spheres[i]);
     for (size_t g = 0; g < nrec / RT_GROUP; ++g) pack_group(ctx, g);
     ctx->h_mats.assign(materials, materials + m);
-    rc = quiesce(ctx);
-    if (rc) return rc;
-    // From here on the device buffers change: until every upload succeeded
-    // there is no scene (a failed call leaves RT_ERR_NO_SCENE, never a
-    // half-written or freed list behind stale counts).
-    ctx->has_scene = false;
-    ctx->cull_dirty = true;
-    ctx->mf_ok = false;
-    ctx->n = ctx->ngroups = ctx->m = 0;
     rc = ensure(ctx, &ctx->d_sph, &ctx->sph_cap, sizeof(float4) * nrec);
     if (rc) return rc;
     rc = ensure(ctx, &ctx->d_grp, &ctx->grp_cap, sizeof(float4) * nrec);
@@ -799,6 +802,27 @@ static int cull_ready(rt_ctx* ctx) {
     return RT_OK;
 }
 
+// The matrix-core fragments of the current scene, rebuilt on the first
+// brute-force call after rt_update_spheres (same size: no allocation). The
+// update quiesced, so no kernel reads the old fragments.
+static int mfma_ready(rt_ctx* ctx) {
+#ifdef RT_MFMA_FILTER
+    if (!ctx->mf_dirty) return RT_OK;
+    int rc = build_mfma(ctx);
+    if (rc) return rc;
+    ctx->mf_dirty = false;
+#else
+    (void)ctx;
+#endif
+    return RT_OK;
+}
+
+// Everything a call with these flags walks: built before its first enqueue,
+// or by rt_reserve so a reserved render allocates and uploads nothing.
+static int scene_ready(rt_ctx* ctx, uint32_t flags) {
+    return (flags & RT_FLAG_CULL) ? cull_ready(ctx) : mfma_ready(ctx);
+}
+
 
 int rt_update_spheres(rt_ctx* ctx, uint32_t first, const rt_sphere* spheres, uint32_t count) {
     if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_update_spheres: ctx is NULL");
@@ -824,8 +848,9 @@ int rt_update_spheres(rt_ctx* ctx, uint32_t first, const rt_sphere* spheres, uin
     ctx->scene_fast = scene_fast_ok(ctx);
     ctx->cull_dirty = true;  // the permutation and bounds follow at the next culled call
 #ifdef RT_MFMA_FILTER
-    rc = build_mfma(ctx);
-    if (rc) return rc;
+    // and the matrix-core fragments at the next call that walks them
+    // (mfma_ready): a caller rendering only the culled list never pays for them
+    ctx->mf_dirty = true;
 #endif
     return RT_OK;
 }
@@ -991,12 +1016,12 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         HIP_TRY(ctx, hipEventCreate(&e));
         f.ev.push_back(e);
     }
-    if (reserve_only) return RT_OK;
-    const bool cull = (p.flags & RT_FLAG_CULL) != 0;
-    if (cull) {
-        int rc = cull_ready(ctx);
+    {
+        int rc = scene_ready(ctx, p.flags);
         if (rc) return rc;
     }
+    if (reserve_only) return RT_OK;
+    const bool cull = (p.flags & RT_FLAG_CULL) != 0;
 
     KParams K_{};
     K_.width = p.width;
@@ -1388,7 +1413,7 @@ int rt_intersect_ex(rt_ctx* ctx, const float* rays, uint32_t n, uint32_t flags, 
     int rc = no_pending(ctx, "rt_intersect");
     if (rc) return rc;
     const bool cull = (flags & RT_FLAG_CULL) != 0;
-    if (cull && (rc = cull_ready(ctx)) != RT_OK) return rc;
+    if ((rc = scene_ready(ctx, flags)) != RT_OK) return rc;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     void* buf = nullptr;
     const size_t rb = sizeof(float) * 6 * (size_t)n, ob = sizeof(int32_t) * (size_t)n;

@@ -210,6 +210,10 @@ __device__ __forceinline__ void filter8(const RayP& R, f2 cxa, f2 cxb, f2 cxc, f
                                         f2 cyb, f2 cyc, f2 cyd, f2 cza, f2 czb, f2 czc, f2 czd,
                                         f2 sa, f2 sb, f2 sc, f2 sd, f2& ha, f2& hb, f2& hc,
                                         f2& hd, float& hmax) {
+    // compiler-allocated registers (early-clobber: every output is written
+    // before the last input is read); the dependent packed ops are 4 apart,
+    // above the 1 wait state hipcc itself puts after a v_pk_fma_f32 whose
+    // result the next VALU reads (tools/hazard_audit.py rule R1)
     asm volatile(
         // hb = k1 + (-dnx) cx + (-dny) cy + (-dnz) cz
         "v_pk_fma_f32 %[ha], %[dx], %[cxa], %[k1]\n\t"
@@ -240,19 +244,23 @@ __device__ __forceinline__ void filter8(const RayP& R, f2 cxa, f2 cxb, f2 cxc, f
         "v_pk_fma_f32 %[ha], %[ox], %[cxa], %[ha]\n\t"
         "v_pk_fma_f32 %[hb], %[ox], %[cxb], %[hb]\n\t"
         "v_pk_fma_f32 %[hc], %[ox], %[cxc], %[hc]\n\t"
-        "v_pk_fma_f32 %[hd], %[ox], %[cxd], %[hd]\n\t"
-        // group max of the 8 H (v_max3 drops a quiet-NaN operand, as fmaxf)
-        "v_max3_f32 %[hm], v40, v41, v42\n\t"
-        "v_max3_f32 %[hm], %[hm], v43, v44\n\t"
-        "v_max3_f32 %[hm], %[hm], v45, v46\n\t"
-        "v_max_f32 %[hm], %[hm], v47"
-        : [ha] "={v[40:41]}"(ha), [hb] "={v[42:43]}"(hb), [hc] "={v[44:45]}"(hc),
-          [hd] "={v[46:47]}"(hd), [hm] "=&v"(hmax)
+        "v_pk_fma_f32 %[hd], %[ox], %[cxd], %[hd]"
+        : [ha] "=&v"(ha), [hb] "=&v"(hb), [hc] "=&v"(hc), [hd] "=&v"(hd)
         : [dx] "v"(R.dx), [dy] "v"(R.dy), [dz] "v"(R.dz), [k1] "v"(R.k1), [ox] "v"(R.ox),
           [oy] "v"(R.oy), [oz] "v"(R.oz), [cxa] "s"(cxa), [cxb] "s"(cxb), [cxc] "s"(cxc),
           [cxd] "s"(cxd), [cya] "s"(cya), [cyb] "s"(cyb), [cyc] "s"(cyc), [cyd] "s"(cyd),
           [cza] "s"(cza), [czb] "s"(czb), [czc] "s"(czc), [czd] "s"(czd), [sa] "s"(sa),
           [sb] "s"(sb), [sc] "s"(sc), [sd] "s"(sd));
+    // group max of the 8 H (v_max3 drops a quiet-NaN operand, as fmaxf; in
+    // asm so that no canonicalising v_max is put in front of each operand)
+    asm volatile(
+        "v_max3_f32 %[hm], %[h0], %[h1], %[h2]\n\t"
+        "v_max3_f32 %[hm], %[hm], %[h3], %[h4]\n\t"
+        "v_max3_f32 %[hm], %[hm], %[h5], %[h6]\n\t"
+        "v_max_f32 %[hm], %[hm], %[h7]"
+        : [hm] "=&v"(hmax)
+        : [h0] "v"(ha.x), [h1] "v"(ha.y), [h2] "v"(hb.x), [h3] "v"(hb.y), [h4] "v"(hc.x),
+          [h5] "v"(hc.y), [h6] "v"(hd.x), [h7] "v"(hd.y));
 }
 
 __device__ __forceinline__ uint32_t ge(float h, float t) { return h >= t ? 1u : 0u; }
@@ -715,26 +723,18 @@ __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, ui
 // never comes from a sphere the exact test can hit (the margins leave V <=
 // -slack) and a NaN only from a ray with a NaN/inf feature, whose exact tests
 // never hit; rows past the last sphere (whole 32-sphere blocks) read pad
-// records, r^2 = -inf, that always miss (rt_set_scene pads the list). V
-// comes straight from the MFMAs and hipcc pads no hazard into inline asm, so
-// the block opens with the 12 wait states the compiler itself puts between the
-// 8-pass v_mfma_f32_32x32x16_f16 and a VALU reading its result (s_nop 11).
+// records, r^2 = -inf, that always miss (rt_set_scene pads the list).
+// Integer ORs of the bits in C++ (no canonicalisation as a float max would
+// need), so hipcc itself places the wait states between the MFMA that writes
+// V and the first VALU reading it (round 2 had this in inline asm opening
+// with a hand-placed s_nop 11, DESIGN.md 4.7 "hazards").
 __device__ __forceinline__ void tile_or(const f16x& H, int* gq, int& g) {
-    asm("s_nop 11\n\t"
-        "v_or3_b32 %0, %5, %6, %7\n\t"
-        "v_or3_b32 %1, %9, %10, %11\n\t"
-        "v_or3_b32 %2, %13, %14, %15\n\t"
-        "v_or3_b32 %3, %17, %18, %19\n\t"
-        "v_or_b32 %0, %0, %8\n\t"
-        "v_or_b32 %1, %1, %12\n\t"
-        "v_or_b32 %2, %2, %16\n\t"
-        "v_or_b32 %3, %3, %20\n\t"
-        "v_or3_b32 %4, %0, %1, %2\n\t"
-        "v_or_b32 %4, %4, %3"
-        : "=&v"(gq[0]), "=&v"(gq[1]), "=&v"(gq[2]), "=&v"(gq[3]), "=&v"(g)
-        : "v"(H[0]), "v"(H[1]), "v"(H[2]), "v"(H[3]), "v"(H[4]), "v"(H[5]), "v"(H[6]),
-          "v"(H[7]), "v"(H[8]), "v"(H[9]), "v"(H[10]), "v"(H[11]), "v"(H[12]), "v"(H[13]),
-          "v"(H[14]), "v"(H[15]));
+    int v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = __float_as_int(H[i]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) gq[q] = (v[4 * q] | v[4 * q + 1] | v[4 * q + 2]) | v[4 * q + 3];
+    g = (gq[0] | gq[1] | gq[2]) | gq[3];
 }
 
 // the sign bits of a group's four values as its 4-bit candidate mask

@@ -680,23 +680,34 @@ def test_cull_shards_and_updates(renderer, K, k):
     assert st["segments"] == segs
 
 
-def test_reserved_renders_allocate_nothing(renderer):
+@pytest.mark.parametrize("flags", [0, abi.RT_FLAG_CULL], ids=["brute", "cull"])
+def test_reserved_renders_allocate_nothing(renderer, flags):
     """After rt_reserve, rt_render (host output, both in-flight slots) and
-    rt_render_frames_device of the reserved size make no device allocation."""
+    rt_render_frames_device of the reserved size make no device allocation --
+    with RT_FLAG_CULL too (rt_reserve builds the culled list), and after a
+    sphere update (the lists are rebuilt in place)."""
     import torch
     sp, mt = arrays(scene.rtiow_final_scene())
     renderer.set_scene(sp, mt)
     cam = default_camera_block()
     W, H, S, D = 64, 40, 9, 6
-    renderer.reserve(2, W, H, S, D)
+    renderer.reserve(2, W, H, S, D, flags=flags)
     before = renderer.alloc_count()
     for f0 in (0, 9, 18):  # rt_render alternates the two slots
-        img, _ = renderer.render(cam, W, H, S, D, frame0=f0)
+        img, _ = renderer.render(cam, W, H, S, D, frame0=f0, flags=flags)
     buf = torch.empty((2, H, W, 4), dtype=torch.float32, device="cuda")
-    renderer.render_frames_device(cam, 2, buf.data_ptr(), W, H, S, D)
+    renderer.render_frames_device(cam, 2, buf.data_ptr(), W, H, S, D, flags=flags)
     renderer.wait()
     assert renderer.alloc_count() == before
     check_exact(img, O.render(cam, sp, mt, W, H, S, D, frame0=18)[0])
+    moved = sp[5:7].copy()
+    moved["center"] += np.float32(0.25)
+    renderer.update_spheres(5, moved)
+    img, _ = renderer.render(cam, W, H, S, D, frame0=18, flags=flags)
+    assert renderer.alloc_count() == before
+    sp2 = sp.copy()
+    sp2[5:7] = moved
+    check_exact(img, O.render(cam, sp2, mt, W, H, S, D, frame0=18)[0])
 
 
 def test_failed_scene_upload_leaves_no_scene():
