@@ -18,15 +18,15 @@ max over ranks. value = algorithmic ray segments of the whole frame (all ranks)
 per second, every segment traced (primary-hit reuse off for the headline;
 its frame time is reported separately as `primary_reuse`).
 
-Roofline: the metric's fp32 roofline. achieved = traced segments x 18 x
-N_spheres flops (the reference's fp32 sphere tests) per render launch / that
-launch's average duration (HIP events on the stream the kernel runs on);
-peak = 157.3 TFLOP/s (MI355X fp32: f32 MFMA = packed VALU,
-/opt/skills/guides/MI355X_MICROARCH.md). The kernel runs the brute-force
-walk's conservative filter as f16 MFMA tiles and the exact fp32 test only on
-candidates, so frac may exceed 1; the executed matrix work (f16 flops, matrix
-pipe busy) and VALU busy come from the rocprofv3 PMC record in profiles/, as
-does the HBM traffic (see DESIGN.md "Measurement").
+Roofline: SIMD issue, the resource the kernel executes on:
+the render kernel's issue cycles per launch (rocprofv3 PMC record in
+profiles/pmc_traffic.json: 4 per VALU instruction, 2 per 32-bit integer one,
+8 per MFMA) over that launch's duration (HIP events on the stream the kernel
+runs on), against 1024 SIMDs x the profiled clock. The metric's fp32 roofline
+(the reference's 18 x N_spheres fp32 flops per segment over 157.3 TF) is kept
+as `fp32_algorithm_ratio`: the kernel runs the brute-force walk's filter as
+f16 MFMA tiles and the exact fp32 test only on candidates, so that ratio
+exceeds 1. Matrix pipe, VALU busy and HBM traffic come from the same record.
 
 cpu_baseline: the C oracle (oracle/, a scalar port of the WGSL) timed on this
 host on a bounded row sample of the same frame, rank 0 at N=1 only.
@@ -148,6 +148,33 @@ def mfma_report(e):
         out["mfma_busy"] = round(m["mfma_busy"], 4)
         out["formula_busy"] = m["formula_busy"]
     return out
+
+
+def simd_issue_roofline(e, frames_per_launch, kms_launch):
+    """The bound the kernel runs against: SIMD issue. Issue
+    cycles per launch from the PMC record (tools/pmc_summary.py: 4 per VALU
+    instruction, 2 per 32-bit integer one, 8 per MFMA; counts scale with the
+    frames of a launch), over this run's HIP-event launch time, against the
+    1024 SIMDs x the clock the profiled launch ran at."""
+    si = (e or {}).get("simd_issue")
+    if not si or not si.get("clock_ghz"):
+        return {"bound": "SIMD issue", "achieved": None, "peak": None,
+                "unit": "G SIMD-issue cycles/s", "frac": None,
+                "note": "no PMC record for this workload in profiles/pmc_traffic.json"}
+    cycles = si["issue_cycles_per_launch"] / e["frames_per_launch"] * frames_per_launch
+    achieved = cycles / (kms_launch * 1e-3) / 1e9
+    peak = 1024 * si["clock_ghz"]
+    return {"bound": "SIMD issue", "achieved": round(achieved, 1), "peak": round(peak, 1),
+            "unit": "G SIMD-issue cycles/s", "frac": round(achieved / peak, 4),
+            "issue": {"valu_share_under_pmc": round(si["valu_share"], 4),
+                      "mfma_share_under_pmc": round(si["mfma_share"], 4),
+                      "busy_under_pmc": round(si["busy"], 4),
+                      "clock_ghz_under_pmc": round(si["clock_ghz"], 4),
+                      "kernel_ms_under_pmc": round(si["kernel_ms_under_pmc"], 3),
+                      "issue_cycles_per_launch": cycles,
+                      "formula": si["formula"], "clock_formula": si["clock_formula"],
+                      "source": "profiles/pmc_traffic.json (rocprofv3 --pmc, one launch of %d "
+                                "frames, tools/pmc_round.sh)" % e["frames_per_launch"]}}
 
 
 def spawn_ranks(args):
@@ -400,6 +427,28 @@ def main():
     traffic = load_traffic(pmc, args.steps / max(1, len(sizes)))
     kms_launch = kernel_ms_total / launches
 
+    roofline = simd_issue_roofline(pmc, args.steps / max(1, len(sizes)), kms_launch)
+    roofline.update({
+        "traffic": traffic,
+        # HBM GB/s of the render kernel: PMC bytes per launch / this run's
+        # HIP-event launch time (peak ~8,000 GB/s: not the bound)
+        "hbm_gbps": round(traffic / (kms_launch * 1e-3) / 1e9, 2) if traffic else None,
+        "hbm_peak_gbps": 8000.0,
+        "valu_busy": valu_report(pmc),
+        "matrix_core": mfma_report(pmc),
+        "kernel": "rt_render_kernel",
+        "kernel_ms_per_launch": round(kms_launch, 3),
+        # the metric's fp32 roofline, kept as a ratio: the reference
+        # algorithm's 18 x N fp32 flops per traced segment at this rate over
+        # the 157.3 TF fp32 peak -- above 1 because the kernel does not execute
+        # them (the filter runs as f16 MFMA tiles, the exact fp32 test only on
+        # candidates)
+        "fp32_algorithm_tflops": round(achieved, 3),
+        "fp32_algorithm_ratio": round(achieved / PEAK_FP32_TFLOPS, 4),
+        "fp32_algorithm_basis": ("traced segments x 18 x N_spheres (intersect.wgsl:97-102, SURVEY "
+                                 "8d) per render launch / its HIP-event duration, over 157.3 TF"),
+    })
+
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -420,25 +469,7 @@ def main():
                                    + ("RCCL gather" if args.dist_backend == "nccl"
                                       else "host-staged gloo gather (rehearsal)"))
                    if dist_on else "single GPU"},
-        "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
-                     "traffic": traffic,
-                     # HBM GB/s of the render kernel: PMC bytes per launch / this
-                     # run's HIP-event launch time (peak ~8,000 GB/s: not the bound)
-                     "hbm_gbps": (round(traffic / (kms_launch * 1e-3) / 1e9, 2)
-                                  if traffic else None),
-                     "hbm_peak_gbps": 8000.0,
-                     "valu_busy": valu_report(pmc),
-                     "matrix_core": mfma_report(pmc),
-                     "kernel": "rt_render_kernel",
-                     "kernel_ms_per_launch": round(kms_launch, 3),
-                     "flops_per_launch": flops_total / launches,
-                     "basis": ("algorithmic: traced segments x 18 x N_spheres, the reference's fp32 "
-                               "sphere tests (intersect.wgsl:97-102) against the fp32 peak (= f32 "
-                               "MFMA = packed VALU, 157.3 TF). Executed: the brute-force walk's "
-                               "conservative filter as f16 hi/lo MFMA tiles (matrix_core), the exact "
-                               "fp32 test only on candidates, so frac can exceed 1 at bit-identical "
-                               "output (DESIGN.md 4.7)")},
+        "roofline": roofline,
         "segments_per_frame": int(segs_all / args.steps),
         "traced_segments_per_frame": int(traced_all / args.steps),
         "primary_reuse": reuse,

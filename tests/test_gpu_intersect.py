@@ -126,3 +126,42 @@ def test_matches_reference_intersect_world(renderer, path, flags):
     hit = idx >= 0
     assert np.array_equal(~hit, z["t"] == np.float32(1e20))
     assert np.array_equal(sp["material"][idx[hit]], z["material"][hit])
+
+
+@pytest.mark.parametrize("fast", [True, False], ids=["short_math", "ieee"])
+def test_valu_and_matrix_waves_side_by_side(renderer, fast):
+    """Round 2 saw VALU-walk waves miss hits only while other waves of the same
+    kernel ran the matrix-core walk (hazards). Here every other
+    wave of 64 rays holds one ray whose origin is outside the f16 split's range
+    (|o| > 2^12: that wave takes the packed VALU filter) and the rest are near
+    (the matrix-core filter), so the two walks run side by side on every CU;
+    four launches, each bit-exact against the oracle."""
+    if not fast:
+        renderer.tune(fast_exact=0)
+    sp, _ = SCENES["mixed"]()
+    from bevy_raytrace_amd.abi import MATERIAL_DTYPE
+    mt = np.zeros(int(sp["material"].max()) + 1, dtype=MATERIAL_DTYPE)
+    rays = adversarial_rays(sp, 400_000, seed=zlib.crc32(b"side_by_side") % 1000)
+    o = rays[:, :3]
+    near = (np.abs(o).max(1) <= 100.0)
+    far = np.abs(o).max(1) > 2.0 ** 12
+    nr, fr = rays[near], rays[far]
+    nw = len(nr) // 63
+    assert nw > 2000 and len(fr) > 0
+    waves = []
+    for w in range(nw):
+        blk = nr[63 * w:63 * w + 63]
+        if w & 1:  # one far ray at a varying lane: a VALU-walk wave
+            blk = np.insert(blk, w % 64, fr[w % len(fr)], axis=0)
+        else:
+            blk = np.vstack([blk, nr[(63 * w + 7) % len(nr)]])
+        waves.append(blk)
+    rays = np.ascontiguousarray(np.vstack(waves), dtype=np.float32)
+    renderer.set_scene(sp, mt)
+    ci, ct = O.intersect_batch(sp, rays)
+    assert (ci >= 0).mean() > 0.05
+    for rep in range(4):
+        gi, gt = renderer.intersect(rays)
+        bad = np.nonzero((gi != ci) | (gt.view(np.uint32) != ct.view(np.uint32)))[0]
+        assert bad.size == 0, f"launch {rep}: {bad.size} rays differ, e.g. {bad[:8].tolist()}"
+

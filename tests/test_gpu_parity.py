@@ -142,6 +142,29 @@ def test_other_camera(renderer):
     assert st["segments"] == segs
 
 
+@pytest.mark.parametrize("flags", [0, NO_REUSE], ids=["reuse", "noreuse"])
+def test_far_camera_alternates_walks(renderer, flags):
+    """The RTIOW scene seen from 400x the default camera distance (|o| ~ 5,500
+    > 2^12, the f16 split's range): a wave holding a primary ray walks the
+    sphere list with the packed VALU filter, a wave of bounce rays (near the
+    scene) with the matrix-core filter, so waves switch walks from one
+    iteration to the next (with primary-hit reuse on, most iterations are
+    bounces). Bit-exact against the oracle; the oracle confirms both kinds of
+    segments occur in quantity."""
+    sp, mt = arrays(scene.rtiow_final_scene())
+    eye = np.array([13.0, 2.0, 3.0]) * 400.0
+    cam = camera_block(Transform.from_xyz(*eye).looking_at((0.0, 0.5, 0.0)), fov=0.0055)
+    W, H, S, D = 96, 54, 16, 8
+    renderer.set_scene(sp, mt)
+    img, st = renderer.render(cam, W, H, S, D, flags=flags)
+    ref, segs = O.render(cam, sp, mt, W, H, S, D)
+    check_exact(img, ref)
+    assert st["segments"] == segs
+    # primary segments (far origin) = W*H*S; the rest are bounces near the
+    # scene (the view is filled: most primaries hit and bounce)
+    assert 1.5 * W * H * S < segs < 8 * W * H * S
+
+
 def test_multi_pass_scratch_identical(renderer):
     """Block sums folded over several passes == one pass (sequential fold)."""
     sp, mt = arrays(scene.config1_scene())
