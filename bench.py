@@ -81,6 +81,9 @@ def parse():
     ap.add_argument("--cull-steps", type=int, default=-1,
                     help="extra frames timed with the culled list, RT_FLAG_CULL (0 = skip; "
                          "default 12 at N=1, skipped at N>1)")
+    ap.add_argument("--shim-frames", type=int, default=120,
+                    help="--config reference1080: frames timed through the Bevy shim's call "
+                         "sequence (rt_wait, dirty check, rt_render_async into a host buffer)")
     ap.add_argument("--lib", default=None,
                     help="A/B only: another build of librt_hip.so (same ABI), e.g. a previous "
                          "round's, to compare on one box")
@@ -175,6 +178,70 @@ def simd_issue_roofline(e, frames_per_launch, kms_launch):
                       "formula": si["formula"], "clock_formula": si["clock_formula"],
                       "source": "profiles/pmc_traffic.json (rocprofv3 --pmc, one launch of %d "
                                 "frames, tools/pmc_round.sh)" % e["frames_per_launch"]}}
+
+
+def shim_sequence(r, cam, spheres, mats, W, H, S, D, nframes):
+    """The Bevy shim's per-frame calls (bevy_shim/src/ray_trace_node.rs
+    RayTraceNode::update, double-buffered): finish the frame enqueued last
+    update (rt_wait), compare the packed scene bytes with the uploaded ones
+    (the dirty check; nothing changes here), rt_render_async the next frame
+    into the host buffer not on show. Timed per flag set with the shim's
+    pageable host buffers (a Rust Vec<f32>), with page-locked ones, and with
+    rt_render_device (no device-to-host copy), so the copy's share of a frame
+    is measured, not assumed."""
+    import torch
+    sp_bytes, mt_bytes = spheres.tobytes(), mats.tobytes()
+    out = {"frames": nframes, "spp": S, "max_depth": D,
+           "note": "per-frame latency of the drop-in path: the reference renders into its "
+                   "texture on the device; the shim copies the Rgba32Float frame to the host "
+                   "for Bevy's write_texture"}
+    for fname, flags in (("brute", abi.RT_FLAG_NO_PRIMARY_CACHE), ("cull", abi.RT_FLAG_CULL)):
+        r.reserve(1, W, H, S, D, flags=flags)
+        res = {}
+        for mode in ("pageable", "pinned", "device"):
+            if mode == "pageable":
+                bufs = [np.empty((H, W, 4), np.float32) for _ in range(2)]
+            elif mode == "pinned":
+                bufs = [torch.empty((H, W, 4), dtype=torch.float32, pin_memory=True).numpy()
+                        for _ in range(2)]
+            else:
+                bufs = [torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+                        for _ in range(2)]
+            calls, stats = [], []
+            pending, ready, t0 = None, None, 0.0
+            for f in range(nframes + 8):  # 8 untimed frames first
+                if f == 8:
+                    torch.cuda.synchronize()
+                    calls, stats, t0 = [], [], time.perf_counter()
+                if pending is not None:  # step 1: rt_wait for last update's frame
+                    stats.append(r.wait())
+                    ready, pending = pending, None
+                dirty = spheres.tobytes() != sp_bytes or mats.tobytes() != mt_bytes  # step 2
+                assert not dirty
+                i = 0 if ready is None else 1 - ready
+                tc = time.perf_counter()
+                if mode == "device":
+                    r.render_device(cam, bufs[i].data_ptr(), W, H, S, D, frame0=f, flags=flags)
+                else:
+                    r.render_async(cam, bufs[i], W, H, S, D, frame0=f, flags=flags)
+                calls.append(time.perf_counter() - tc)
+                pending = i
+            stats.append(r.wait())
+            dt = time.perf_counter() - t0
+            res[mode] = {"frame_interval_ms": round(dt / nframes * 1e3, 4),
+                         "fps": round(nframes / dt, 1),
+                         "enqueue_call_ms": round(float(np.mean(calls)) * 1e3, 4),
+                         "gpu_total_ms": round(float(np.mean([s["total_ms"] for s in stats])), 4),
+                         "kernel_ms": round(float(np.mean([s["kernel_ms"] for s in stats])), 4),
+                         "mrays_per_s": round(float(np.mean([s["segments"] for s in stats]))
+                                              / (dt / nframes) / 1e3, 1)}
+        dev = res["device"]["gpu_total_ms"]
+        for mode in ("pageable", "pinned"):
+            d2h = res[mode]["gpu_total_ms"] - dev
+            res[mode]["d2h_ms"] = round(d2h, 4)
+            res[mode]["d2h_share_of_frame"] = round(d2h / res[mode]["frame_interval_ms"], 4)
+        out[fname] = res
+    return out
 
 
 def spawn_ranks(args):
@@ -490,6 +557,8 @@ def main():
         out["tune"] = args.tune
     if args.lib:
         out["lib"] = os.path.relpath(os.path.abspath(args.lib), ROOT)
+    if world == 1 and wl.key == "reference1080" and args.shim_frames > 0:
+        out["shim_sequence"] = shim_sequence(r, cam, spheres, mats, W, H, S, D, args.shim_frames)
     if world == 1 and not args.no_cpu_baseline:
         def gpu_shard(K, j):
             """Rows of shard j of K (one-row blocks, dealt serpentine: spread

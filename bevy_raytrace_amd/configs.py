@@ -35,6 +35,12 @@ WORKLOADS = {
                         "same scene, 8K, 1024 spp, row-tiled over 8 GPUs"),
     "spheres10k1080": Workload("spheres10k1080", 1920, 1080, 128, 16, "ten_thousand_scene", 1,
                                "10,000 spheres, 128 spp (sphere list streamed)"),
+    # the reference's own per-frame workload through the drop-in path:
+    # RENDER_TARGET_SIZE 1920x1080, SAMPLES_PER_RAY 1 (src/lib.rs:25-26), 3
+    # (intersect, shade) rounds (src/ray_trace_node.rs:213), its dim-7 scene
+    # with its own material split (src/sphere.rs:48-91)
+    "reference1080": Workload("reference1080", 1920, 1080, 1, 3, "reference_scene", 1,
+                              "the reference's own frame: 1 spp, depth 3, dim-7 scene"),
 }
 
 HEADLINE = "rtiow1080"

@@ -635,21 +635,26 @@ static int quiesce(rt_ctx* ctx) {  // no kernel may be reading the scene while i
 // ---- matrix-core filter fragments (rt_dev_intersect.h intersect_world_mfma) ----
 // The filter value less the ray's k1^2, H0 = S' + L.c + sum_ab Q_ab c_a c_b, is
 // one 32-term dot product of a sphere row and a ray column (K = 32: two
-// chained v_mfma_f32_32x32x16_f16). Sphere row j, each feature as f16 hi/lo:
-//   K 0..8   c_a          [hi, hi, lo] for a = x, y, z
-//   K 9..26  c_a c_b 2^-sq [hi, hi, lo] for ab = xx, yy, zz, xy, xz, yz
-//   K 27, 28 S' = r^2 - (1 - m - mu')|c|^2  [hi, lo]
-//   K 29, 30 1, 1                         (against the ray's T0 hi, lo)
-//   K 31     0
-// (the ray column holds the negated partner parts [hi, lo, hi], -1, -1 against
-// S' and T0's parts: the MFMAs give T0 - H0, rt_dev_intersect.h).
-// hi = RN_f16(x), lo = RN_f16(x - hi), all from double. sq scales the
-// quadratic features into f16 range (max |c_a c_b| 2^-sq <= 2^14); the ray
-// side carries 2^sq. Block b (spheres 32b..32b+31): two uint4 per lane, A0
-// (K 0..15) then A1 (K 16..31), 64 lanes each; lane l: row l & 31, elements
-// k = 8 (l >> 5) .. + 8 of that half. Pad rows: 0, S'_hi = -inf (T0 - H0 =
-// +inf or NaN: never a candidate). Only scenes with |c_i| <= 2^12 and |S'| <= 2^15
-// take it (mf_ok); the rest keep the VALU filter.
+// chained v_mfma_f32_32x32x16_f16). The sphere's features y_0..y_8 = c_x, c_y,
+// c_z, then c_a c_b 2^-sq for ab = xx, yy, zz, xy, xz, yz, each as f16 hi/lo;
+// row j in words of two halves (K 2m, 2m+1 in word m):
+//   K group 0  w0..w3   (hi y0, hi y1) .. (hi y6, hi y7)
+//              w4..w7   (lo y0, lo y1) .. (lo y6, lo y7)
+//   K group 1  w8..w11  (hi y0, hi y1) .. (hi y6, hi y7)
+//              w12      (hi y8, hi y8)
+//              w13      (lo y8, 1)          1 against the ray's T0 hi
+//              w14      (1, S' hi)          S' = r^2 - (1 - m - mu')|c|^2
+//              w15      (S' lo, 0)
+// against the ray column's hi x / hi x / lo x pairs, (hi x8, lo x8), (hi x8,
+// T0 hi), (T0 lo, -1), (-1, 0) (x = the NEGATED ray features): the MFMAs give
+// T0 - H0 (rt_dev_intersect.h). hi = RN_f16(x), lo = RN_f16(x - hi), all from
+// double. sq scales the quadratic features into f16 range (max |c_a c_b|
+// 2^-sq <= 2^14); the ray side carries 2^sq. Block b (spheres 32b..32b+31):
+// two uint4 per lane, A0 (K 0..15) then A1 (K 16..31), 64 lanes each; lane l:
+// row l & 31, elements k = 8 (l >> 5) .. + 8 of that half. Pad rows: 0, the
+// two 1s, S' hi = -inf (T0 - H0 = +inf or NaN: never a candidate). Only scenes
+// with |c_i| <= 2^12 and |S'| <= 2^15 take it (mf_ok); the rest keep the VALU
+// filter.
 static uint16_t f16_bits(double x) {
     const _Float16 h = (_Float16)x;
     uint16_t u;
@@ -691,28 +696,24 @@ static int build_mfma(rt_ctx* ctx) {
             if (j < n) {
                 const float4 q = ctx->h_sph[j];
                 const double c[3] = {q.x, q.y, q.z};
-                uint16_t hi, lo;
-                for (int a = 0; a < 3; ++a) {
-                    f16_split(c[a], hi, lo);
-                    row[3 * a] = hi;
-                    row[3 * a + 1] = hi;
-                    row[3 * a + 2] = lo;
+                uint16_t hi[9], lo[9];
+                for (int a = 0; a < 3; ++a) f16_split(c[a], hi[a], lo[a]);
+                for (int f = 0; f < 6; ++f)
+                    f16_split(std::ldexp(c[QA[f]] * c[QB[f]], -sq), hi[3 + f], lo[3 + f]);
+                for (int f = 0; f < 8; ++f) {
+                    row[f] = hi[f];       // w0..w3
+                    row[8 + f] = lo[f];   // w4..w7
+                    row[16 + f] = hi[f];  // w8..w11
                 }
-                for (int f = 0; f < 6; ++f) {
-                    f16_split(std::ldexp(c[QA[f]] * c[QB[f]], -sq), hi, lo);
-                    row[9 + 3 * f] = hi;
-                    row[9 + 3 * f + 1] = hi;
-                    row[9 + 3 * f + 2] = lo;
-                }
+                row[24] = row[25] = hi[8];  // w12
+                row[26] = lo[8];            // w13
                 const double S = (double)q.w - kS * (c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
                 if (!(std::fabs(S) <= 0x1p15)) return RT_OK;
-                f16_split(S, hi, lo);
-                row[27] = hi;
-                row[28] = lo;
+                f16_split(S, row[29], row[30]);  // w14 hi half, w15 lo half
             } else {
-                row[27] = f16_bits(-INFINITY);
+                row[29] = f16_bits(-INFINITY);
             }
-            row[29] = row[30] = f16_bits(1.0);  // against the ray's T0 hi, lo
+            row[27] = row[28] = f16_bits(1.0);  // against the ray's T0 hi, lo
             for (int half = 0; half < 2; ++half)  // A0: K 0..15, A1: K 16..31
                 std::memcpy(&h[(((size_t)b * 2 + half) * 64 + l) * 8], &row[16 * half + 8 * hh], 16);
         }

@@ -785,42 +785,62 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
     f[6] = ((2.0f * ex) * ey) * mf_qs;
     f[7] = ((2.0f * ex) * ez) * mf_qs;
     f[8] = ((2.0f * ey) * ez) * mf_qs;
-    // the ray column, K 0..31: per NEGATED feature [hi, lo, hi] (the sphere
-    // row holds [hi, hi, lo]), then -1, -1 (against S'_hi, S'_lo), T0's hi, lo
-    // (against 1, 1), 0: the dot product is T0 - H0. A lane without a ray has
-    // T0 = +inf (hi +inf, lo 0): V = +inf, never a candidate.
-    _Float16 col[32];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        const float x = -f[k];
-        const _Float16 hi = (_Float16)x;
-        const _Float16 lo = (_Float16)(x - (float)hi);
-        col[3 * k] = hi;
-        col[3 * k + 1] = lo;
-        col[3 * k + 2] = hi;
-    }
-    col[27] = (_Float16)-1.0f;
-    col[28] = (_Float16)-1.0f;
-    {
-        const _Float16 hi = (_Float16)T;
-        const float r = T - (float)hi;
-        col[29] = hi;
-        col[30] = (_Float16)(live ? r : 0.0f);
-    }
-    col[31] = (_Float16)0.0f;
+    // The ray column, 16 words of two f16 (K 2m, 2m+1 in word m), against the
+    // sphere rows of rt_api.cpp build_mfma (x_f = -f[f], the NEGATED features;
+    // y_f the sphere's; hi = RN_f16(x), lo = RN_f16(x - hi)):
+    //   K group 0  w0..w3   (hi x0, hi x1) .. (hi x6, hi x7)  vs (hi y) pairs
+    //              w4..w7   the same hi pairs                  vs (lo y) pairs
+    //   K group 1  w8..w11  (lo x0, lo x1) .. (lo x6, lo x7)  vs (hi y) pairs
+    //              w12      (hi x8, lo x8)                     vs (hi y8, hi y8)
+    //              w13      (hi x8, T0 hi)                     vs (lo y8, 1)
+    //              w14      (T0 lo, -1)                        vs (1, S' hi)
+    //              w15      (-1, 0)                            vs (S' lo, 0)
+    // -- per feature hi.hi + hi.lo + lo.hi, T0 against two exact 1s, -1 against
+    // S': the dot product is T0 - H0. The hi / lo pairs come from packed
+    // converts (v_cvt_pk_f16_f32, round to nearest even); x - hi is exact in
+    // f32. A lane without a ray has T0 = +inf (hi +inf, lo 0): V = +inf,
+    // never a candidate.
+    typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+    auto pk = [](float lo_half, float hi_half) {
+        const h2v v = {(_Float16)lo_half, (_Float16)hi_half};
+        uint32_t u;
+        __builtin_memcpy(&u, &v, 4);
+        return u;
+    };
+    // the f32 value of one half of a packed word: v_cvt_f32_f16 (SDWA for the
+    // upper half) of the word itself -- the empty asm keeps the compiler from
+    // converting x a second time for it
+    auto half_f32 = [](uint32_t u, int half) {
+        const uint16_t b = half ? (uint16_t)(u >> 16) : (uint16_t)u;
+        _Float16 x;
+        __builtin_memcpy(&x, &b, 2);
+        return (float)x;
+    };
     uint32_t w[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        uint16_t u0, u1;
-        __builtin_memcpy(&u0, &col[2 * k], 2);
-        __builtin_memcpy(&u1, &col[2 * k + 1], 2);
-        w[k] = (uint32_t)u0 | ((uint32_t)u1 << 16);
+    for (int q = 0; q < 4; ++q) {
+        const float xa = -f[2 * q], xb = -f[2 * q + 1];
+        uint32_t hi = pk(xa, xb);
+        asm volatile("" : "+v"(hi));
+        w[q] = w[4 + q] = hi;
+        w[8 + q] = pk(xa - half_f32(hi, 0), xb - half_f32(hi, 1));
+    }
+    {
+        const float x8 = -f[8];
+        uint32_t h8t = pk(x8, T);  // (hi x8, T0 hi)
+        asm volatile("" : "+v"(h8t));
+        const float l8 = x8 - half_f32(h8t, 0);
+        const float tl = live ? T - half_f32(h8t, 1) : 0.0f;
+        w[12] = pk(x8, l8);
+        w[13] = h8t;
+        w[14] = pk(tl, -1.0f);
+        w[15] = pk(-1.0f, 0.0f);
     }
     // B fragments of K group g (K 16g..16g+15), half t: lane l holds column
-    // l & 31, k = 8 (l >> 5) .. + 8. v_permlane32_swap(lo, hi) swaps lo's upper
-    // 32 lanes with hi's lower 32 (profiles/r02_permlane32_swap.log): from each
-    // lane's own K 16g..+7 (lo) and 16g+8..+15 (hi) its first result is half
-    // 0's fragment, its second half 1's.
+    // l & 31, k = 16g + 8 (l >> 5) .. + 8. v_permlane32_swap(lo, hi) swaps lo's
+    // upper 32 lanes with hi's lower 32 (profiles/r02_permlane32_swap.log): from
+    // each lane's own words 8g+q (K 16g + 2q ..) and 8g+4+q its first result is
+    // half 0's fragment word q, its second half 1's.
     uint32_t b0[2][4], b1[2][4];  // [K group][word] of half 0 / half 1
 #pragma unroll
     for (int g = 0; g < 2; ++g)

@@ -18,16 +18,21 @@
 // a pixel's slots in sample order -- the oracle's summation order.
 //
 // Intersection (the hot loop, intersect.wgsl:133-143): every sphere of the
-// list is tested for every live ray (brute force). The list is read as groups
-// of 8 spheres (SoA cx[8] cy[8] cz[8] S[8]) with scalar loads and fed to
-// hand-scheduled v_pk_fma_f32 as SGPR pairs (filter8: 28 packed FMAs + a
-// v_max3 chain + 1 compare per group):
+// list is tested for every live ray (brute force), in two stages. A
+// conservative filter proves most (sphere, ray) pairs miss: by default on the
+// matrix cores, one 32-term f16 hi/lo dot product per pair -- two chained
+// v_mfma_f32_32x32x16_f16 per 32-sphere x 32-ray tile give V = T0 - H0 and a
+// pair is a candidate iff V < 0 (rt_dev_intersect.h intersect_world_mfma,
+// DESIGN.md 4.7); the culled list, and waves with a ray outside the f16
+// split's range, run the same test as packed fp32 FMAs over groups of 8
+// spheres read with scalar loads (filter8):
 //   H - T = hb^2 + r^2 - (1 - m)|o - c|^2 + mu (|o|^2 + |c|^2),  hb = dn.(o - c)
 // H < T proves the reference's discriminant (intersect.wgsl:102) is negative.
-// Lanes queue their candidate groups (group, 8-bit mask) in LDS; after the
-// walk each lane runs the reference's exact op sequence (intersect.wgsl:
-// 97-115) on its own candidates in list order with the strict `<` tie-break
-// (:137), so the result is bit-identical to the brute-force reference loop.
+// Lanes queue their candidates in LDS; after the walk each lane runs the
+// reference's exact op sequence (intersect.wgsl:97-115) on its own candidates
+// with the strict `<` tie-break (:137; a (t, index) lexicographic minimum
+// where the candidates come in another order), so the result is
+// bit-identical to the brute-force reference loop.
 //
 // Sources: rt_dev_math.h (vector ops, correctly rounded short forms, camera
 // rays), rt_dev_intersect.h (exact test, filter8, candidate queues,

@@ -134,6 +134,23 @@ class Renderer:
                                               ctypes.c_void_p(int(stream)) if stream else None)
         check(self.lib, self.ctx, rc)
 
+    def render_async(self, camera: np.ndarray, out: np.ndarray, width, height, spp, max_depth,
+                     frame0=0, row_block=8, shard_count=1, shard_index=0, flags=0):
+        """rt_render_async: enqueue one frame whose image lands in the HOST
+        array `out` (rows, W, 4) float32 -- the Bevy shim's per-frame call
+        (bevy_shim/src/ray_trace_node.rs). Call wait() before reading it."""
+        cam = np.ascontiguousarray(camera, dtype=abi.CAMERA_DTYPE)
+        p = make_params(width, height, spp, max_depth, frame0, row_block, shard_count, shard_index,
+                        flags)
+        rows = self.lib.rt_shard_rows(p.height, p.row_block, max(1, p.shard_count), p.shard_index)
+        if out.dtype != np.float32 or not out.flags.c_contiguous or out.size < rows * int(width) * 4:
+            raise ValueError("render_async: out must be a C-contiguous float32 array of "
+                             f"{rows} x {width} x 4")
+        self._keep_async = getattr(self, "_keep_async", [])[-1:] + [(cam, p, out)]
+        rc = self.lib.rt_render_async(self.ctx, cam.ctypes.data_as(ctypes.c_void_p),
+                                      ctypes.byref(p), out.ctypes.data_as(ctypes.c_void_p))
+        check(self.lib, self.ctx, rc)
+
     def reserve(self, nframes, width, height, spp, max_depth, frame0=0, row_block=8,
                 shard_count=1, shard_index=0, flags=0):
         """Allocate the work buffers of a render_frames_device(nframes, ...) in

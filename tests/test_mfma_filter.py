@@ -67,19 +67,24 @@ def sphere_rows(sp, sq):
         hi = x.astype(H16)
         return hi, (x - hi.astype(D)).astype(H16)
 
-    cols = []
+    his, los = [], []
     for a in range(3):
         hi, lo = hl(c[:, a])
-        cols += [hi, hi, lo]
+        his.append(hi)
+        los.append(lo)
     for a, b in QUAD:
         hi, lo = hl(c[:, a] * c[:, b] * 2.0 ** -sq)
-        cols += [hi, hi, lo]
+        his.append(hi)
+        los.append(lo)
     S = r2 - (1.0 - M - MU) * (c ** 2).sum(1)
     assert np.all(np.abs(S) <= 2.0 ** 15)  # mf_ok
-    hi, lo = hl(S)
+    shi, slo = hl(S)
     n = len(sp)
     one = np.ones(n, H16)
-    cols += [hi, lo, one, one, np.zeros(n, H16)]  # K 29, 30: against T0's hi, lo
+    # K group 0: hi y0..y7, lo y0..y7; group 1: hi y0..y7, hi y8, hi y8, lo y8,
+    # 1, 1, S' hi, S' lo, 0 (build_mfma's words w0..w15)
+    cols = his[:8] + los[:8] + his[:8] + [his[8], his[8], los[8], one, one, shi, slo,
+                                          np.zeros(n, H16)]
     return np.stack(cols, 1).astype(F)
 
 
@@ -106,14 +111,17 @@ def ray_columns(rays, sq, abs_margin):
         feats = [fma32(F(2.0) * k1, e[:, a], o2[:, a]) for a in range(3)]
         feats += [((F(2.0) * e[:, a] if a != b else e[:, a]) * e[:, b]) * sc for a, b in QUAD]
         T0 = (fma32(-k1, k1, F(1.0 - M - MU) * oo) - F(abs_margin)).astype(F)
-    cols = []
+    his, los = [], []
     for x in feats:
         hi, lo = split(-x)
-        cols += [hi, lo, hi]
+        his.append(hi)
+        los.append(lo)
     m1, z = -np.ones(len(rays), F), np.zeros(len(rays), F)
     with np.errstate(invalid="ignore", over="ignore"):
         thi, tlo = split(T0)
-    cols += [m1, m1, thi, tlo, z]
+    # the kernel's words w0..w15: hi x0..x7 twice, lo x0..x7, (hi x8, lo x8),
+    # (hi x8, T0 hi), (T0 lo, -1), (-1, 0)
+    cols = his[:8] + his[:8] + los[:8] + [his[8], los[8], his[8], thi, tlo, m1, m1, z]
     return np.stack(cols, 1), T0
 
 
