@@ -180,28 +180,43 @@ def simd_issue_roofline(e, frames_per_launch, kms_launch):
                                 "frames, tools/pmc_round.sh)" % e["frames_per_launch"]}}
 
 
-def shim_sequence(r, cam, spheres, mats, W, H, S, D, nframes):
+def shim_sequence(r, cam, spheres, mats, W, H, S, D, nframes, host_work_ms=1.0):
     """The Bevy shim's per-frame calls (bevy_shim/src/ray_trace_node.rs
     RayTraceNode::update, double-buffered): finish the frame enqueued last
     update (rt_wait), compare the packed scene bytes with the uploaded ones
     (the dirty check; nothing changes here), rt_render_async the next frame
-    into the host buffer not on show. Timed per flag set with the shim's
-    pageable host buffers (a Rust Vec<f32>), with page-locked ones, and with
-    rt_render_device (no device-to-host copy), so the copy's share of a frame
-    is measured, not assumed."""
+    into the host buffer not on show. Timed per flag set into pageable host
+    buffers (a Rust Vec<f32>), the same buffers after rt_host_register (what
+    the shim does), page-locked torch buffers, and rt_render_device (no
+    device-to-host copy), so the copy's share of a frame is measured, not
+    assumed; then pageable vs registered again with `host_work_ms` of busy host
+    work per frame standing in for the rest of Bevy's frame, which a
+    registered buffer overlaps with the GPU's work and a pageable one cannot."""
     import torch
     sp_bytes, mt_bytes = spheres.tobytes(), mats.tobytes()
-    out = {"frames": nframes, "spp": S, "max_depth": D,
+    out = {"frames": nframes, "spp": S, "max_depth": D, "host_work_ms": host_work_ms,
            "note": "per-frame latency of the drop-in path: the reference renders into its "
                    "texture on the device; the shim copies the Rgba32Float frame to the host "
                    "for Bevy's write_texture"}
+
+    def busy(ms):
+        t = time.perf_counter() + ms * 1e-3
+        while time.perf_counter() < t:
+            pass
+
     for fname, flags in (("brute", abi.RT_FLAG_NO_PRIMARY_CACHE), ("cull", abi.RT_FLAG_CULL)):
         r.reserve(1, W, H, S, D, flags=flags)
         res = {}
-        for mode in ("pageable", "pinned", "device"):
-            if mode == "pageable":
+        for mode in ("pageable", "registered", "pinned", "device", "pageable+host_work",
+                     "registered+host_work"):
+            base = mode.split("+")[0]
+            work = host_work_ms if mode.endswith("host_work") else 0.0
+            if base in ("pageable", "registered"):
                 bufs = [np.empty((H, W, 4), np.float32) for _ in range(2)]
-            elif mode == "pinned":
+                if base == "registered":
+                    for b in bufs:
+                        r.host_register(b)
+            elif base == "pinned":
                 bufs = [torch.empty((H, W, 4), dtype=torch.float32, pin_memory=True).numpy()
                         for _ in range(2)]
             else:
@@ -220,23 +235,27 @@ def shim_sequence(r, cam, spheres, mats, W, H, S, D, nframes):
                 assert not dirty
                 i = 0 if ready is None else 1 - ready
                 tc = time.perf_counter()
-                if mode == "device":
+                if base == "device":
                     r.render_device(cam, bufs[i].data_ptr(), W, H, S, D, frame0=f, flags=flags)
                 else:
                     r.render_async(cam, bufs[i], W, H, S, D, frame0=f, flags=flags)
                 calls.append(time.perf_counter() - tc)
                 pending = i
+                busy(work)  # the rest of the app's frame
             stats.append(r.wait())
             dt = time.perf_counter() - t0
+            if base == "registered":
+                for b in bufs:
+                    r.host_unregister(b)
+            segs = float(np.mean([s["segments"] for s in stats]))
             res[mode] = {"frame_interval_ms": round(dt / nframes * 1e3, 4),
                          "fps": round(nframes / dt, 1),
                          "enqueue_call_ms": round(float(np.mean(calls)) * 1e3, 4),
                          "gpu_total_ms": round(float(np.mean([s["total_ms"] for s in stats])), 4),
                          "kernel_ms": round(float(np.mean([s["kernel_ms"] for s in stats])), 4),
-                         "mrays_per_s": round(float(np.mean([s["segments"] for s in stats]))
-                                              / (dt / nframes) / 1e3, 1)}
+                         "mrays_per_s": round(segs / (dt / nframes) / 1e6, 1)}
         dev = res["device"]["gpu_total_ms"]
-        for mode in ("pageable", "pinned"):
+        for mode in ("pageable", "registered", "pinned"):
             d2h = res[mode]["gpu_total_ms"] - dev
             res[mode]["d2h_ms"] = round(d2h, 4)
             res[mode]["d2h_share_of_frame"] = round(d2h / res[mode]["frame_interval_ms"], 4)

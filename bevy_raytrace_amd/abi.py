@@ -125,6 +125,8 @@ _PROTOS = {
                                                _VP, _VP]),
     "rt_reserve": (ctypes.c_int, [_VP, ctypes.POINTER(RtParams), ctypes.c_uint32]),
     "rt_render_async": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(RtParams), _VP]),
+    "rt_host_register": (ctypes.c_int, [_VP, _VP, ctypes.c_size_t]),
+    "rt_host_unregister": (ctypes.c_int, [_VP, _VP]),
     "rt_wait": (ctypes.c_int, [_VP, ctypes.POINTER(RtStats)]),
     "rt_assemble_shards": (ctypes.c_int, [_VP, _VP, _U32, _VP, _U32, _U32, _U32, _U32, _VP]),
     "rt_assemble_shard_frames": (ctypes.c_int,

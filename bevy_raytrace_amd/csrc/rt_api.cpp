@@ -128,6 +128,8 @@ struct rt_ctx {
     hipStream_t stream = nullptr;  // = fr[0].stream: scene uploads, intersect, progressive
     unsigned long long dbg[16] = {};  // diagnostic counters of the last waited frame
 
+    std::vector<std::pair<void*, size_t>> host_regs;  // rt_host_register'd buffers
+
     float4* d_prog = nullptr;       // progressive running sum (rt_render_progressive)
     size_t prog_cap = 0;
     uint64_t prog_total = 0;        // samples accumulated so far
@@ -301,6 +303,7 @@ void rt_destroy(rt_ctx* ctx) {
         if (f.stream) hipStreamSynchronize(f.stream);
         if (f.pending_stream) hipStreamSynchronize(f.pending_stream);
     }
+    for (const auto& r : ctx->host_regs) hipHostUnregister(r.first);
     hipFree(ctx->d_grp);
     hipFree(ctx->d_sph);
     hipFree(ctx->d_sph_rm);
@@ -1070,9 +1073,10 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     // processing order: tiles of tile_h x tile_w pixels (8 x 8 for a whole
     // image; a shard's tiles are one row block high, so a tile's pixels stay
     // neighbours in the image -- 8 packed shard rows would span two blocks
-    // shard_count x row_block rows apart). Only the work order changes: every
-    // pixel's result is its own.
-    const uint32_t th = (K > 1 && B < 8) ? B : 8, tw = (64 + th - 1) / th;
+    // shard_count x row_block rows apart; 9-row blocks, the N = 8 split of
+    // 1080 rows, give 9 x 8 tiles). Only the work order changes: every pixel's
+    // result is its own.
+    const uint32_t th = (K > 1 && B != 8 && B <= 12) ? B : 8, tw = (64 + th - 1) / th;
     K_.tile_h = th;
     K_.tile_w = tw;
     K_.tile_full_rows = rows / th;
@@ -1294,6 +1298,30 @@ int rt_render_async(rt_ctx* ctx, const rt_camera* camera, const rt_params* param
     rc = enqueue(ctx, *f, camera, params, 1, f->d_out, f->stream);
     if (rc) return rc;
     return commit(ctx, *f, f->stream, out_rgba, f->d_out, bytes);
+}
+
+int rt_host_register(rt_ctx* ctx, void* ptr, size_t bytes) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_host_register: ctx is NULL");
+    if (!ptr || !bytes) return fail(ctx, RT_ERR_INVALID_ARG, "rt_host_register: empty buffer");
+    for (const auto& r : ctx->host_regs)
+        if (r.first == ptr) return fail(ctx, RT_ERR_INVALID_ARG, "rt_host_register: %p already registered", ptr);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    ctx->host_regs.emplace_back(ptr, bytes);
+    return RT_OK;
+}
+
+int rt_host_unregister(rt_ctx* ctx, void* ptr) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_host_unregister: ctx is NULL");
+    for (size_t i = 0; i < ctx->host_regs.size(); ++i) {
+        if (ctx->host_regs[i].first != ptr) continue;
+        int rc = quiesce(ctx);  // no pending copy may still target it
+        if (rc) return rc;
+        ctx->host_regs.erase(ctx->host_regs.begin() + (long)i);
+        HIP_TRY(ctx, hipHostUnregister(ptr));
+        return RT_OK;
+    }
+    return fail(ctx, RT_ERR_INVALID_ARG, "rt_host_unregister: %p is not registered", ptr);
 }
 
 int rt_wait(rt_ctx* ctx, rt_stats* stats) {

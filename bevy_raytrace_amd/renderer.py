@@ -151,6 +151,15 @@ class Renderer:
                                       ctypes.byref(p), out.ctypes.data_as(ctypes.c_void_p))
         check(self.lib, self.ctx, rc)
 
+    def host_register(self, arr: np.ndarray):
+        """rt_host_register: page-lock a host array render_async writes (it
+        must outlive the registration: host_unregister or close)."""
+        check(self.lib, self.ctx, self.lib.rt_host_register(
+            self.ctx, ctypes.c_void_p(arr.ctypes.data), arr.nbytes))
+
+    def host_unregister(self, arr: np.ndarray):
+        check(self.lib, self.ctx, self.lib.rt_host_unregister(self.ctx, ctypes.c_void_p(arr.ctypes.data)))
+
     def reserve(self, nframes, width, height, spp, max_depth, frame0=0, row_block=8,
                 shard_count=1, shard_index=0, flags=0):
         """Allocate the work buffers of a render_frames_device(nframes, ...) in

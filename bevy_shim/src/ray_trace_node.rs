@@ -58,6 +58,8 @@ struct Uploaded {
 struct HostFrame {
     texels: Vec<f32>,
     size: (u32, u32),
+    /// texels' (pointer, length) as given to rt_host_register, if registered
+    registered: Option<(usize, usize)>,
 }
 
 pub struct RayTraceNode {
@@ -92,10 +94,11 @@ impl RayTraceNode {
             frame0: frame,
             row_block: 8,
             shard_count: 1,
-            // the culled sphere list: the same frame bit for bit as the
-            // reference's brute-force intersect_world, 1.35x faster on the
-            // RTIOW scene
-            flags: RT_FLAG_CULL,
+            // the brute-force walk (matrix-core filter): on the reference's
+            // own frame (1920x1080, 1 spp, depth 3, its dim-7 scene) it is
+            // faster than the culled list, 0.66 vs 0.80 ms of kernel per
+            // frame (profiles/r03_bench_reference1080.json: shim_sequence)
+            flags: 0,
             ..Default::default()
         }
     }
@@ -232,6 +235,22 @@ impl render_graph::Node for RayTraceNode {
         let buf = &mut self.frames[i];
         buf.texels.resize((size.0 * size.1 * 4) as usize, 0.0);
         buf.size = size;
+        // page-locked once per allocation: the device->host copy is then a DMA
+        // and rt_render_async returns at once instead of waiting for the frame
+        // (1.32 vs 0.03 ms per call at 1080p, profiles/r03_bench_reference1080.json)
+        let key = (buf.texels.as_ptr() as usize, buf.texels.len());
+        if buf.registered != Some(key) {
+            if let Some((p, _)) = buf.registered.take() {
+                let _ = self.ctx.check(unsafe { rt_host_unregister(self.ctx.0, p as *mut _) });
+            }
+            let bytes = buf.texels.len() * std::mem::size_of::<f32>();
+            match self.ctx.check(unsafe {
+                rt_host_register(self.ctx.0, buf.texels.as_mut_ptr() as *mut _, bytes)
+            }) {
+                Ok(()) => buf.registered = Some(key),
+                Err(e) => error!("rt_host_register: {e}"),
+            }
+        }
         let rc = unsafe {
             rt_render_async(self.ctx.0, self.camera.as_ptr() as *const _, &params,
                             buf.texels.as_mut_ptr())

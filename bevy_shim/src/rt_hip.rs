@@ -70,6 +70,10 @@ extern "C" {
     pub fn rt_render_async(ctx: *mut rt_ctx, camera: *const c_void, params: *const rt_params,
                            out_rgba: *mut f32) -> c_int;
     pub fn rt_wait(ctx: *mut rt_ctx, stats: *mut rt_stats) -> c_int;
+    // page-lock a host buffer rt_render_async writes: its copy is then a DMA
+    // and rt_render_async returns at once (pageable: it waits for the frame)
+    pub fn rt_host_register(ctx: *mut rt_ctx, ptr: *mut c_void, bytes: usize) -> c_int;
+    pub fn rt_host_unregister(ctx: *mut rt_ctx, ptr: *mut c_void) -> c_int;
     pub fn rt_intersect(ctx: *mut rt_ctx, rays: *const f32, n: u32, hit_index: *mut i32,
                         hit_t: *mut f32) -> c_int;
     pub fn rt_last_error(ctx: *const rt_ctx) -> *const c_char;

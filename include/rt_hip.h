@@ -262,10 +262,25 @@ int rt_render_frames_device(rt_ctx* ctx, const rt_camera* camera, const rt_param
 int rt_reserve(rt_ctx* ctx, const rt_params* params, uint32_t nframes);
 
 /* Asynchronous host-output variant: enqueue, return; rt_wait() completes the
- * device->host copy into out_rgba and fills stats. */
+ * device->host copy into out_rgba and fills stats. Into pageable memory the
+ * HIP runtime stages the copy and this call returns only once the frame has
+ * been copied; into a buffer given to rt_host_register it returns at once. */
 int rt_render_async(rt_ctx* ctx, const rt_camera* camera, const rt_params* params,
                     float* out_rgba);
 int rt_wait(rt_ctx* ctx, rt_stats* stats);
+
+/* Page-lock a host buffer that rt_render_async writes (the Bevy shim's two
+ * frame buffers), so the frame's device->host copy is a DMA straight into it
+ * and rt_render_async does not wait for the frame (measured: a 1080p frame
+ * blocks the pageable call for its whole 1.3 ms, the registered one for
+ * 0.03 ms, profiles/r03_bench_reference1080.json). No reference counterpart:
+ * the reference's frame stays on the GPU as the wgpu texture
+ * (src/ray_trace_output.rs:41-61); the drop-in path hands it to Bevy through
+ * the host. The buffer must stay allocated until rt_host_unregister(ptr) or
+ * rt_destroy. Registering an already registered pointer is an error;
+ * rt_host_unregister waits for pending frames first. */
+int rt_host_register(rt_ctx* ctx, void* ptr, size_t bytes);
+int rt_host_unregister(rt_ctx* ctx, void* ptr);
 
 /* Closest-hit query for a batch of rays against the current scene: the same
  * intersect_world code path the renderer traces with (intersect.wgsl:133-143).

@@ -72,9 +72,14 @@ def test_bench_line_carries_the_contract_fields():
     rf = d["roofline"]
     for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
         assert k in rf, k
-    assert rf["unit"] == "TFLOP/s" and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    # SIMD issue from the committed PMC record (none for config 1: achieved,
+    # peak and frac are null) and the metric's fp32 algorithm ratio beside it
+    assert rf["bound"] == "SIMD issue" and rf["unit"] == "G SIMD-issue cycles/s"
+    assert rf["frac"] is None or abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    assert rf["fp32_algorithm_ratio"] > 0 and rf["kernel_ms_per_launch"] > 0
     cb = d["cpu_baseline"]
     for k in ("value", "unit", "cores", "kind", "sample"):
         assert k in cb, k
     assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port"
     assert cb.get("gpu_rows_bit_exact") is True
+    assert cb.get("segments_equal") is True and cb.get("gpu_shard_equals_headline") is True

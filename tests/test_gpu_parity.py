@@ -165,6 +165,31 @@ def test_far_camera_alternates_walks(renderer, flags):
     assert 1.5 * W * H * S < segs < 8 * W * H * S
 
 
+def test_render_async_into_registered_host_buffers(renderer):
+    """The Bevy shim's per-frame path: rt_render_async into page-locked host
+    buffers (rt_host_register), two frames alternating, bit-exact against the
+    oracle; registering twice or unregistering an unknown buffer is refused."""
+    sp, mt = arrays(scene.reference_scene())
+    cam = default_camera_block()
+    W, H, S, D = 96, 54, 1, 3
+    renderer.set_scene(sp, mt)
+    bufs = [np.empty((H, W, 4), np.float32) for _ in range(2)]
+    for b in bufs:
+        renderer.host_register(b)
+    with pytest.raises(abi.RayTraceError):
+        renderer.host_register(bufs[0])
+    with pytest.raises(abi.RayTraceError):
+        renderer.host_unregister(np.empty(16, np.float32))
+    for f in range(4):
+        renderer.render_async(cam, bufs[f & 1], W, H, S, D, frame0=f)
+        st = renderer.wait()
+        ref, segs = O.render(cam, sp, mt, W, H, S, D, frame0=f)
+        check_exact(bufs[f & 1], ref)
+        assert st["segments"] == segs
+    for b in bufs:
+        renderer.host_unregister(b)
+
+
 def test_multi_pass_scratch_identical(renderer):
     """Block sums folded over several passes == one pass (sequential fold)."""
     sp, mt = arrays(scene.config1_scene())

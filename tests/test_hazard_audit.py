@@ -46,6 +46,17 @@ def test_rule_detects_short_and_accepts_padded(tmp_path, rule):
     assert audit_text(tmp_path, padded) == []
 
 
+def test_r6_packed_half_select_beside_mfma(tmp_path):
+    """op_sel / op_sel_hi on a VGPR source of v_pk_fma_f32 is refused in a
+    kernel with MFMAs; on an SGPR source, or without MFMAs, it is not."""
+    mf = "v_mfma_f32_32x32x16_f16 v[0:15], v[16:19], v[20:23], 0\n s_nop 11\n"
+    bc = "v_pk_fma_f32 v[30:31], v[32:33], s[0:1], v[34:35] op_sel_hi:[0,1,1]"
+    assert "R6" in audit_text(tmp_path, mf + bc)
+    assert audit_text(tmp_path, bc) == []
+    sg = "v_pk_fma_f32 v[30:31], s[2:3], v[32:33], v[34:35] op_sel_hi:[0,1,1]"
+    assert audit_text(tmp_path, mf + sg) == []
+
+
 def test_chained_mfma_accumulate_needs_no_wait(tmp_path):
     body = ("v_mfma_f32_32x32x16_f16 v[0:15], v[16:19], v[20:23], 0\n"
             " v_mfma_f32_32x32x16_f16 v[0:15], v[24:27], v[28:31], v[0:15]")
@@ -73,4 +84,4 @@ def test_shipped_kernels_have_every_wait_state(tmp_path):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "hazard_audit.py")],
                        capture_output=True, text=True, env=dict(os.environ, RT_AUDIT_ASM=str(out)))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-    assert "short pairs: 0" in r.stdout
+    assert "short pairs / refused forms: 0" in r.stdout

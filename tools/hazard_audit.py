@@ -21,6 +21,13 @@ following control flow backwards through every predecessor of a block:
       the next MFMA taking the same registers whole as C needs none.
   R4  VALU writes a VGPR -> v_permlane16/32_swap reading it: 2 wait states.
   R5  VALU writes a VGPR -> v_readlane / v_readfirstlane reading it: 1.
+  R6  (not a wait-state rule) in a kernel that issues MFMAs, no v_pk_*_f32
+      may select a VGPR source's halves with op_sel / op_sel_hi (anything but
+      op_sel:0, op_sel_hi:1 on a VGPR operand). Measured on gfx950: such
+      half-broadcasts return wrong values while other waves of the kernel run
+      MFMAs (tools/ubench/opsel_mfma.hip, tools/isect_diag.py).
+      hipcc itself emits these forms for f2{x, x} operands, so the rule is
+      checked on compiler code as well as on inline asm.
 
 The rules were read off hipcc's own output for probe kernels (the s_nop it
 inserts between each producer/consumer pair; tools/ubench/pk_opsel_probe.hip)
@@ -43,7 +50,7 @@ CSRC = os.path.join(ROOT, "bevy_raytrace_amd", "csrc")
 REG = re.compile(r"\b([vs])(\d+)\b|\b([vs])\[(\d+):(\d+)\]|\b(vcc|exec)\b")
 LABEL = re.compile(r"^(\.LBB\w+|[A-Za-z_]\w*):")
 BRANCH = re.compile(r"^\s*(s_branch|s_cbranch_\w+)\s+(\.LBB\w+)")
-NEED = {"R1": 1, "R2": 2, "R3": 12, "R4": 2, "R5": 1}
+NEED = {"R1": 1, "R2": 2, "R3": 12, "R4": 2, "R5": 1, "R6": 0}
 WINDOW = 12  # the largest wait-state requirement above
 
 
@@ -210,6 +217,19 @@ def audit_kernel(name, items):
                 j -= 1
 
     bad = []
+    has_mfma = any(it[0] == "inst" and it[1].is_mfma for it in items)
+    for it in items:
+        if not has_mfma or it[0] != "inst" or not re.match(r"v_pk_\w+_f32", it[1].op):
+            continue
+        c = it[1]
+        m1 = re.search(r"op_sel:\[([\d,]+)\]", c.text)
+        m2 = re.search(r"op_sel_hi:\[([\d,]+)\]", c.text)
+        sel = [int(x) for x in m1.group(1).split(",")] if m1 else [0, 0, 0]
+        hi = [int(x) for x in m2.group(1).split(",")] if m2 else [1, 1, 1]
+        for k, opnd in enumerate(c.ops[1:4]):
+            if opnd.startswith("v") and k < len(sel) and (sel[k] != 0 or hi[k] != 1):
+                bad.append(("R6", "asm" if c.in_asm else "compiler", c.text, c.text, 0))
+                break
     for i, it in enumerate(items):
         if it[0] != "inst" or not it[1].is_valu:
             continue
@@ -253,9 +273,12 @@ def main():
         print(f"{name[:60]:60s} {len(items):6d} lines, {n_asm:4d} asm instructions, "
               f"{len(bad)} short")
         for rule, where, p, c, w in bad[:20]:
-            print(f"   {rule} ({where}): {p!r} -> {c!r}: {w} of {NEED[rule]} wait states")
+            if rule == "R6":
+                print(f"   R6 ({where}): {c!r}: VGPR half-select in a kernel with MFMAs")
+            else:
+                print(f"   {rule} ({where}): {p!r} -> {c!r}: {w} of {NEED[rule]} wait states")
         total += len(bad)
-    print("short pairs:", total)
+    print("short pairs / refused forms:", total)
     return 1 if total else 0
 
 

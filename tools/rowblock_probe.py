@@ -18,7 +18,7 @@ r.set_scene(sc.objects_gpu(), sc.materials_gpu())
 W, H, S, D = wl.width, wl.height, wl.spp, wl.max_depth
 N = int(sys.argv[1])
 Bs = [int(b) for b in sys.argv[2:]] or [configs.pick_row_block(H, N), 8]
-F = 12
+F = int(os.environ.get("PROBE_F", "20"))
 buf = torch.empty((F, H, W, 4), dtype=torch.float32, device="cuda:0")
 
 

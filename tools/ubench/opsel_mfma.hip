@@ -13,7 +13,7 @@
 // v_mfma_f32_32x32x16_f16 (mode "mfma") or sleep (mode "idle"). A third mode
 // runs both filter forms in every wave and no MFMA at all ("valu").
 //
-//   hipcc --offload-arch=gfx950 -O3 -o opsel_mfma opsel_mfma.hip && ./opsel_mfma
+//   hipcc --offload-arch=gfx950 -O3 -fno-slp-vectorize -o opsel_mfma opsel_mfma.hip && ./opsel_mfma
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -116,17 +116,38 @@ __device__ __forceinline__ void grp_dup(f2 dx, f2 dy, f2 dz, f2 k1, f2 ox, f2 oy
           [sc] "s"(sc), [sd] "s"(sd));
 }
 
+// scalar reference: filter2's op order with one v_fma_f32 per step (compiled
+// with -fno-slp-vectorize: no packed ops), for sphere pair (cx, cy, cz, S)
+__device__ __forceinline__ f2 grp_scalar2(float ex, float ey, float ez, float k1, float ox,
+                                          float oy, float oz, f2 cx, f2 cy, f2 cz, f2 S) {
+    f2 h;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const float hb = __builtin_fmaf(ez, cz[e], __builtin_fmaf(ey, cy[e], __builtin_fmaf(ex, cx[e], k1)));
+        h[e] = __builtin_fmaf(ox, cx[e], __builtin_fmaf(oy, cy[e], __builtin_fmaf(oz, cz[e],
+                              __builtin_fmaf(hb, hb, S[e]))));
+    }
+    return h;
+}
+
 __device__ __forceinline__ unsigned neq(f2 a, f2 b) {
     return (__float_as_uint(a.x) != __float_as_uint(b.x)) + (__float_as_uint(a.y) != __float_as_uint(b.y));
 }
 
 // mode 0: even waves MFMA, odd waves both filter forms; 1: even waves idle;
-// 2: every wave both filter forms, no MFMA
+// 2: every wave both filter forms, no MFMA; 3: even waves v_permlane32_swap
+// chains; 4: even waves LDS queue traffic (ds_write / ds_read of other lanes'
+// words); 5: even waves the matrix-core walk's mix -- MFMA tiles, ORs of the
+// results, permlane swaps and LDS queue writes/reads (rt_dev_intersect.h)
 __global__ __launch_bounds__(256) void k_opsel(const float4* grp, uint32_t ngroups,
                                                const float* rays, int mode,
                                                unsigned* __restrict__ bad,
+                                               unsigned* __restrict__ bad_opsel,
+                                               unsigned* __restrict__ bad_dup,
                                                float* __restrict__ sink) {
+    __shared__ uint32_t q[4 * 64 * 8];
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
     const uint32_t gid = blockIdx.x * 256 + threadIdx.x;
     const bool filt = mode == 2 || (wave & 1);
     if (!filt) {
@@ -134,17 +155,55 @@ __global__ __launch_bounds__(256) void k_opsel(const float4* grp, uint32_t ngrou
             for (int i = 0; i < ITERS / 8; ++i) __builtin_amdgcn_s_sleep(8);
             return;
         }
+        uint32_t* wq = q + wave * 64 * 8;
+        if (mode == 3) {
+            uint32_t x = gid, y = gid * 7u;
+            for (int i = 0; i < ITERS * 16; ++i) {
+                const auto r = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+                x = r[0] + 1u;
+                y = r[1] ^ 3u;
+            }
+            sink[gid] = (float)(x ^ y);
+            return;
+        }
+        if (mode == 4) {
+            uint32_t acc = 0;
+            for (int i = 0; i < ITERS * 4; ++i) {
+                wq[(i & 7) * 64 + lane] = acc + (uint32_t)i;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                acc += wq[(i & 7) * 64 + (lane ^ 32u)];
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            sink[gid] = (float)acc;
+            return;
+        }
         h8v a, b;
         for (int k = 0; k < 8; ++k) {
-            a[k] = (_Float16)(0.001f * (float)((threadIdx.x + k) & 15));
-            b[k] = (_Float16)(0.002f * (float)((threadIdx.x * 3 + k) & 15));
+            a[k] = (_Float16)(0.001f * (float)((threadIdx.x + k) & 15) - 0.004f);
+            b[k] = (_Float16)(0.002f * (float)((threadIdx.x * 3 + k) & 15) - 0.01f);
         }
         f16x acc = {};
+        uint32_t cnt = 0, sw = gid;
         for (int i = 0; i < ITERS * 4; ++i) {
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, mode == 5 ? f16x{} : acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(b, a, acc, 0, 0, 0);
+            if (mode == 5) {
+                int o = 0;
+                for (int k = 0; k < 16; ++k) o |= __float_as_int(acc[k]);
+                if (__builtin_amdgcn_ballot_w64(o < 0) != 0) {
+                    wq[(cnt & 7) * 64 + lane] = (uint32_t)o;
+                    ++cnt;
+                }
+                const auto r = __builtin_amdgcn_permlane32_swap(sw, cnt, false, false);
+                sw = r[0] + r[1];
+                if ((i & 15) == 15) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    sw += wq[(cnt & 7) * 64 + (lane ^ 32u)];
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                }
+            }
         }
-        float s = 0.f;
+        float s = (float)sw;
         for (int k = 0; k < 16; ++k) s += acc[k];
         sink[gid] = s;
         return;
@@ -155,7 +214,7 @@ __global__ __launch_bounds__(256) void k_opsel(const float4* grp, uint32_t ngrou
     const f2 dx = {ex, ex}, dy = {ey, ey}, dz = {ez, ez}, kk = {k1, k1}, oxx = {ox, ox},
              oyy = {oy, oy}, ozz = {oz, oz};
     const cfloat4* gp = (const cfloat4*)(uintptr_t)grp;
-    unsigned nbad = 0;
+    unsigned nbad = 0, nbad_seen = 0, nb_op = 0, nb_dup = 0;
     float acc = 0.f;
     for (int it = 0; it < ITERS; ++it) {
         const uint32_t g = (uint32_t)it % ngroups;
@@ -172,9 +231,24 @@ __global__ __launch_bounds__(256) void k_opsel(const float4* grp, uint32_t ngrou
                 f2{Z0.x, Z0.y}, f2{Z0.z, Z0.w}, f2{Z1.x, Z1.y}, f2{Z1.z, Z1.w}, f2{S0.x, S0.y},
                 f2{S0.z, S0.w}, f2{S1.x, S1.y}, f2{S1.z, S1.w}, a1, b1, c1, d1);
         nbad += neq(a0, a1) + neq(b0, b1) + neq(c0, c1) + neq(d0, d1);
+        if (nbad != nbad_seen) {  // which form is off: both against the scalar reference
+            nbad_seen = nbad;
+            const f2 ra = grp_scalar2(ex, ey, ez, k1, ox, oy, oz, f2{X0.x, X0.y}, f2{Y0.x, Y0.y},
+                                      f2{Z0.x, Z0.y}, f2{S0.x, S0.y});
+            const f2 rb = grp_scalar2(ex, ey, ez, k1, ox, oy, oz, f2{X0.z, X0.w}, f2{Y0.z, Y0.w},
+                                      f2{Z0.z, Z0.w}, f2{S0.z, S0.w});
+            const f2 rc = grp_scalar2(ex, ey, ez, k1, ox, oy, oz, f2{X1.x, X1.y}, f2{Y1.x, Y1.y},
+                                      f2{Z1.x, Z1.y}, f2{S1.x, S1.y});
+            const f2 rd = grp_scalar2(ex, ey, ez, k1, ox, oy, oz, f2{X1.z, X1.w}, f2{Y1.z, Y1.w},
+                                      f2{Z1.z, Z1.w}, f2{S1.z, S1.w});
+            nb_op += neq(a0, ra) + neq(b0, rb) + neq(c0, rc) + neq(d0, rd);
+            nb_dup += neq(a1, ra) + neq(b1, rb) + neq(c1, rc) + neq(d1, rd);
+        }
         acc += a0.x + d1.y;
     }
     bad[gid] = nbad;
+    bad_opsel[gid] = nb_op;
+    bad_dup[gid] = nb_dup;
     sink[gid] = acc;
 }
 
@@ -194,27 +268,34 @@ int main(int argc, char** argv) {
     for (size_t i = 0; i < (size_t)n; ++i)
         for (int k = 0; k < 8; ++k) hr[i * 8 + k] = (k < 3 ? 2.f * U() - 1.f : 26.f * U() - 13.f);
     float *dg, *dr, *sink;
-    unsigned* dbad;
+    unsigned *dbad, *dbo, *dbd;
     hipMalloc(&dg, hg.size() * 4);
     hipMalloc(&dr, hr.size() * 4);
     hipMalloc(&sink, (size_t)n * 4);
     hipMalloc(&dbad, (size_t)n * 4);
+    hipMalloc(&dbo, (size_t)n * 4);
+    hipMalloc(&dbd, (size_t)n * 4);
     hipMemcpy(dg, hg.data(), hg.size() * 4, hipMemcpyHostToDevice);
     hipMemcpy(dr, hr.data(), hr.size() * 4, hipMemcpyHostToDevice);
-    std::vector<unsigned> hb(n);
-    const char* names[3] = {"mfma (even waves MFMA, odd waves filter)",
+    std::vector<unsigned> hb(n), hbo(n), hbd(n);
+    const char* names[6] = {"mfma (even waves MFMA, odd waves filter)",
                             "idle (even waves s_sleep, odd waves filter)",
-                            "valu (every wave filter, no MFMA)"};
+                            "valu (every wave filter, no MFMA)",
+                            "permlane (even waves permlane32_swap)",
+                            "lds (even waves LDS queue traffic)",
+                            "walk (even waves MFMA + OR + swap + LDS)"};
     int fails = 0;
-    for (int mode = 0; mode < 3; ++mode)
+    for (int mode = 0; mode < 6; ++mode)
         for (int rep = 0; rep < reps; ++rep) {
             hipMemset(dbad, 0, (size_t)n * 4);
+            hipMemset(dbo, 0, (size_t)n * 4);
+            hipMemset(dbd, 0, (size_t)n * 4);
             hipEvent_t e0, e1;
             hipEventCreate(&e0);
             hipEventCreate(&e1);
             hipEventRecord(e0);
             hipLaunchKernelGGL(k_opsel, dim3(blocks), dim3(256), 0, 0, (const float4*)dg, ngroups,
-                               dr, mode, dbad, sink);
+                               dr, mode, dbad, dbo, dbd, sink);
             hipEventRecord(e1);
             if (hipEventSynchronize(e1) != hipSuccess) {
                 printf("launch failed\n");
@@ -223,15 +304,21 @@ int main(int argc, char** argv) {
             float ms = 0.f;
             hipEventElapsedTime(&ms, e0, e1);
             hipMemcpy(hb.data(), dbad, (size_t)n * 4, hipMemcpyDeviceToHost);
-            unsigned long long tot = 0, lanes = 0;
-            for (unsigned v : hb) {
-                tot += v;
-                lanes += v != 0;
+            hipMemcpy(hbo.data(), dbo, (size_t)n * 4, hipMemcpyDeviceToHost);
+            hipMemcpy(hbd.data(), dbd, (size_t)n * 4, hipMemcpyDeviceToHost);
+            unsigned long long tot = 0, lanes = 0, to = 0, td = 0;
+            for (size_t i = 0; i < hb.size(); ++i) {
+                tot += hb[i];
+                lanes += hb[i] != 0;
+                to += hbo[i];
+                td += hbd[i];
             }
             printf("%-46s rep %d: %8.2f ms, %llu differing values in %llu lanes "
-                   "(of %llu op_sel filter groups)\n",
+                   "(of %llu op_sel filter groups); first differing group per lane vs the "
+                   "scalar fma reference: op_sel form %llu values off, duplicated-pair form %llu\n",
                    names[mode], rep, ms, tot, lanes,
-                   (unsigned long long)(mode == 2 ? n : n / 2) * ITERS);
+                   (unsigned long long)(mode == 2 ? n : n / 2) * ITERS, to, td);
+            fflush(stdout);
             fails += tot != 0;
         }
     return 0;
