@@ -673,8 +673,8 @@ __device__ __forceinline__ bool mfma_wave_ok(v3 o, bool live) {
 }
 
 #ifdef RT_PROFILE
-#define MF_ECNT , uint32_t& ecnt_, uint32_t& slots_
-#define MF_ECNT_PASS , ecnt_, slots_
+#define MF_ECNT , uint32_t& ecnt_
+#define MF_ECNT_PASS , ecnt_
 #define MF_ECNT_INC ++ecnt_
 #else
 #define MF_ECNT
@@ -699,20 +699,14 @@ __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, ui
     uint32_t ecnt[2] = {0, 0};  // (exact-test counts are not reported for this path)
 #endif
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#ifdef RT_PROFILE
-    // exact-test slots the nested loops below cost the wave: per side and
-    // entry k, the max over lanes of the entry's candidate count
-    for (uint32_t side = 0; side < 2; ++side) {
-        const uint32_t n = side ? nb : na, col = side ? j + 32u : j;
-        const uint32_t nmax = wave_max_u32(n);
-        for (uint32_t k = 0; k < nmax; ++k)
-            slots_ += wave_max_u32(k < n ? (uint32_t)__popc(q[k * 64u + col] & 15u) : 0u);
-    }
-#endif
-#ifdef RT_MF_FLAT
-    // one loop over the lane's (entry, bit) pairs of both columns: the wave
-    // pays the max over lanes of the lane's candidate count (every queued
-    // entry has a bit set, so each pass tests one candidate)
+    // One loop over the lane's (entry, bit) pairs of both columns, in any
+    // order (the LEX tie-break makes the order free): the wave pays the max
+    // over lanes of the lane's candidate count. Every queued entry has a bit
+    // set, so each pass tests one candidate. The nested form (per column, per
+    // entry, per bit) cost the wave 4.79 exact-test slots per iteration against
+    // this loop's 4.01 (RT_PROFILE, 20-frame launch) and 2.2 % per launch
+    // (profiles/r03/ab_drain/); loading the next candidate's record ahead of
+    // the current test (123 VGPRs) cost 2.2 %.
     const uint32_t total = na + nb;
     uint32_t i = 0, m = 0, base = 0;
     while (m != 0 || i < total) {
@@ -729,23 +723,6 @@ __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, ui
         exact_body<FAST, false, true>(sph[base + b], (int)(base + b), o, d, a, ya, best_t, best_i,
                                       nullptr EXACT_PASS);
     }
-#else
-    for (uint32_t side = 0; side < 2; ++side) {
-        const uint32_t n = side ? nb : na, col = side ? j + 32u : j;
-        for (uint32_t k = 0; k < n; ++k) {
-            const uint32_t e = q[k * 64u + col];
-            uint32_t m = e & 15u;
-            const uint32_t base = (e >> 4) * 4u;
-            while (m) {
-                const uint32_t b = __builtin_ctz(m);
-                m &= m - 1;
-                MF_ECNT_INC;
-                exact_body<FAST, false, true>(sph[base + b], (int)(base + b), o, d, a, ya, best_t,
-                                              best_i, nullptr EXACT_PASS);
-            }
-        }
-    }
-#endif
 }
 
 // The ORs of a tile's 16 values V = T0 - H0 per group of 4 and over the tile
@@ -898,8 +875,7 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
     // is the ray of this lane's column live, per half
     const bool col0 = (live_mask >> (lane & 31u)) & 1u, col1 = (live_mask >> (32u + (lane & 31u))) & 1u;
 #ifdef RT_PROFILE
-    uint32_t ecnt_ = 0;   // this lane's exact tests (c[13]: wave max, c[15]: lane sum)
-    uint32_t slots_ = 0;  // the wave's exact-test slots (c[14])
+    uint32_t ecnt_ = 0;  // this lane's exact tests (c[13]: wave max, c[15]: lane sum)
 #endif
     // wave-uniform upper bounds of every lane's queue length per half (SGPRs):
     // one per group some lane queued from since the last drain
@@ -974,7 +950,6 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
 #ifdef RT_PROFILE
     {
         PROF_ADD(13, wave_max_u32(ecnt_));
-        PROF_ADD(14, slots_);
         uint32_t sum0 = ecnt_;
         for (int off = 32; off > 0; off >>= 1) sum0 += __shfl_xor(sum0, off);
         PROF_ADD(15, sum0);
