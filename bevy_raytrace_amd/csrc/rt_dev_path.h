@@ -115,50 +115,56 @@ struct PixelEntry {
 // of one pixel, each sample's colour stored on its own.
 __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint32_t item,
                                            const PixelEntry* __restrict__ tab, ItemLds L) {
+    // The launch parameters are read as values (scalar loads) and the item
+    // kinds pick among values: selecting among fields of P by reference let
+    // the compiler load them through a per-lane selected address (a vector
+    // load from the kernarg segment on every item start).
+    const uint32_t npix = P.npix, main_all = P.main_all, sample_base = P.sample_base;
     uint32_t k, s0, s1;  // pixel in processing order; the (first block's) samples [s0, s1)
-    if (item < P.main_all) {
+    if (item < main_all) {
+        const uint32_t main_pix = P.main_pix, nblocks = P.nblocks, qpix = P.qpix;
+        const uint32_t block_begin = P.block_begin, spp = P.spp;
         uint32_t f, b0, b1;  // frame, the item's blocks [b0, b1) (pass-relative)
         float4 a0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (item < P.main_pix) {
+        if (item < main_pix) {
             f = fdiv(item, P.div_npix);
-            k = item - f * P.npix;
+            k = item - f * npix;
             b0 = 0;
-            b1 = min(P.nblocks, P.qpix - f * P.nblocks);
+            b1 = min(nblocks, qpix - f * nblocks);
             // a later pass over the frame's blocks (frames above the scratch
             // budget) continues the fold of the earlier passes (rt_collect_kernel
             // left it in acc_in): ((acc + b0) + b1) ..., the single-pass order
-            if (P.block_begin) {
+            if (block_begin) {
                 a0 = P.acc_in[order_to_pixel(P, k)];
                 a0.w = 1.0f;
             }
         } else {
-            const uint32_t j = item - P.main_pix;
+            const uint32_t j = item - main_pix;
             const uint32_t r = fdiv(j, P.div_npix);
-            k = j - r * P.npix;
-            const uint32_t q = P.qpix + r;
+            k = j - r * npix;
+            const uint32_t q = qpix + r;
             f = fdiv(q, P.div_nblocks);
-            b0 = q - f * P.nblocks;
+            b0 = q - f * nblocks;
             b1 = b0 + 1;
         }
-        const uint32_t base = P.sample_base + f * P.spp;
-        s0 = base + (P.block_begin + b0) * RT_SAMPLE_BLOCK;
-        const uint32_t iend = base + min(P.spp, (P.block_begin + b1) * RT_SAMPLE_BLOCK);
+        const uint32_t base = sample_base + f * spp;
+        s0 = base + (block_begin + b0) * RT_SAMPLE_BLOCK;
+        const uint32_t iend = base + min(spp, (block_begin + b1) * RT_SAMPLE_BLOCK);
         s1 = min(s0 + RT_SAMPLE_BLOCK, iend);
         L->iend = iend;
         L->acc = a0;
     } else {  // tail item: z = 4, 2 or 1 consecutive samples, each stored on its own
-        uint32_t j = item - P.main_all, z, gb, ge;
-        if (j < P.ti1) {
-            z = 4; gb = P.g0; ge = P.g1;
-        } else if (j < P.ti2) {
-            j -= P.ti1; z = 2; gb = P.g1; ge = P.g2;
-        } else {
-            j -= P.ti2; z = 1; gb = P.g2; ge = P.g_end;
-        }
+        const uint32_t ti1 = P.ti1, ti2 = P.ti2, g0 = P.g0, g1 = P.g1, g2 = P.g2,
+                       g_end = P.g_end;
+        uint32_t j = item - main_all;
+        const bool four = j < ti1, two = !four && j < ti2;
+        const uint32_t z = four ? 4u : (two ? 2u : 1u);
+        j -= four ? 0u : (two ? ti1 : ti2);
+        const uint32_t gb = four ? g0 : (two ? g1 : g2), ge = four ? g1 : (two ? g2 : g_end);
         const uint32_t g = fdiv(j, P.div_npix);
-        k = j - g * P.npix;
-        s0 = P.sample_base + gb + g * z;
-        s1 = P.sample_base + min(gb + g * z + z, ge);
+        k = j - g * npix;
+        s0 = sample_base + gb + g * z;
+        s1 = sample_base + min(gb + g * z + z, ge);
     }
     const float4 q4 = tab[k].d;
     // main item: its output slot (= queue index); tail item: RT_TAIL_ITEM | k

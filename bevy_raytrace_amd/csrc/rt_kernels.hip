@@ -123,14 +123,14 @@ __device__ __forceinline__ void render_body(
     // per-lane candidate queues: RT_CQ_CAP entries per lane for the VALU walk,
     // 2 halves x RT_MF_CAP for the matrix-core walk (RT_MFMA_FILTER); a wave
     // drains the queue of one walk before it starts another, so both share
-    // one array (the brute-force kernel's LDS: 36 KB per workgroup)
+    // one array (+ the balanced drain's 64 keys; the brute-force kernel's LDS: 38 KB per workgroup)
 #ifdef RT_MFMA_FILTER
-    constexpr uint32_t QW = CULL ? 64u * RT_CQ_CAP : 2u * RT_MF_CAP * 64u;  // words per wave
+    constexpr uint32_t QW = CULL ? 64u * RT_CQ_CAP : RT_MF_QW;  // words per wave
     static_assert(2u * RT_MF_CAP >= RT_CQ_CAP, "the shared queue holds the VALU walk's");
 #else
     constexpr uint32_t QW = 64u * RT_CQ_CAP;
 #endif
-    __shared__ uint32_t s_cq[(RT_BLOCK_THREADS / 64) * QW];
+    __shared__ __attribute__((aligned(8))) uint32_t s_cq[(RT_BLOCK_THREADS / 64) * QW];
     uint32_t* cq = s_cq + wave * QW;
 #ifdef RT_MFMA_FILTER
     uint32_t* cqm = cq;
@@ -494,7 +494,7 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_mfma_kernel(
     const float4* __restrict__ sph, uint32_t ngroups, uint32_t scene_fast,
     const float* __restrict__ rays, uint32_t n, int* __restrict__ out_i, float* __restrict__ out_t) {
     __shared__ uint32_t s_cq[RT_BLOCK_THREADS * RT_CQ_CAP];
-    __shared__ uint32_t s_cqm[(RT_BLOCK_THREADS / 64) * 2 * RT_MF_CAP * 64];
+    __shared__ __attribute__((aligned(8))) uint32_t s_cqm[(RT_BLOCK_THREADS / 64) * RT_MF_QW];
     const uint32_t wave = threadIdx.x / 64u;
     PROF_DECL
     PROF_START();
@@ -516,7 +516,7 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_mfma_kernel(
     if (mfma_wave_ok(o, live)) {
 #endif
         hi = intersect_world_mfma(mfA, nblk, mf_qs, mf_abs, sph, scene_fast, o, d, live, lm, t,
-                                  s_cqm + wave * (2u * RT_MF_CAP * 64u)
+                                  s_cqm + wave * RT_MF_QW
 #ifdef RT_PROFILE
                                   , prof_
 #endif
