@@ -671,13 +671,8 @@ typedef float f16x __attribute__((ext_vector_type(16)));
 #ifndef RT_MF_CAP
 #define RT_MF_CAP 12  // queue entries per lane and half (LDS)
 #endif
-// LDS words per wave of the matrix-core walk: the two halves' queues (then
-// 64 (t, index) keys for the balanced drain)
-#ifdef RT_BALANCED_DRAIN
-#define RT_MF_QW (2u * RT_MF_CAP * 64u + 128u)
-#else
+// LDS words per wave of the matrix-core walk: the two halves' queues
 #define RT_MF_QW (2u * RT_MF_CAP * 64u)
-#endif
 
 __device__ __forceinline__ uint32_t bperm(uint32_t src_lane, uint32_t v) {
     return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
@@ -700,10 +695,8 @@ __device__ __forceinline__ bool mfma_wave_ok(v3 o, bool live) {
 #define MF_ECNT_PASS
 #define MF_ECNT_INC
 #endif
-#ifndef RT_BALANCED_DRAIN
 template <bool FAST>
 __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, uint32_t cnt1,
-                                           uint32_t, uint32_t,
                                            const float4* __restrict__ sph, v3 o, v3 d, float a,
                                            float ya, float& best_t, int& best_i MF_ECNT) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -745,123 +738,7 @@ __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, ui
                                       nullptr EXACT_PASS);
     }
 }
-#endif
 
-#ifdef RT_BALANCED_DRAIN
-__device__ __forceinline__ float bpermf(uint32_t src_lane, float v) {
-    return __uint_as_float(bperm(src_lane, __float_as_uint(v)));
-}
-
-// The drain with the exact tests spread over the wave. The flat drain above
-// costs the wave the max over lanes of a ray's candidate count (4.02 per wave
-// iteration against a lane mean of 1.69, RT_PROFILE); here every lane takes
-// the (candidate, ray) pairs it QUEUED (its own column of both halves), the
-// pairs are compacted into one list (a ballot per pass), and the list is
-// tested 64 pairs per round, ceil(pairs / 64) rounds, with the ray's operands
-// fetched from its lane (ds_bpermute, whole wave) and the result folded into
-// the ray's (t, index) key with an LDS 64-bit atomic min -- the LEX order,
-// since t > 0 compares as its bits, so the order of the tests is free. The
-// list sits in the free rows of the emptier half's queue (rows >= that
-// half's bound ub, no entry there); pairs it has no room for are tested by
-// the lane that queued them.
-template <bool FAST>
-__device__ __forceinline__ void mfma_drain(uint32_t* cq, uint32_t cnt0, uint32_t cnt1,
-                                           uint32_t ub0, uint32_t ub1,
-                                           const float4* __restrict__ sph, v3 o, v3 d, float a,
-                                           float ya, float& best_t, int& best_i MF_ECNT) {
-    const uint32_t lane = __lane_id();
-    const uint32_t j = lane & 31u;
-    unsigned long long* keys = reinterpret_cast<unsigned long long*>(cq + 2u * RT_MF_CAP * 64u);
-#ifdef RT_PROFILE
-    uint32_t ecnt[2] = {0, 0};
-#endif
-    // the ray's running best: a miss is (VERY_FAR, 0xFFFFFFFF), above every key
-    // of a root < VERY_FAR (a root of exactly VERY_FAR never wins the scan:
-    // it ties best_t only while best_i is -1)
-    keys[lane] = ((unsigned long long)__float_as_uint(best_t) << 32) | (uint32_t)best_i;
-    // ub0 / ub1 bound the rows in use but may pass RT_MF_CAP (a group counts
-    // there even when no lane's own queue is near full, block() flushes only
-    // on the lanes' counts), so clamp
-    const bool in0 = ub0 < ub1;
-    const uint32_t ub = min(in0 ? ub0 : ub1, (uint32_t)RT_MF_CAP);
-    uint32_t* list = cq + (in0 ? 0u : RT_MF_CAP * 64u) + ub * 64u;
-    const uint32_t cap = (RT_MF_CAP - ub) * 64u;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint32_t total = cnt0 + cnt1;
-    uint32_t i = 0, m = 0, base = 0, rl = 0;
-    auto next = [&]() {  // the lane's next own entry once the current one is used up
-        if (m == 0 && i < total) {
-            const bool s1 = i >= cnt0;
-            const uint32_t e = cq[(s1 ? (i - cnt0) + RT_MF_CAP : i) * 64u + lane];
-            m = e & 15u;
-            base = (e >> 4) * 4u;
-            rl = s1 ? j + 32u : j;
-            ++i;
-        }
-    };
-    uint32_t np = 0;  // pairs in the list (wave-uniform)
-    for (;;) {
-        next();
-        const uint64_t has = rt_ballot(m != 0);
-        const uint32_t n = (uint32_t)__builtin_popcountll(has);
-        if (n == 0 || np + n > cap) break;
-        if (m != 0) {
-            const uint32_t b = __builtin_ctz(m);
-            m &= m - 1u;
-            list[np + lanemask_lt_count(has)] = ((base + b) << 6) | rl;
-        }
-        np += n;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // one pair per lane: w = sphere << 6 | ray lane; the bpermutes run with
-    // the whole wave (a disabled source lane would read as 0)
-    auto test = [&](uint32_t w, bool on) {
-        const uint32_t src = w & 63u;
-        const v3 ro = mk(bpermf(src, o.x), bpermf(src, o.y), bpermf(src, o.z));
-        const v3 rd = mk(bpermf(src, d.x), bpermf(src, d.y), bpermf(src, d.z));
-        const float ra = bpermf(src, a), rya = bpermf(src, ya);
-        if (on) {
-            const uint32_t k = w >> 6;
-            MF_ECNT_INC;
-            exact_core<FAST>(sph[k], ro, rd, ra, rya, [&](float root) {
-                if (root < VERY_FAR)
-                    __hip_atomic_fetch_min(
-                        keys + src, ((unsigned long long)__float_as_uint(root) << 32) | k,
-                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-            } EXACT_PASS);
-        }
-    };
-    // 64 list pairs per round, then the pairs the list had no room for (each
-    // lane its own); one copy of the test
-    uint32_t p0 = 0;
-    for (;;) {
-        uint32_t w = lane;
-        bool on;
-        if (p0 < np) {
-            on = p0 + lane < np;
-            if (on) w = list[p0 + lane];
-            p0 += 64u;
-        } else {
-            next();
-            on = m != 0;
-            if (rt_ballot(on) == 0) break;
-            if (on) {
-                const uint32_t b = __builtin_ctz(m);
-                m &= m - 1u;
-                w = ((base + b) << 6) | rl;
-            }
-        }
-        test(w, on);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const unsigned long long key = keys[lane];
-    best_t = __uint_as_float((uint32_t)(key >> 32));
-    best_i = (int)(uint32_t)key;
-}
-#endif  // RT_BALANCED_DRAIN
 
 // The ORs of a tile's 16 values V = T0 - H0 per group of 4 and over the tile
 // (10 VALU: v_or3 / v_or). A group or tile with a candidate (V < 0) has the
@@ -1027,9 +904,9 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
         if (max(ub0, ub1) + 4u > RT_MF_CAP && rt_ballot(max(cnt0, cnt1) + 4u > RT_MF_CAP) != 0) {
             PROF_ADD(11, 1);  // queue flushes
             if (fast)
-                mfma_drain<true>(cq, cnt0, cnt1, ub0, ub1, sph, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
+                mfma_drain<true>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
             else
-                mfma_drain<false>(cq, cnt0, cnt1, ub0, ub1, sph, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
+                mfma_drain<false>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
             cnt0 = cnt1 = 0;
             ub0 = ub1 = 0;
         }
@@ -1081,9 +958,9 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
     if (b < nblk) block(b, a0, a1);
     PROF_MARK(1);
     if (fast)
-        mfma_drain<true>(cq, cnt0, cnt1, ub0, ub1, sph, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
+        mfma_drain<true>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
     else
-        mfma_drain<false>(cq, cnt0, cnt1, ub0, ub1, sph, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
+        mfma_drain<false>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
     PROF_MARK(2);
 #ifdef RT_PROFILE
     {

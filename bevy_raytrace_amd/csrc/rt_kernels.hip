@@ -123,7 +123,7 @@ __device__ __forceinline__ void render_body(
     // per-lane candidate queues: RT_CQ_CAP entries per lane for the VALU walk,
     // 2 halves x RT_MF_CAP for the matrix-core walk (RT_MFMA_FILTER); a wave
     // drains the queue of one walk before it starts another, so both share
-    // one array (+ the balanced drain's 64 keys; the brute-force kernel's LDS: 38 KB per workgroup)
+    // one array (the brute-force kernel's LDS: 36 KB per workgroup)
 #ifdef RT_MFMA_FILTER
     constexpr uint32_t QW = CULL ? 64u * RT_CQ_CAP : RT_MF_QW;  // words per wave
     static_assert(2u * RT_MF_CAP >= RT_CQ_CAP, "the shared queue holds the VALU walk's");

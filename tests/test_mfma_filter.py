@@ -252,37 +252,3 @@ def test_scale_is_the_whole_scenes():
     assert scene_rows("rtiow")[1] == qscale(SCENES["rtiow"]())
     full = SCENES["spheres10k"]()
     assert scene_rows("spheres10k")[1] == qscale(full)
-
-
-def test_drain_key_order_is_the_scan():
-    """The balanced drain (rt_dev_intersect.h, RT_BALANCED_DRAIN) folds each
-    hit into its ray's key (t bits << 32 | index) with a 64-bit atomic min,
-    roots of exactly VERY_FAR (and NaN / misses) never folded, a ray's key
-    starting from its running best (VERY_FAR, 0xFFFFFFFF when it has none).
-    Any order of the folds must give the reference's sequential strict-<
-    scan over the list (intersect.wgsl:137), ties in t included."""
-    rng = np.random.default_rng(7)
-    tvals = np.array([EPSILON, F(0.5), F(1.0), F(1.0) + np.spacing(F(1.0)), F(7.25),
-                      np.nextafter(VERY_FAR, F(0)), VERY_FAR, F(np.nan)], dtype=F)
-    for _ in range(4000):
-        n = int(rng.integers(0, 10))
-        idx = np.sort(rng.choice(1000, size=n, replace=False))
-        t = tvals[rng.integers(0, len(tvals), size=n)]
-        # the sequential scan in list order (the reference's answer)
-        best_t, best_i = VERY_FAR, -1
-        for ti, ii in zip(t, idx):
-            if ti < best_t:
-                best_t, best_i = ti, int(ii)
-        # a flush drain: a prefix of the list already folded into (bt, bi)
-        cut = int(rng.integers(0, n + 1))
-        bt, bi = VERY_FAR, -1
-        for ti, ii in zip(t[:cut], idx[:cut]):
-            if ti < bt or (ti == bt and ii < bi):
-                bt, bi = ti, int(ii)
-        key = (int(np.asarray(bt, F).view(np.uint32)) << 32) | (bi & 0xFFFFFFFF)
-        for p in rng.permutation(np.arange(cut, n)):
-            if t[p] < VERY_FAR:
-                key = min(key, (int(np.asarray(t[p], F).view(np.uint32)) << 32) | int(idx[p]))
-        got_t = np.array([key >> 32], dtype=np.uint32).view(F)[0]
-        got_i = np.array([key & 0xFFFFFFFF], dtype=np.uint32).view(np.int32)[0]
-        assert (got_t, got_i) == (best_t, best_i)
