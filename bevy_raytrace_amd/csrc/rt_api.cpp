@@ -70,6 +70,12 @@ struct Tuning {
     bool tail_split = true;       // single-sample tail items at the end of a launch
     double tail[3] = {0.0, 0.0, 6.0};  // tail regions (4-, 2-, 1-sample items) x D x lanes
     double block_region = 96.0;   // single-block items before the tail, x D x lanes samples
+    // KParams::item_order: pixel-major block / tail items (bit 0) and pixel
+    // items (bit 1): a wave's lanes then share pixels, so its primary rays
+    // (and first-bounce origins) coincide -- warm 20-frame launches, one box
+    // (profiles/r03/item_order/): full frame 243.7 -> 240.2 ms, N=8 shard
+    // 34.9 -> 33.5 ms; 1 alone 242.6 / 33.5, 2 alone 241.0 / 35.4
+    uint32_t item_order = 3;
     bool prefetch = true;         // waves prefetch their next work chunk
     uint32_t prio_mode = 1;       // s_setprio rotation: 0 off, 1 by iteration, 3 by wall time
     uint32_t prio_shift = 14;     // mode 3 step: 2^prio_shift ticks of 10 ns
@@ -213,6 +219,9 @@ static bool tune_set(Tuning& t, const char* name, const char* v) {
         t.split_all = x != 0;
     } else if (!strcmp(name, "tail_split")) {
         t.tail_split = x != 0;
+    } else if (!strcmp(name, "item_order")) {
+        if (x < 0 || x > 3) return false;
+        t.item_order = (uint32_t)x;
     } else if (!strcmp(name, "block_region")) {
         if (x < 0) return false;
         t.block_region = x;
@@ -1149,6 +1158,10 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         K_.ti1 = (uint32_t)((g1 - g0 + 3) / 4 * npix);
         K_.ti2 = K_.ti1 + (uint32_t)((g2 - g1 + 1) / 2 * npix);
         K_.tail_items = K_.ti2 + (uint32_t)((g_end - g2) * npix);
+        K_.item_order = tn.item_order;
+        K_.div_nreg = make_fastdiv(K_.qmain > K_.qpix ? K_.qmain - K_.qpix : 1u);
+        K_.div_nfpix = make_fastdiv(npix && K_.main_pix ? K_.main_pix / npix : 1u);
+        K_.div_ng1 = make_fastdiv(g_end > g2 ? (uint32_t)(g_end - g2) : 1u);
         const uint64_t items = (uint64_t)K_.main_all + K_.tail_items;
         const uint64_t chunks = (items + RT_WAVE_CHUNK - 1) / RT_WAVE_CHUNK;
         const uint64_t need_blocks = (chunks + (RT_BLOCK_THREADS / 64) - 1) / (RT_BLOCK_THREADS / 64);

@@ -121,14 +121,21 @@ __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint
     // load from the kernarg segment on every item start).
     const uint32_t npix = P.npix, main_all = P.main_all, sample_base = P.sample_base;
     uint32_t k, s0, s1;  // pixel in processing order; the (first block's) samples [s0, s1)
+    uint32_t slot = item;  // a main item's output slot
     if (item < main_all) {
         const uint32_t main_pix = P.main_pix, nblocks = P.nblocks, qpix = P.qpix;
         const uint32_t block_begin = P.block_begin, spp = P.spp;
         uint32_t f, b0, b1;  // frame, the item's blocks [b0, b1) (pass-relative)
         float4 a0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (item < main_pix) {
-            f = fdiv(item, P.div_npix);
-            k = item - f * npix;
+            if (P.item_order & 2u) {  // pixel-major: one pixel's frames back to back
+                k = fdiv(item, P.div_nfpix);
+                f = item - k * (main_pix / npix);
+                slot = f * npix + k;
+            } else {
+                f = fdiv(item, P.div_npix);
+                k = item - f * npix;
+            }
             b0 = 0;
             b1 = min(nblocks, qpix - f * nblocks);
             // a later pass over the frame's blocks (frames above the scratch
@@ -140,8 +147,15 @@ __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint
             }
         } else {
             const uint32_t j = item - main_pix;
-            const uint32_t r = fdiv(j, P.div_npix);
-            k = j - r * npix;
+            uint32_t r;  // the pair (relative to qpix); slot main_pix + r * npix + k
+            if (P.item_order & 1u) {  // pixel-major: one pixel's pairs back to back
+                k = fdiv(j, P.div_nreg);
+                r = j - k * (P.qmain - qpix);
+                slot = main_pix + r * npix + k;
+            } else {
+                r = fdiv(j, P.div_npix);
+                k = j - r * npix;
+            }
             const uint32_t q = qpix + r;
             f = fdiv(q, P.div_nblocks);
             b0 = q - f * nblocks;
@@ -161,14 +175,20 @@ __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint
         const uint32_t z = four ? 4u : (two ? 2u : 1u);
         j -= four ? 0u : (two ? ti1 : ti2);
         const uint32_t gb = four ? g0 : (two ? g1 : g2), ge = four ? g1 : (two ? g2 : g_end);
-        const uint32_t g = fdiv(j, P.div_npix);
-        k = j - g * npix;
+        uint32_t g;
+        if ((P.item_order & 1u) && !four && !two) {  // pixel-major single samples
+            k = fdiv(j, P.div_ng1);
+            g = j - k * (g_end - g2);
+        } else {
+            g = fdiv(j, P.div_npix);
+            k = j - g * npix;
+        }
         s0 = sample_base + gb + g * z;
         s1 = sample_base + min(gb + g * z + z, ge);
     }
     const float4 q4 = tab[k].d;
     // main item: its output slot (= queue index); tail item: RT_TAIL_ITEM | k
-    st.item = item < P.main_all ? item : (RT_TAIL_ITEM | k);
+    st.item = item < P.main_all ? slot : (RT_TAIL_ITEM | k);
     st.pix = __float_as_uint(q4.w);
     st.s = s0;
     st.s_end = s1;

@@ -102,6 +102,14 @@ struct KParams {
     const uint4* mfA;
     uint32_t mf_nblk;
     float mf_qs, mf_abs;  // 2^sq (quadratic features' ray-side scale), threshold margin
+    // queue order (knob item_order, bits): bit 0 the block items and the
+    // single-sample tail items, bit 1 the pixel items, pixel-major
+    // (consecutive items: one pixel's pairs / samples / frames) instead of
+    // pair- / sample- / frame-major (consecutive items: neighbouring pixels)
+    uint32_t item_order;
+    FastDiv div_nfpix; // by main_pix / npix (frames with pixel items)
+    FastDiv div_nreg;  // by qmain - qpix (pairs of the block-item region)
+    FastDiv div_ng1;   // by g_end - g2 (samples of the single-sample tail region)
 };
 
 // Row block b of the image -> owning shard (rt_params: serpentine deal).

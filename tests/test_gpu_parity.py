@@ -243,6 +243,32 @@ def test_tail_split_identical(renderer, S):
     assert st_on["segments"] == segs
 
 
+@pytest.mark.parametrize("S,region", [(21, "1000000"), (64, "1000000"), (64, "96"), (64, "0")])
+def test_item_order_identical(renderer, S, region):
+    """Pixel-major block and single-sample tail items (knob item_order: one
+    pixel's pairs / samples back to back in the queue) give the frames of the
+    pair-major order -- only the work order changes, each item keeps its
+    slot. Three frames in one launch, so the block region spans frames."""
+    import torch
+    sp, mt = arrays(scene.rtiow_final_scene())
+    cam = default_camera_block()
+    W, H, F = 72, 40, 3
+    renderer.set_scene(sp, mt)
+    renderer.tune(block_region=region)
+    outs = []
+    for order in ("0", "1", "2", "3"):
+        renderer.tune(item_order=order)
+        buf = torch.empty((F, H, W, 4), dtype=torch.float32, device="cuda")
+        renderer.render_frames_device(cam, F, buf.data_ptr(), W, H, S, 10, flags=NO_REUSE)
+        st = renderer.wait()
+        outs.append((buf.cpu().numpy(), st["segments"]))
+    for o in outs[1:]:
+        check_exact(o[0], outs[0][0])
+        assert o[1] == outs[0][1]
+    ref, segs = O.render(cam, sp, mt, W, H, S, 10, frame0=S)  # launch frame 1 = samples S..2S
+    check_exact(outs[1][0][1], ref)
+
+
 @pytest.mark.parametrize("K,B", [(2, 8), (3, 5), (8, 1)])
 def test_shards_and_device_assembly(renderer, K, B):
     import torch
