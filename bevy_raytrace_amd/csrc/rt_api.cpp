@@ -68,7 +68,7 @@ struct Tuning {
     size_t scratch_bytes = (size_t)16 << 30;  // block sums per launch (of 288 GB HBM)
     bool split_all = false;       // without primary reuse, every block as single samples
     bool tail_split = true;       // single-sample tail items at the end of a launch
-    double tail[3] = {0.0, 0.0, 6.0};  // tail regions (4-, 2-, 1-sample items) x D x lanes
+    double tail[3] = {0.0, 1.0, 1.0};  // tail regions (4-, 2-, 1-sample items) x D x lanes
     double block_region = 96.0;   // single-block items before the tail, x D x lanes samples
     // KParams::item_order: pixel-major block / tail items (bit 0) and pixel
     // items (bit 1): a wave's lanes then share pixels, so its primary rays
@@ -933,10 +933,13 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     const size_t per_block = (size_t)npix * sizeof(float4);  // one slot per pixel
     // Tail: per lane ~a1*D single samples, and before them optionally a2*D
     // samples in 2-sample items and a4*D in 4-sample items (knob tail="a4,a2,a1";
-    // default 0,0,6 = single samples only, the measured best on the RTIOW
-    // frames and N=8 shards with the matrix-core kernel; 0,0,12 before it): a block item (<= 8*D iterations) taken before the tail has
-    // finished when the queue runs dry, and an item taken in the tail leaves
-    // at most one short path per lane to drain. In samples per pixel:
+    // default 0,1,1 since the pixel-major item order, the measured best on
+    // the N=8 shards -- 31.4 vs 33.0 ms per 20-frame launch for 0,0,6 -- at
+    // the same full frame, profiles/r03/item_order/sweep_tail*.log; 0,0,6
+    // with the pair-major order, 0,0,12 before the matrix-core kernel): a
+    // block item (<= 8*D iterations) taken before the tail has finished when
+    // the queue runs dry, and an item taken in the tail leaves at most one
+    // short path per lane to drain. In samples per pixel:
     const Tuning& tn = ctx->tune;
     const int bpc = (p.flags & RT_FLAG_CULL) ? ctx->blocks_per_cu_c : ctx->blocks_per_cu;
     const uint64_t lanes = (uint64_t)ctx->cu_count * bpc * RT_BLOCK_THREADS;
@@ -1161,6 +1164,8 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         K_.item_order = tn.item_order;
         K_.div_nreg = make_fastdiv(K_.qmain > K_.qpix ? K_.qmain - K_.qpix : 1u);
         K_.div_nfpix = make_fastdiv(npix && K_.main_pix ? K_.main_pix / npix : 1u);
+        K_.div_ng4 = make_fastdiv(g1 > g0 ? (uint32_t)((g1 - g0 + 3) / 4) : 1u);
+        K_.div_ng2 = make_fastdiv(g2 > g1 ? (uint32_t)((g2 - g1 + 1) / 2) : 1u);
         K_.div_ng1 = make_fastdiv(g_end > g2 ? (uint32_t)(g_end - g2) : 1u);
         const uint64_t items = (uint64_t)K_.main_all + K_.tail_items;
         const uint64_t chunks = (items + RT_WAVE_CHUNK - 1) / RT_WAVE_CHUNK;

@@ -175,10 +175,11 @@ __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint
         const uint32_t z = four ? 4u : (two ? 2u : 1u);
         j -= four ? 0u : (two ? ti1 : ti2);
         const uint32_t gb = four ? g0 : (two ? g1 : g2), ge = four ? g1 : (two ? g2 : g_end);
-        uint32_t g;
-        if ((P.item_order & 1u) && !four && !two) {  // pixel-major single samples
-            k = fdiv(j, P.div_ng1);
-            g = j - k * (g_end - g2);
+        uint32_t g;  // the item's sample group within its region
+        if (P.item_order & 1u) {  // pixel-major: one pixel's groups back to back
+            const FastDiv dz = four ? P.div_ng4 : (two ? P.div_ng2 : P.div_ng1);
+            k = fdiv(j, dz);
+            g = j - k * dz.d;
         } else {
             g = fdiv(j, P.div_npix);
             k = j - g * npix;

@@ -109,7 +109,9 @@ struct KParams {
     uint32_t item_order;
     FastDiv div_nfpix; // by main_pix / npix (frames with pixel items)
     FastDiv div_nreg;  // by qmain - qpix (pairs of the block-item region)
-    FastDiv div_ng1;   // by g_end - g2 (samples of the single-sample tail region)
+    // by the sample groups per pixel of the tail regions: (g1 - g0 + 3) / 4,
+    // (g2 - g1 + 1) / 2, g_end - g2 (4-, 2-, 1-sample items)
+    FastDiv div_ng4, div_ng2, div_ng1;
 };
 
 // Row block b of the image -> owning shard (rt_params: serpentine deal).

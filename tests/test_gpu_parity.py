@@ -243,18 +243,20 @@ def test_tail_split_identical(renderer, S):
     assert st_on["segments"] == segs
 
 
-@pytest.mark.parametrize("S,region", [(21, "1000000"), (64, "1000000"), (64, "96"), (64, "0")])
-def test_item_order_identical(renderer, S, region):
-    """Pixel-major block and single-sample tail items (knob item_order: one
-    pixel's pairs / samples back to back in the queue) give the frames of the
-    pair-major order -- only the work order changes, each item keeps its
-    slot. Three frames in one launch, so the block region spans frames."""
+@pytest.mark.parametrize("S,region,tail", [(21, "1000000", "0,0,6"), (64, "1000000", "0,1,1"),
+                                           (64, "96", "0.01,0.01,0.01"), (64, "0", "0,1,1")])
+def test_item_order_identical(renderer, S, region, tail):
+    """Pixel-major items (knob item_order bits: one pixel's pairs / tail
+    sample groups, and its frames, back to back in the queue) give the frames
+    of the pair- / sample- / frame-major order -- only the work order changes,
+    each item keeps its slot. Three frames in one launch, so the regions span
+    frames; the 0.01 tail holds 4-, 2- and 1-sample items."""
     import torch
     sp, mt = arrays(scene.rtiow_final_scene())
     cam = default_camera_block()
     W, H, F = 72, 40, 3
     renderer.set_scene(sp, mt)
-    renderer.tune(block_region=region)
+    renderer.tune(block_region=region, tail=tail)
     outs = []
     for order in ("0", "1", "2", "3"):
         renderer.tune(item_order=order)
