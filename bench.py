@@ -69,6 +69,12 @@ def parse():
                          "gather, for rehearsing N>1 on a one-GPU box")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank on cuda:0 (rehearsal with --dist-backend gloo)")
+    ap.add_argument("--gather", default="auto", choices=["auto", "ipc", "rccl"],
+                    help="N>1: ipc = rank 0's image mapped into every rank (HIP IPC), each "
+                         "rank writing its rows straight into it (RT_FLAG_IMAGE_OUT: no "
+                         "gather, no re-assembly); rccl = one gather of the shard slabs to "
+                         "rank 0 and a device re-assembly; auto = ipc, else rccl if "
+                         "mapping fails on any rank")
     ap.add_argument("--check", action="store_true",
                     help="add a checksum of the assembled frames to the JSON line")
     ap.add_argument("--force-dist", action="store_true",
@@ -363,21 +369,58 @@ def main():
     FPL = max(1, args.frames_per_launch)
     image = (torch.empty((FPL, H, W, 4), dtype=torch.float32, device="cuda")
              if rank == 0 else None)
+    # N>1: rank 0's image mapped into every rank, unless the
+    # mapping fails on some rank (then every rank takes the gather path)
+    use_ipc, img_ptr, ipc_map = False, None, None
+    if dist_on and args.gather in ("auto", "ipc"):
+        from bevy_raytrace_amd import distributed as rdist
+        blob = None
+        if rank == 0:
+            try:
+                blob = rdist.ipc_export(image.data_ptr())
+            except Exception as e:  # noqa: BLE001 -- reported, then the gather path
+                print(f"bench.py: IPC export failed: {e}", file=sys.stderr)
+        objs = [blob]
+        dist.broadcast_object_list(objs, src=0)
+        ok = objs[0] is not None
+        if ok and rank == 0:
+            img_ptr = image.data_ptr()
+        elif ok:
+            try:
+                ipc_map, img_ptr = rdist.ipc_import(objs[0])
+            except Exception as e:  # noqa: BLE001
+                print(f"bench.py: IPC import failed on rank {rank}: {e}", file=sys.stderr)
+                ok = False
+        flag = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        use_ipc = float(flag.item()) == 1.0
+        if not use_ipc:
+            if ipc_map is not None:
+                rdist.ipc_close(ipc_map)
+                ipc_map = None
+            if args.gather == "ipc":
+                raise RuntimeError("--gather ipc: mapping rank 0's image failed")
     # N=1: the single shard is the image; render straight into it.
-    shard = image if not dist_on else torch.empty((FPL, max_rows, W, 4), dtype=torch.float32,
-                                                  device="cuda")
+    gather_path = dist_on and not use_ipc
+    shard = image if not dist_on else (torch.empty((FPL, max_rows, W, 4), dtype=torch.float32,
+                                                   device="cuda") if gather_path else None)
     gathered = (torch.empty((world, FPL, max_rows, W, 4), dtype=torch.float32, device="cuda")
-                if (rank == 0 and dist_on) else None)
+                if (rank == 0 and gather_path) else None)
     # The library writes frame i of a launch at i * rows * W (this rank's own
     # row count); the gather needs equal slabs of max_rows. With uneven shards
     # (H not a multiple of B*world) a shorter rank renders into its own buffer
     # and copies each frame into the padded slab.
     packed = (torch.empty((FPL, len(rows), W, 4), dtype=torch.float32, device="cuda")
-              if dist_on and len(rows) != max_rows else None)
+              if gather_path and len(rows) != max_rows else None)
 
     def launch(first, nf, flags):
         """Enqueue frames [first, first + nf): render, then (N > 1) one RCCL
-        gather of the nf shard slabs to rank 0 and the device re-assembly."""
+        gather of the nf shard slabs to rank 0 and the device re-assembly --
+        or, with rank 0's image mapped, render the rank's rows straight into it."""
+        if use_ipc:
+            r.render_frames_device(cam, nf, img_ptr, W, H, S, D, first * S, B, world, rank,
+                                   flags | abi.RT_FLAG_IMAGE_OUT, stream=stream.cuda_stream)
+            return
         dst = shard if packed is None else packed
         r.render_frames_device(cam, nf, dst.data_ptr(), W, H, S, D, first * S, B, world, rank,
                                flags, stream=stream.cuda_stream)
@@ -496,7 +539,10 @@ def main():
                           "identical frames and segment counts, less filter work (no roofline: "
                           "the brute-force 18*N flops per segment are no longer all executed)"}
 
-    if rank != 0:
+    if rank != 0:  # (all of its writes into rank 0's image completed in timed())
+        if ipc_map is not None:
+            from bevy_raytrace_amd import distributed as rdist
+            rdist.ipc_close(ipc_map)
         if dist_on:
             dist.destroy_process_group()
         return
@@ -552,7 +598,9 @@ def main():
                    "width": W, "height": H, "spp": S, "max_depth": D, "spheres": nsph,
                    "frames_per_launch": FPL, "launch_sizes": sizes,
                    "parallelism": (f"row-tiled x{world} (blocks of {B} rows) + "
-                                   + ("RCCL gather" if args.dist_backend == "nccl"
+                                   + ("rows written into rank 0's image (HIP IPC, xGMI)"
+                                      if use_ipc else
+                                      "RCCL gather" if args.dist_backend == "nccl"
                                       else "host-staged gloo gather (rehearsal)"))
                    if dist_on else "single GPU"},
         "roofline": roofline,

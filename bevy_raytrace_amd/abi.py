@@ -38,6 +38,7 @@ RT_FLAG_JITTER = 0x2             # opt-in sub-pixel jitter (include/rt_hip.h)
 RT_FLAG_THIN_LENS = 0x4          # opt-in thin-lens sample (generate.wgsl:85-107)
 RT_FLAG_CULL = 0x8               # culled list: group bounds, identical hits (include/rt_hip.h)
 RT_FLAG_VALU_FILTER = 0x10       # packed-fp32 VALU filter instead of the matrix-core one (identical hits)
+RT_FLAG_IMAGE_OUT = 0x20         # device output in the image layout (owned rows at their image rows)
 RT_MAX_PENDING = 2          # frames in flight per ctx (rt_render_device / rt_render_async)
 
 SPHERE_DTYPE = np.dtype(

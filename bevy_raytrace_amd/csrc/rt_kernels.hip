@@ -137,6 +137,10 @@ __device__ __forceinline__ void render_body(
 #endif
     __shared__ LaneLds s_lane[RT_BLOCK_THREADS];  // per-lane item state (rt_dev_path.h)
     const ItemLds lds = s_lane + wave * 64u + lane;
+    // fused collect: per wave a list of finished (frame, pixel) counters,
+    // finalized 64 at a time (one per lane)
+    __shared__ uint32_t s_fin[(RT_BLOCK_THREADS / 64) * 128];
+    uint32_t* const fin_list = s_fin + wave * 128u;
 #ifdef RT_SPHERES_LDS
     // Experiment variant: the filter reads the sphere groups from LDS (staged
     // once per workgroup) instead of the scalar cache.
@@ -185,6 +189,43 @@ __device__ __forceinline__ void render_body(
     const uint32_t wave_slot = __builtin_amdgcn_s_getreg((3 << 11) | 4);
     uint32_t pref = 0;            // lane 0: base of the prefetched chunk
     uint32_t pref_chunk = 0;      // its size (0 = none in flight)
+    // Fused collect (P.fin_cnt). An item's completion is counted one
+    // iteration late: lanes whose item ended (fin_pend) increment its
+    // (frame, pixel) counter after the next walk, when its write-through slot
+    // stores have long drained (the s_waitcnt vmcnt(0) there is free), and
+    // check the returned count after that iteration's shading (fin_chk); the
+    // lane that completes the count queues the (frame, pixel) in the wave's
+    // list, and the wave finalizes 64 at a time.
+    uint64_t fin_pend = 0, fin_chk = 0;  // wave-uniform lane masks
+    uint32_t fin_fk = 0, fin_res = 0;    // the lane's counter index, returned count
+    uint32_t fin_n = 0;                  // entries in the wave's list
+    auto fin_push = [&](bool done) {
+        const uint64_t m = rt_ballot(done);
+        if (m) {
+            if (done) fin_list[fin_n + lanemask_lt_count(m)] = fin_fk;
+            fin_n += (uint32_t)__popcll(m);
+        }
+    };
+    auto fin_task = [&](const KParams& Q, uint32_t cnt) {  // the list's top cnt entries
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane < cnt) fin_pixel(Q, block_sums, fin_list[fin_n - cnt + lane]);
+        fin_n -= cnt;
+    };
+    auto fin_count = [&](const KParams& Q) {  // the pending lanes' counter increments
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if ((fin_pend >> lane) & 1u)
+            fin_res = __hip_atomic_fetch_add(Q.fin_cnt + fin_fk, 1u, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        fin_chk = fin_pend;
+        fin_pend = 0;
+    };
+    auto fin_check = [&](const KParams& Q) {
+        const bool done = ((fin_chk >> lane) & 1u) &&
+                          fin_res + 1u == fin_units(Q, fdiv(fin_fk, Q.div_npix));
+        fin_chk = 0;
+        fin_push(done);
+    };
 
     for (;;) {
 #ifndef RT_PARAMS_HOLD
@@ -305,6 +346,7 @@ __device__ __forceinline__ void render_body(
 #endif
                                        P.bnd, P.perm, P.nclusters, P.cull_supers != 0);
         }
+        if (fin_pend) fin_count(P);
         traced = __builtin_amdgcn_readfirstlane(traced + (uint32_t)__popcll(live));
         if (use_cache && has_item && st.bounce == 0)  // the item's first sample: its primary hit
             lds->cache = make_float2(__int_as_float(hi), t);
@@ -326,9 +368,9 @@ __device__ __forceinline__ void render_body(
                     // a tail item stores every sample's colour for the collect
                     if (st.item & RT_TAIL_ITEM) {
                         const v3 c = add(mk(0.0f, 0.0f, 0.0f), st.color);
-                        block_sums[P.main_all +
-                                   (st.s - P.sample_base - P.g0) * P.npix + (st.item & ~RT_TAIL_ITEM)] =
-                            make_float4(c.x, c.y, c.z, 0.0f);
+                        put_slot(block_sums + P.main_all +
+                                     (st.s - P.sample_base - P.g0) * P.npix + (st.item & ~RT_TAIL_ITEM),
+                                 c, P.fin_cnt != nullptr);
                     } else {
                         st.bsum = add(st.bsum, st.color);
                     }
@@ -348,7 +390,7 @@ __device__ __forceinline__ void render_body(
                             st.s_end = min(st.s + RT_SAMPLE_BLOCK, iend);
                             next = true;
                         } else {
-                            block_sums[st.item] = make_float4(acc.x, acc.y, acc.z, 0.0f);
+                            put_slot(block_sums + st.item, acc, P.fin_cnt != nullptr);
                         }
                     }
                     if (next) {
@@ -365,7 +407,24 @@ __device__ __forceinline__ void render_body(
                 }
             }
         }
+        if (fin_chk) fin_check(P);
+        if (P.fin_cnt) {
+            const uint64_t ended = live & ~rt_ballot(has_item);
+            if ((ended >> lane) & 1u) fin_fk = lds->fk;
+            fin_pend = ended;
+            if (fin_n >= 64u) fin_task(P, 64u);
+        }
         PROF_MARK(3);
+    }
+    {  // fused collect: the last items' counts, then the rest of the list
+#ifndef RT_PARAMS_HOLD
+        const KParams& P = fresh_params();
+#endif
+        if (fin_pend) {
+            fin_count(P);
+            fin_check(P);
+        }
+        while (fin_n) fin_task(P, min(fin_n, 64u));
     }
 
 #ifdef RT_PROFILE
@@ -560,7 +619,6 @@ __global__ void rt_collect_kernel(KParams P, const float4* __restrict__ block_su
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= P.npix) return;
     const uint32_t f = blockIdx.y;
-    out += (size_t)f * P.npix;
     const uint32_t p = order_to_pixel(P, k);
     float ax = 0.0f, ay = 0.0f, az = 0.0f;
     bool have = !first_pass;
@@ -568,47 +626,18 @@ __global__ void rt_collect_kernel(KParams P, const float4* __restrict__ block_su
         const float4 v = acc[p];
         ax = v.x; ay = v.y; az = v.z;
     }
-    const uint32_t q0 = f * P.nblocks;
-    auto blocks_below = [&](uint32_t q) { return q > q0 ? min(P.nblocks, q - q0) : 0u; };
-    const uint32_t bp = blocks_below(P.qpix), bm = blocks_below(P.qmain);
-    auto fold = [&](float vx, float vy, float vz) {
-        if (have) {
-            ax = ax + vx; ay = ay + vy; az = az + vz;
-        } else {
-            ax = vx; ay = vy; az = vz;
-            have = true;
-        }
-    };
-    if (bp) {  // the lane's fold already continued acc (start_item, later passes)
-        const float4 v = block_sums[(size_t)f * P.npix + k];
-        ax = v.x; ay = v.y; az = v.z;
-        have = true;
-    }
-    for (uint32_t b = bp; b < bm; ++b) {  // block items
-        const float4 v = block_sums[(size_t)P.main_pix + (size_t)(q0 + b - P.qpix) * P.npix + k];
-        fold(v.x, v.y, v.z);
-    }
-    for (uint32_t b = bm; b < P.nblocks; ++b) {  // tail blocks: their samples' colours
-        const uint32_t sl = (P.block_begin + b) * RT_SAMPLE_BLOCK;
-        const uint32_t g_end = f * P.spp + min(P.spp, sl + RT_SAMPLE_BLOCK);
-        float vx = 0.0f, vy = 0.0f, vz = 0.0f;
-        for (uint32_t g = f * P.spp + sl; g < g_end; ++g) {
-            const float4 c = block_sums[(size_t)P.main_all + (size_t)(g - P.g0) * P.npix + k];
-            vx = vx + c.x; vy = vy + c.y; vz = vz + c.z;
-        }
-        fold(vx, vy, vz);
-    }
+    fold_frame(P, f, k, have, ax, ay, az, [&](size_t slot) { return block_sums[slot]; });
     if (!last_pass) {
         acc[p] = make_float4(ax, ay, az, 0.0f);
     } else if (prog_mode == 0) {
-        out[p] = make_float4(ax / spp, ay / spp, az / spp, 1.0f);
+        *out_pixel(P, out, f, p) = make_float4(ax / spp, ay / spp, az / spp, 1.0f);
     } else {
         if (prog_mode == 2) {
             const float4 v = prog[p];
             ax = v.x + ax; ay = v.y + ay; az = v.z + az;
         }
         prog[p] = make_float4(ax, ay, az, 0.0f);
-        out[p] = make_float4(ax / prog_total, ay / prog_total, az / prog_total, 1.0f);
+        out[(size_t)f * P.npix + p] = make_float4(ax / prog_total, ay / prog_total, az / prog_total, 1.0f);
     }
 }
 

@@ -46,6 +46,8 @@ pub const RT_FLAG_CULL: u32 = 0x8;
 /// The packed-fp32 VALU filter instead of the matrix-core one: identical hits
 /// (rt_hip.h; A/B and cross-checks).
 pub const RT_FLAG_VALU_FILTER: u32 = 0x10;
+/// Device-output calls write whole images: the owned rows at their image rows.
+pub const RT_FLAG_IMAGE_OUT: u32 = 0x20;
 
 extern "C" {
     pub fn rt_version() -> c_int;

@@ -165,6 +165,15 @@ typedef struct rt_params {
  * identical; the flag exists for A/B timing and for checking one filter
  * against the other (rt_render*, rt_intersect_ex). */
 #define RT_FLAG_VALU_FILTER 0x10u
+/* RT_FLAG_IMAGE_OUT (device-output calls: rt_render_device,
+ * rt_render_frames_device): the output pointer addresses whole images --
+ * frame i at out + i*width*height pixels -- and the call writes the rows it
+ * owns at their image rows (y*width + x), leaving the other rows untouched,
+ * instead of its rows packed. N row shards of one frame then write one image:
+ * e.g. rank 0's buffer mapped into every rank (hipIpcOpenMemHandle), so the
+ * row tiling needs no gather. The reference has no
+ * counterpart (one device, ray_trace_node.rs:213-224). */
+#define RT_FLAG_IMAGE_OUT 0x20u
 #define RT_JITTER_HASH_MUL 0x9E3779B1u
 #define RT_LENS_HASH_MUL   0x85EBCA77u
 

@@ -1,8 +1,9 @@
-"""bench.py's data paths on the GPU (one MI355X): the N>1 path -- shard slab,
-gather through the process group (backend nccl = RCCL), device re-assembly --
-taken at world size 1 (`--force-dist`) must give the frames of the
-single-GPU path bit for bit, and stdout must hold exactly the one JSON line
-(RCCL prints a version banner to fd 1 at communicator init)."""
+"""bench.py's data paths on the GPU (one MI355X): the N>1 paths -- shard slab,
+gather through the process group (backend nccl = RCCL), device re-assembly;
+or every rank writing into rank 0's image mapped with HIP IPC -- taken at
+world size 1 (`--force-dist`) or with N ranks on the one GPU must give the
+frames of the single-GPU path bit for bit, and stdout must hold exactly the
+one JSON line (RCCL prints a version banner to fd 1 at communicator init)."""
 import json
 import os
 import subprocess
@@ -25,27 +26,32 @@ def _bench(*extra):
 
 
 @pytest.mark.gpu
-def test_rccl_gather_path_matches_single_gpu():
+@pytest.mark.parametrize("gather", ["rccl", "ipc"])
+def test_rccl_gather_path_matches_single_gpu(gather):
+    """--force-dist at world 1: the RCCL gather + device re-assembly, and the
+    image-layout path (RT_FLAG_IMAGE_OUT into rank 0's own image)."""
     a = _bench()
-    b = _bench("--force-dist", "--dist-backend", "nccl")
+    b = _bench("--force-dist", "--dist-backend", "nccl", "--gather", gather)
     assert a["config"]["parallelism"] == "single GPU"
-    assert "RCCL gather" in b["config"]["parallelism"]
+    assert ("RCCL gather" if gather == "rccl" else "rank 0's image") in b["config"]["parallelism"]
     assert a["check"] == b["check"] and len(a["check"]) == 2  # the last launch's frames
     assert a["segments_per_frame"] == b["segments_per_frame"]
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [2, 3])
-def test_bench_launches_its_own_ranks(n):
+@pytest.mark.parametrize("n,gather", [(2, "rccl"), (3, "rccl"), (2, "ipc"), (3, "ipc")])
+def test_bench_launches_its_own_ranks(n, gather):
     """`python bench.py --gpus N` with no launcher around it (the driver's
-    scaling command) starts the N ranks itself and relays rank 0's line;
-    the assembled frames (rt_assemble_shard_frames over 2-frame launches;
-    225 rows split unevenly) equal the single-GPU run's (all ranks on the one
-    GPU of this box, host-staged gloo gather)."""
+    scaling command) starts the N ranks itself and relays rank 0's line; the
+    frames (2-frame launches; 225 rows split unevenly) equal the single-GPU
+    run's -- all ranks on the one GPU of this box, either gathered (host-staged
+    gloo gather + rt_assemble_shard_frames) or written by every rank straight
+    into rank 0's image mapped into it with HIP IPC (RT_FLAG_IMAGE_OUT)."""
     a = _bench()
-    b = _bench("--gpus", str(n), "--same-device", "--dist-backend", "gloo")
+    b = _bench("--gpus", str(n), "--same-device", "--dist-backend", "gloo", "--gather", gather)
     assert b["n_gpus"] == n and len(b["ranks"]["segments"]) == n
     assert sum(b["ranks"]["segments"]) // 4 == a["segments_per_frame"]  # 4 timed frames
+    assert ("rank 0's image" in b["config"]["parallelism"]) == (gather == "ipc")
     assert a["check"] == b["check"]
     assert a["segments_per_frame"] == b["segments_per_frame"]
 
