@@ -51,8 +51,6 @@ struct Frame {
     uint32_t* d_counters = nullptr; // [0..3] 2 x u64 segment counters, [4..] per-pass work counters
     size_t counters_cap = 0;        // in u32 words
     unsigned long long* h_segs = nullptr;  // pinned, 18 counters
-    uint32_t* d_fin = nullptr;      // fused collect: item counters per (frame, pixel) of a launch
-    size_t fin_cap = 0;
     std::vector<hipEvent_t> ev;     // 2 per pass
     hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;
     // the pending call in this slot
@@ -78,7 +76,6 @@ struct Tuning {
     // (profiles/r03/item_order/): full frame 243.7 -> 240.2 ms, N=8 shard
     // 34.9 -> 33.5 ms; 1 alone 242.6 / 33.5, 2 alone 241.0 / 35.4
     uint32_t item_order = 3;
-    bool fused_collect = false;   // KParams::fin_cnt: single-pass launches fold in the render kernel
     bool prefetch = true;         // waves prefetch their next work chunk
     uint32_t prio_mode = 1;       // s_setprio rotation: 0 off, 1 by iteration, 3 by wall time
     uint32_t prio_shift = 14;     // mode 3 step: 2^prio_shift ticks of 10 ns
@@ -222,8 +219,6 @@ static bool tune_set(Tuning& t, const char* name, const char* v) {
         t.split_all = x != 0;
     } else if (!strcmp(name, "tail_split")) {
         t.tail_split = x != 0;
-    } else if (!strcmp(name, "fused_collect")) {
-        t.fused_collect = x != 0;
     } else if (!strcmp(name, "item_order")) {
         if (x < 0 || x > 3) return false;
         t.item_order = (uint32_t)x;
@@ -956,11 +951,8 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         return (v + mult - 1) / mult * mult;
     };
     const bool all_single = tn.split_all && (p.flags & RT_FLAG_NO_PRIMARY_CACHE);
-    // (every region a multiple of 4 samples, so with spp % 4 == 0 no 2- or
-    // 4-sample tail item straddles two frames: the fused collect counts items
-    // per frame)
-    const uint64_t A4 = all_single ? 0 : per_px(ta[0], 4), A2 = all_single ? 0 : per_px(ta[1], 4);
-    const uint64_t A1 = all_single ? ~0ull / 4 : per_px(ta[2], 4);
+    const uint64_t A4 = all_single ? 0 : per_px(ta[0], 4), A2 = all_single ? 0 : per_px(ta[1], 2);
+    const uint64_t A1 = all_single ? ~0ull / 4 : per_px(ta[2], 1);
     auto tail_pairs = [&](uint64_t pairs) -> uint64_t {
         if (!tail_on || !npix) return 0;
         const uint64_t L = (A4 + A2 + A1 + RT_SAMPLE_BLOCK - 1) / RT_SAMPLE_BLOCK;
@@ -1028,14 +1020,6 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         if (rc) return rc;
         rc = ensure(ctx, &f.d_pd, &f.pd_cap, per_block);  // 16-B pixel table entries
         if (rc) return rc;
-        // fused collect: whole-frame passes only (a frame split over passes
-        // carries its partial sum between launches: rt_collect_kernel)
-        if (tn.fused_collect && prog_mode == 0 && passes[0].nblocks == blocks_total) {
-            uint32_t maxf = 0;
-            for (const Pass& ps : passes) maxf = std::max(maxf, ps.nframes);
-            rc = ensure(ctx, &f.d_fin, &f.fin_cap, (size_t)maxf * npix * sizeof(uint32_t));
-            if (rc) return rc;
-        }
     }
     const size_t words = RT_CNT_WORK_OFFSET + passes.size();
     const size_t words_pad = (words + 3) & ~(size_t)3;  // 16-B multiple
@@ -1184,15 +1168,6 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         K_.item_order = tn.item_order;
         K_.div_nreg = make_fastdiv(K_.qmain > K_.qpix ? K_.qmain - K_.qpix : 1u);
         K_.div_nfpix = make_fastdiv(npix && K_.main_pix ? K_.main_pix / npix : 1u);
-        K_.div_spp = make_fastdiv(p.spp);
-        // fused collect when the pass holds whole frames and no 2- / 4-sample
-        // tail item straddles two frames (spp % 4 == 0 with the tail regions'
-        // 4-sample rounding, or no such regions)
-        const bool fused = tn.fused_collect && prog_mode == 0 && ps.block_begin == 0 &&
-                           ps.nblocks == blocks_total && f.d_fin &&
-                           (p.spp % 4 == 0 || g2 == g0);
-        K_.fin_cnt = fused ? f.d_fin : nullptr;
-        K_.fin_out = d_out + (size_t)ps.frame_begin * fstride;
         K_.div_ng4 = make_fastdiv(g1 > g0 ? (uint32_t)((g1 - g0 + 3) / 4) : 1u);
         K_.div_ng2 = make_fastdiv(g2 > g1 ? (uint32_t)((g2 - g1 + 1) / 2) : 1u);
         K_.div_ng1 = make_fastdiv(g_end > g2 ? (uint32_t)(g_end - g2) : 1u);
@@ -1202,8 +1177,6 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         const uint32_t grid = (uint32_t)(need_blocks < grid_full ? need_blocks : grid_full);
         const uint64_t tail_items = 2ull * RT_WAVE_CHUNK * grid * (RT_BLOCK_THREADS / 64);
         K_.tail_start = (uint32_t)(items > tail_items ? items - tail_items : 0);
-        if (fused)
-            HIP_TRY_Q(hipMemsetAsync(f.d_fin, 0, (size_t)ps.nframes * npix * sizeof(uint32_t), stream));
         HIP_TRY_Q(hipEventRecord(f.ev[2 * i], stream));
         HIP_TRY_Q(rt_launch_render(&K_, cull ? ctx->d_grp_c : ctx->d_grp,
                                       cull ? ctx->d_sph_c : ctx->d_sph,
@@ -1215,10 +1188,9 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         HIP_TRY_Q(hipEventRecord(f.ev[2 * i + 1], stream));
         const bool first_pass = ps.block_begin == 0;
         const bool last_pass = ps.block_begin + ps.nblocks == blocks_total;
-        if (!fused)
-            HIP_TRY_Q(rt_launch_collect(&K_, f.d_block_sums, f.d_acc, first_pass, last_pass,
-                                           (float)p.spp, d_out + (size_t)ps.frame_begin * fstride,
-                                           ctx->d_prog, prog_mode, prog_total, stream));
+        HIP_TRY_Q(rt_launch_collect(&K_, f.d_block_sums, f.d_acc, first_pass, last_pass,
+                                       (float)p.spp, d_out + (size_t)ps.frame_begin * fstride,
+                                       ctx->d_prog, prog_mode, prog_total, stream));
     }
     HIP_TRY_Q(hipMemcpyAsync(f.h_segs, f.d_counters, 18 * sizeof(unsigned long long),
                                 hipMemcpyDeviceToHost, stream));

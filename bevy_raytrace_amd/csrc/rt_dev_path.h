@@ -25,7 +25,7 @@ struct LaneLds {
     float4 acc;       // fold of the item's block sums so far
     float2 cache;     // primary hit (index bits, t) -- primary-hit reuse only
     uint32_t iend;    // end of the item's samples
-    uint32_t fk;      // fused collect: the item's (frame, pixel) counter, f * npix + k
+    uint32_t pad;
 };
 typedef LaneLds* ItemLds;  // the lane's own record
 
@@ -161,7 +161,6 @@ __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint
             b0 = q - f * nblocks;
             b1 = b0 + 1;
         }
-        L->fk = f * npix + k;
         const uint32_t base = sample_base + f * spp;
         s0 = base + (block_begin + b0) * RT_SAMPLE_BLOCK;
         const uint32_t iend = base + min(spp, (block_begin + b1) * RT_SAMPLE_BLOCK);
@@ -187,8 +186,6 @@ __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint
         }
         s0 = sample_base + gb + g * z;
         s1 = sample_base + min(gb + g * z + z, ge);
-        // (the fused collect's plan keeps a tail item inside one frame)
-        if (P.fin_cnt) L->fk = fdiv(gb + g * z, P.div_spp) * npix + k;
     }
     const float4 q4 = tab[k].d;
     // main item: its output slot (= queue index); tail item: RT_TAIL_ITEM | k
@@ -311,8 +308,7 @@ __device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, f
 // then its tail blocks, whose samples' colours are summed here exactly as a
 // lane sums a block, ((0 + c0) + c1) + ..., in sample order; each folded as
 // the lane folds (first as is, then acc + it). `have` / (ax, ay, az) carry an
-// earlier pass's partial sum. ld(slot) reads one slot: plain loads in
-// rt_collect_kernel, write-through (sc1) loads in the fused collect.
+// earlier pass's partial sum. ld(slot) reads one slot.
 template <typename LD>
 __device__ __forceinline__ void fold_frame(const KParams& P, uint32_t f, uint32_t k, bool& have,
                                            float& ax, float& ay, float& az, LD ld) {
@@ -358,59 +354,4 @@ __device__ __forceinline__ float4* out_pixel(const KParams& P, float4* out, uint
         return out + (size_t)f * P.width * P.height + (size_t)y * P.width + x;
     }
     return out + (size_t)f * P.npix + p;
-}
-
-// ---- fused collect (KParams::fin_cnt) --------------------------------------
-// Slots an item leaves for the fused collect are written through to memory
-// (agent-scope relaxed atomic stores: `global_store_dword ... sc1`), drained
-// (s_waitcnt vmcnt(0)) before the item's counter increment, and read back
-// with agent-scope loads (sc1) by whichever wave finalizes the (frame, pixel)
-// -- the cross-XCD hand-off form of MI355X_MICROARCH.md (per-XCD L2s are not
-// coherent; a plain store could sit in the writer's L2).
-__device__ __forceinline__ void put_slot(float4* p, v3 c, bool through) {
-    if (through) {
-        uint32_t* q = reinterpret_cast<uint32_t*>(p);
-        __hip_atomic_store(q + 0, __float_as_uint(c.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(q + 1, __float_as_uint(c.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(q + 2, __float_as_uint(c.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        *p = make_float4(c.x, c.y, c.z, 0.0f);
-    }
-}
-
-__device__ __forceinline__ float4 get_slot_through(const float4* p) {
-    const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
-    return make_float4(
-        __uint_as_float(__hip_atomic_load(q + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
-        __uint_as_float(__hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
-        __uint_as_float(__hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)), 0.0f);
-}
-
-// Items covering frame f of one pixel: its pixel item (pairs below qpix), its
-// block items, and its tail items (the plan keeps each inside one frame).
-__device__ __forceinline__ uint32_t fin_units(const KParams& P, uint32_t f) {
-    const uint32_t q0 = f * P.nblocks;
-    uint32_t u = q0 < P.qpix ? 1u : 0u;
-    const uint32_t qa = max(q0, P.qpix), qb = min(q0 + P.nblocks, P.qmain);
-    u += qb > qa ? qb - qa : 0u;
-    const uint32_t a = f * P.spp, b = a + P.spp;  // the frame's launch samples
-    auto ov = [&](uint32_t lo, uint32_t hi) {
-        lo = max(lo, a);
-        hi = min(hi, b);
-        return hi > lo ? hi - lo : 0u;
-    };
-    return u + ov(P.g0, P.g1) / 4u + ov(P.g1, P.g2) / 2u + ov(P.g2, P.g_end);
-}
-
-// One lane's share of a finalize task: the fold of (frame, pixel) fk, / spp,
-// written where the frame goes.
-__device__ __forceinline__ void fin_pixel(const KParams& P, const float4* block_sums, uint32_t fk) {
-    const uint32_t f = fdiv(fk, P.div_npix), k = fk - f * P.npix;
-    bool have = false;
-    float ax = 0.0f, ay = 0.0f, az = 0.0f;
-    fold_frame(P, f, k, have, ax, ay, az,
-               [&](size_t slot) { return get_slot_through(block_sums + slot); });
-    const float spp = (float)P.spp;
-    *out_pixel(P, P.fin_out, f, order_to_pixel(P, k)) =
-        make_float4(ax / spp, ay / spp, az / spp, 1.0f);
 }

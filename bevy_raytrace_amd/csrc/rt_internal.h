@@ -108,15 +108,6 @@ struct KParams {
     // pair- / sample- / frame-major (consecutive items: neighbouring pixels)
     uint32_t item_order;
     FastDiv div_nfpix; // by main_pix / npix (frames with pixel items)
-    FastDiv div_spp;   // by spp (a tail item's frame)
-    // Fused collect (single-pass launches, knob fused_collect): the render
-    // kernel folds each (frame, pixel) itself once the last item covering it
-    // has completed -- per (frame, pixel) an item counter, fin_cnt[f * npix +
-    // k], compared with fin_units(f) -- and writes frame f at fin_out (shard
-    // layout, or the image layout with RT_FLAG_IMAGE_OUT). Null: the launch's
-    // rt_collect_kernel does it.
-    uint32_t* fin_cnt;
-    float4* fin_out;
     FastDiv div_nreg;  // by qmain - qpix (pairs of the block-item region)
     // by the sample groups per pixel of the tail regions: (g1 - g0 + 3) / 4,
     // (g2 - g1 + 1) / 2, g_end - g2 (4-, 2-, 1-sample items)

@@ -137,10 +137,6 @@ __device__ __forceinline__ void render_body(
 #endif
     __shared__ LaneLds s_lane[RT_BLOCK_THREADS];  // per-lane item state (rt_dev_path.h)
     const ItemLds lds = s_lane + wave * 64u + lane;
-    // fused collect: per wave a list of finished (frame, pixel) counters,
-    // finalized 64 at a time (one per lane)
-    __shared__ uint32_t s_fin[(RT_BLOCK_THREADS / 64) * 128];
-    uint32_t* const fin_list = s_fin + wave * 128u;
 #ifdef RT_SPHERES_LDS
     // Experiment variant: the filter reads the sphere groups from LDS (staged
     // once per workgroup) instead of the scalar cache.
@@ -189,43 +185,6 @@ __device__ __forceinline__ void render_body(
     const uint32_t wave_slot = __builtin_amdgcn_s_getreg((3 << 11) | 4);
     uint32_t pref = 0;            // lane 0: base of the prefetched chunk
     uint32_t pref_chunk = 0;      // its size (0 = none in flight)
-    // Fused collect (P.fin_cnt). An item's completion is counted one
-    // iteration late: lanes whose item ended (fin_pend) increment its
-    // (frame, pixel) counter after the next walk, when its write-through slot
-    // stores have long drained (the s_waitcnt vmcnt(0) there is free), and
-    // check the returned count after that iteration's shading (fin_chk); the
-    // lane that completes the count queues the (frame, pixel) in the wave's
-    // list, and the wave finalizes 64 at a time.
-    uint64_t fin_pend = 0, fin_chk = 0;  // wave-uniform lane masks
-    uint32_t fin_fk = 0, fin_res = 0;    // the lane's counter index, returned count
-    uint32_t fin_n = 0;                  // entries in the wave's list
-    auto fin_push = [&](bool done) {
-        const uint64_t m = rt_ballot(done);
-        if (m) {
-            if (done) fin_list[fin_n + lanemask_lt_count(m)] = fin_fk;
-            fin_n += (uint32_t)__popcll(m);
-        }
-    };
-    auto fin_task = [&](const KParams& Q, uint32_t cnt) {  // the list's top cnt entries
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (lane < cnt) fin_pixel(Q, block_sums, fin_list[fin_n - cnt + lane]);
-        fin_n -= cnt;
-    };
-    auto fin_count = [&](const KParams& Q) {  // the pending lanes' counter increments
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if ((fin_pend >> lane) & 1u)
-            fin_res = __hip_atomic_fetch_add(Q.fin_cnt + fin_fk, 1u, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-        fin_chk = fin_pend;
-        fin_pend = 0;
-    };
-    auto fin_check = [&](const KParams& Q) {
-        const bool done = ((fin_chk >> lane) & 1u) &&
-                          fin_res + 1u == fin_units(Q, fdiv(fin_fk, Q.div_npix));
-        fin_chk = 0;
-        fin_push(done);
-    };
 
     for (;;) {
 #ifndef RT_PARAMS_HOLD
@@ -346,7 +305,6 @@ __device__ __forceinline__ void render_body(
 #endif
                                        P.bnd, P.perm, P.nclusters, P.cull_supers != 0);
         }
-        if (fin_pend) fin_count(P);
         traced = __builtin_amdgcn_readfirstlane(traced + (uint32_t)__popcll(live));
         if (use_cache && has_item && st.bounce == 0)  // the item's first sample: its primary hit
             lds->cache = make_float2(__int_as_float(hi), t);
@@ -368,9 +326,9 @@ __device__ __forceinline__ void render_body(
                     // a tail item stores every sample's colour for the collect
                     if (st.item & RT_TAIL_ITEM) {
                         const v3 c = add(mk(0.0f, 0.0f, 0.0f), st.color);
-                        put_slot(block_sums + P.main_all +
-                                     (st.s - P.sample_base - P.g0) * P.npix + (st.item & ~RT_TAIL_ITEM),
-                                 c, P.fin_cnt != nullptr);
+                        block_sums[P.main_all +
+                                   (st.s - P.sample_base - P.g0) * P.npix + (st.item & ~RT_TAIL_ITEM)] =
+                            make_float4(c.x, c.y, c.z, 0.0f);
                     } else {
                         st.bsum = add(st.bsum, st.color);
                     }
@@ -390,7 +348,7 @@ __device__ __forceinline__ void render_body(
                             st.s_end = min(st.s + RT_SAMPLE_BLOCK, iend);
                             next = true;
                         } else {
-                            put_slot(block_sums + st.item, acc, P.fin_cnt != nullptr);
+                            block_sums[st.item] = make_float4(acc.x, acc.y, acc.z, 0.0f);
                         }
                     }
                     if (next) {
@@ -407,24 +365,7 @@ __device__ __forceinline__ void render_body(
                 }
             }
         }
-        if (fin_chk) fin_check(P);
-        if (P.fin_cnt) {
-            const uint64_t ended = live & ~rt_ballot(has_item);
-            if ((ended >> lane) & 1u) fin_fk = lds->fk;
-            fin_pend = ended;
-            if (fin_n >= 64u) fin_task(P, 64u);
-        }
         PROF_MARK(3);
-    }
-    {  // fused collect: the last items' counts, then the rest of the list
-#ifndef RT_PARAMS_HOLD
-        const KParams& P = fresh_params();
-#endif
-        if (fin_pend) {
-            fin_count(P);
-            fin_check(P);
-        }
-        while (fin_n) fin_task(P, min(fin_n, 64u));
     }
 
 #ifdef RT_PROFILE

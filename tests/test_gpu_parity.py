@@ -271,48 +271,17 @@ def test_item_order_identical(renderer, S, region, tail):
     check_exact(outs[1][0][1], ref)
 
 
-@pytest.mark.parametrize("S,F,region,tail", [(64, 3, "96", "0,1,1"), (16, 2, "1000000", "0.01,0.01,0.01"),
-                                             (64, 2, "0", "0,0,6"), (21, 2, "96", "0,1,1"),
-                                             (8, 5, "96", "1,1,1")])
-def test_fused_collect_identical(renderer, S, F, region, tail):
-    """The fused collect (knob fused_collect: each (frame, pixel) folded in the
-    render kernel by the wave whose item completes its count, from
-    write-through slots) gives rt_collect_kernel's frames and segment counts:
-    pixel, block and 4-/2-/1-sample tail items, several frames per launch;
-    S=21 keeps the collect kernel (2-sample tail items could straddle frames)."""
-    import torch
-    sp, mt = arrays(scene.rtiow_final_scene())
-    cam = default_camera_block()
-    W, H = 72, 40
-    renderer.set_scene(sp, mt)
-    outs = []
-    for fused in ("0", "1"):
-        renderer.tune(None)
-        renderer.tune(block_region=region, tail=tail, fused_collect=fused)
-        buf = torch.full((F, H, W, 4), -7.0, dtype=torch.float32, device="cuda")
-        renderer.render_frames_device(cam, F, buf.data_ptr(), W, H, S, 10, frame0=3, flags=NO_REUSE)
-        st = renderer.wait()
-        outs.append((buf.cpu().numpy(), st["segments"]))
-    check_exact(outs[1][0], outs[0][0])
-    assert outs[1][1] == outs[0][1]
-    ref, segs = O.render(cam, sp, mt, W, H, S, 10, frame0=3 + S)  # launch frame 1
-    check_exact(outs[1][0][1], ref)
-
-
-@pytest.mark.parametrize("fused", ["0", "1"])
 @pytest.mark.parametrize("K,B", [(3, 5), (8, 1)])
-def test_image_out_shards_fill_one_image(renderer, fused, K, B):
+def test_image_out_shards_fill_one_image(renderer, K, B):
     """RT_FLAG_IMAGE_OUT: K row shards of a 2-frame launch write their rows
     at their image rows of ONE buffer (what every rank does through rank 0's
-    IPC-mapped image, bench.py) -- together the full render, with the
-    collect kernel and with the fused collect; rows a shard does not own are
-    left untouched."""
+    IPC-mapped image, bench.py) -- together the full render; rows a shard
+    does not own are left untouched."""
     import torch
     sp, mt = arrays(scene.rtiow_final_scene())
     cam = default_camera_block()
     W, H, S, D, F = 96, 61, 8, 8, 2
     renderer.set_scene(sp, mt)
-    renderer.tune(fused_collect=fused)
     full = torch.empty((F, H, W, 4), dtype=torch.float32, device="cuda")
     renderer.render_frames_device(cam, F, full.data_ptr(), W, H, S, D, flags=NO_REUSE)
     renderer.wait()
