@@ -10,10 +10,11 @@ through the persistent HIP kernel, depth 16, written to an HBM image. Inputs
 N > 1 runs one process per GPU under torch.distributed.run; a bare
 `python bench.py --gpus N` (no WORLD_SIZE in the environment) launches that
 itself as a child process before touching the GPU and relays rank 0's line. The image
-is row-tiled in blocks dealt serpentine to the ranks, each rank
-renders its rows,
-then one RCCL gather over xGMI lands the shards on rank 0, which re-assembles
-the image on the device. Timing: barrier + synchronize around exactly K steps,
+is row-tiled in blocks dealt serpentine to the ranks; rank 0's
+image is mapped into every rank (HIP IPC) and each rank's collect writes its
+rows straight into it over xGMI (RT_FLAG_IMAGE_OUT) -- or, if the mapping
+fails on some rank, one RCCL gather lands the shards on rank 0, which
+re-assembles the image on the device (--gather). Timing: barrier + synchronize around exactly K steps,
 max over ranks. value = algorithmic ray segments of the whole frame (all ranks)
 per second, every segment traced (primary-hit reuse off for the headline;
 its frame time is reported separately as `primary_reuse`).
