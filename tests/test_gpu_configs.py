@@ -56,13 +56,13 @@ def _render_shard_device(renderer, cam, W, H, S, D, B, K, k, flags):
 @pytest.mark.parametrize("k", [0, 7])
 def test_config4_8k_shard_of_8(renderer, k):
     """One rank's part of the 8-GPU 8K frame (row blocks of
-    pick_row_block(4320, 8) = 6 rows, serpentine deal): the shard's first and
+    pick_row_block(4320, 8) = 1 row, serpentine deal): the shard's first and
     last rows and rows on both sides of y*W = 2^24, bit-exact."""
     wl, sp, mt = _scene("rtiow8k")
     W, H, S, D = wl.width, wl.height, wl.spp, wl.max_depth
     K = 8
     B = pick_row_block(H, K)
-    assert B == 6 and H % (B * K) == 0
+    assert B == 1 and H % (B * K) == 0
     cam = default_camera_block()
     renderer.set_scene(sp, mt)
     rows, img, st = _render_shard_device(renderer, cam, W, H, S, D, B, K, k, NO_REUSE)
@@ -115,7 +115,7 @@ def test_config5_10k_full_frame(renderer):
 def test_config5_10k_segments_exact(renderer):
     """Segment count exact against the oracle on a 4-row shard (B = 1,
     K = 270), and on the full frame as the union of the 8 shards of the
-    8-GPU layout (pick_row_block(1080, 8) = 5)."""
+    8-GPU layout (pick_row_block(1080, 8) = 1)."""
     wl, sp, mt = _scene("spheres10k1080")
     W, H, S, D = wl.width, wl.height, wl.spp, wl.max_depth
     cam = default_camera_block()

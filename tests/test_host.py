@@ -86,7 +86,8 @@ def test_row_block_choice():
     for n in (2, 4, 8):
         b = pick_row_block(1080, n)
         assert 1080 % b == 0 and (1080 // b) % n == 0
-    assert pick_row_block(4320, 8) == 6  # 720 blocks, 90 per rank
+    assert pick_row_block(4320, 8) == 1  # single rows, 540 per rank
+    assert pick_row_block(225, 2) == 8  # no even split: the round-2 fallback
     assert WORKLOADS["rtiow1080"].spp == 64 and WORKLOADS["rtiow1080"].max_depth == 16
 
 
