@@ -10,7 +10,7 @@ struct PathState {
     v3 nseed;           // normalize(seed)
     float seedx;        // seed.x (dielectric Schlick test)
     uint32_t pix;       // global pixel x + W*y (the seed's pixel term, shade.wgsl:216-218)
-    uint32_t item;      // main item: its queue index (= output slot); tail: RT_TAIL_ITEM | pixel
+    uint32_t item;      // main item: its output slot; tail: RT_TAIL_ITEM | pixel
     uint32_t s, s_end;  // current sample, end of the current sample block
     uint32_t bounce;
 };
@@ -108,11 +108,13 @@ struct PixelEntry {
 // order -- the lane sums each block of RT_SAMPLE_BLOCK samples in registers
 // (st.s_end = the block's end), folds the block sums in block order (acc =
 // bsum_0; acc = acc + bsum_b, rt_collect_kernel's fold) and stores the fold
-// once, at slot = its queue index. Pairs [qpix, qmain) as block items (item <
-// main_all): one block of one pixel, its sum stored at its slot -- short
-// items at the end of the main part, so no lane holds a long pixel item
-// when the queue runs dry. A tail item is z = 4, 2 or 1 consecutive samples
-// of one pixel, each sample's colour stored on its own.
+// once, at slot f*npix + k. Pairs [qpix, qmain) as block items (item <
+// main_all): one block of one pixel, its sum stored at slot main_pix +
+// r*npix + k (r = q - qpix) -- short items at the end of the main part, so
+// no lane holds a long pixel item when the queue runs dry. A tail item is
+// z = 4, 2 or 1 consecutive samples of one pixel, each sample's colour
+// stored on its own. item_order picks the item -> (frame / pair / group,
+// pixel) map: pixel-major (default) puts one pixel's items back to back.
 __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint32_t item,
                                            const PixelEntry* __restrict__ tab, ItemLds L) {
     // The launch parameters are read as values (scalar loads) and the item
@@ -188,7 +190,7 @@ __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint
         s1 = sample_base + min(gb + g * z + z, ge);
     }
     const float4 q4 = tab[k].d;
-    // main item: its output slot (= queue index); tail item: RT_TAIL_ITEM | k
+    // main item: its output slot; tail item: RT_TAIL_ITEM | k
     st.item = item < P.main_all ? slot : (RT_TAIL_ITEM | k);
     st.pix = __float_as_uint(q4.w);
     st.s = s0;

@@ -48,18 +48,19 @@ struct KParams {
     // frame0 + that) x blocks [block_begin, block_begin + nblocks) of each.
     // Its (frame, block) pairs q = f*nblocks + b: pairs q < qmain are the main
     // part, dealt as pixel items for q < qpix -- one item per (frame, pixel),
-    // items [0, main_pix = ceil(qpix / nblocks) * npix), frame-major, covering
-    // that frame's pairs below qpix; the lane folds their block sums and
-    // stores the fold at slot = its queue index -- then as block items for
-    // q in [qpix, qmain): items [main_pix, main_all), one (pair, pixel) each,
-    // pair-major, storing the block's sum at slot = its queue index (short
-    // items, so no lane holds a long pixel item when the queue runs dry). The
-    // rest -- the launch's tail, launch samples g = f*spp + s in [g0, g_end)
-    // -- is dealt as shrinking items: 4-sample items over [g0, g1), 2-sample
-    // over [g1, g2), single samples over [g2, g_end), each region
-    // sample-major; a tail item stores every sample's colour at slot
-    // main_all + (g - g0)*npix + k. rt_collect_kernel folds them per pixel in
-    // block / sample order.
+    // items [0, main_pix = ceil(qpix / nblocks) * npix), covering that
+    // frame's pairs below qpix; the lane folds their block sums and stores
+    // the fold at slot = f*npix + k -- then as block items for q in
+    // [qpix, qmain): items [main_pix, main_all), one (pair, pixel) each,
+    // storing the block's sum at slot = main_pix + r*npix + k (short items,
+    // so no lane holds a long pixel item when the queue runs dry). The rest
+    // -- the launch's tail, launch samples g = f*spp + s in [g0, g_end) -- is
+    // dealt as shrinking items: 4-sample items over [g0, g1), 2-sample over
+    // [g1, g2), single samples over [g2, g_end); a tail item stores every
+    // sample's colour at slot main_all + (g - g0)*npix + k. Which item index
+    // maps to which (frame / pair / sample group, pixel) is item_order's
+    // business (below); the slots, and so the fold, do not depend on it.
+    // rt_collect_kernel folds them per pixel in block / sample order.
     uint32_t nframes, sample_base, qmain, main_all;
     uint32_t qpix, main_pix;
     uint32_t g0, g1, g2, g_end;
@@ -102,8 +103,8 @@ struct KParams {
     const uint4* mfA;
     uint32_t mf_nblk;
     float mf_qs, mf_abs;  // 2^sq (quadratic features' ray-side scale), threshold margin
-    // queue order (knob item_order, bits): bit 0 the block items and the
-    // single-sample tail items, bit 1 the pixel items, pixel-major
+    // queue order (knob item_order, bits; default 3): bit 0 the block items
+    // and the tail items, bit 1 the pixel items, pixel-major
     // (consecutive items: one pixel's pairs / samples / frames) instead of
     // pair- / sample- / frame-major (consecutive items: neighbouring pixels)
     uint32_t item_order;
