@@ -684,7 +684,9 @@ static void f16_split(double x, uint16_t& hi, uint16_t& lo) {
 static int build_mfma(rt_ctx* ctx) {
     const uint32_t n = ctx->n;
     ctx->mf_ok = false;
-    if (!n) return RT_OK;
+    // queue entries hold a 14-bit group index (rt_dev_intersect.h mf_spread):
+    // larger lists use the VALU filter
+    if (!n || n > (1u << 16)) return RT_OK;
     const double kS = 1.0 - 0x1p-16 - 0x1p-16;  // 1 - m - mu' (RT_MF_MU)
     double qmax = 1.0;
     for (uint32_t j = 0; j < n; ++j) {

@@ -642,8 +642,8 @@ __device__ __forceinline__ uint32_t lanemask_lt_count(uint64_t m) {
 // (a tile or group with a candidate has a value with the sign bit set) and
 // compares. Output layout (MI355X guide): lane l holds column (ray) l & 31 of
 // the half, rows (spheres) (i & 3) + 8 (i >> 2) + 4 (l >> 5) in register i:
-// four whole groups of 4 spheres per lane. A lane queues (group-of-4 index
-// << 4 | 4-bit mask) per half; the ray's lane drains the entries of its
+// four whole groups of 4 spheres per lane. A lane queues (group index, 4
+// candidate flags) per half (RT_MF_FLAGS); the ray's lane drains the entries of its
 // column's two lanes, in any order, with the (t, index) tie-break (exact_body
 // LEX).
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
@@ -673,6 +673,28 @@ typedef float f16x __attribute__((ext_vector_type(16)));
 #endif
 // LDS words per wave of the matrix-core walk: the two halves' queues
 #define RT_MF_QW (2u * RT_MF_CAP * 64u)
+
+// Queue entry of a group of 4 spheres: its candidate flags in bits 7, 15, 23,
+// 31 (sphere 4g + 0..3; v_perm_b32 sign-replicated bytes, mf_flags) and its
+// group index g' = 8b + 2q (block b, group q; the half h is the queuing
+// lane's, known to the drain) in the other bits, 7 per byte (mf_spread):
+// g' < 2^14, so the matrix-core walk takes lists of up to 2^16 spheres
+// (rt_api.cpp build_mfma; larger lists use the VALU filter).
+#define RT_MF_FLAGS 0x80808080u
+__host__ __device__ __forceinline__ uint32_t mf_spread(uint32_t g) {
+    return (g & 0x7Fu) | ((g & 0x3F80u) << 1);
+}
+__device__ __forceinline__ uint32_t mf_unspread(uint32_t e) {
+    return (e & 0x7Fu) | ((e >> 1) & 0x3F80u);
+}
+// the candidate flags of a group's four values V: bytes 0..3 = 0xFF when
+// V[4q + byte] has its sign bit set (v_perm_b32 selectors 9 / 11 replicate
+// bit 31 of the low / high source), two perms and an OR
+__device__ __forceinline__ uint32_t mf_flags(float v0, float v1, float v2, float v3) {
+    const uint32_t lo = __builtin_amdgcn_perm(__float_as_uint(v1), __float_as_uint(v0), 0x0C0C0B09u);
+    const uint32_t hi = __builtin_amdgcn_perm(__float_as_uint(v3), __float_as_uint(v2), 0x0B090C0Cu);
+    return lo | hi;
+}
 
 __device__ __forceinline__ uint32_t bperm(uint32_t src_lane, uint32_t v) {
     return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
@@ -727,11 +749,13 @@ __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, ui
         if (m == 0) {
             const bool s1 = i >= na;
             const uint32_t e = q[(s1 ? i - na : i) * 64u + (s1 ? j + 32u : j)];
-            m = e & 15u;
-            base = (e >> 4) * 4u;
+            m = e & RT_MF_FLAGS;
+            // group index 8b + 2q (mf_unspread), + h: the column's lane
+            // j (h = 0) or j + 32 (h = 1) queued it
+            base = (mf_unspread(e) + (s1 ? 1u : 0u)) * 4u;
             ++i;
         }
-        const uint32_t b = __builtin_ctz(m);
+        const uint32_t b = __builtin_ctz(m) >> 3;
         m &= m - 1;
         MF_ECNT_INC;
         exact_body<FAST, false, true>(sph[base + b], (int)(base + b), o, d, a, ya, best_t, best_i,
@@ -742,7 +766,7 @@ __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, ui
 
 // The ORs of a tile's 16 values V = T0 - H0 per group of 4 and over the tile
 // (10 VALU: v_or3 / v_or). A group or tile with a candidate (V < 0) has the
-// sign bit set in its OR. The per-value masks are sign bits too (sgn4), so a
+// sign bit set in its OR. The per-value flags are sign bits too (mf_flags), so a
 // -0 or a NaN with the sign bit set is queued as well: harmless, since a -0
 // never comes from a sphere the exact test can hit (the margins leave V <=
 // -slack) and a NaN only from a ray with a NaN/inf feature, whose exact tests
@@ -759,12 +783,6 @@ __device__ __forceinline__ void tile_or(const f16x& H, int* gq, int& g) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) gq[q] = (v[4 * q] | v[4 * q + 1] | v[4 * q + 2]) | v[4 * q + 3];
     g = (gq[0] | gq[1] | gq[2]) | gq[3];
-}
-
-// the sign bits of a group's four values as its 4-bit candidate mask
-__device__ __forceinline__ uint32_t sgn4(float a, float b, float c, float d) {
-    return (__float_as_uint(a) >> 31) | ((__float_as_uint(b) >> 30) & 2u) |
-           ((__float_as_uint(c) >> 29) & 4u) | ((__float_as_uint(d) >> 28) & 8u);
 }
 
 // Called by the whole wave (the MFMA operands span all 64 lanes): lanes
@@ -789,7 +807,6 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
     const bool fast = ray_fast(scene_fast, o, a);
     const float ya = fast ? rt_recip_rn(a) : a;
     const uint32_t lane = __lane_id();
-    const uint32_t h = lane >> 5;
     // ray constants (ray_filter_consts, with the wider mu'), then the features
     const float rs = __builtin_amdgcn_rsqf(dot(d, d));
     const float ex = -(d.x * rs), ey = -(d.y * rs), ez = -(d.z * rs);  // e = -dn
@@ -885,10 +902,14 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
 
     float best_t = VERY_FAR;
     int best_i = -1;
-    uint32_t cnt0 = 0, cnt1 = 0;
+    // each lane's next queue slot per half (LDS word pointers, never below the
+    // queue: a DS address past the LDS window drops the write): an append is
+    // one store and one add; the counts are derived when needed
+    uint32_t* const q0 = cq + lane;
+    uint32_t* const q1 = cq + RT_MF_CAP * 64u + lane;
+    uint32_t *qp0 = q0, *qp1 = q1;
+    auto qcount = [](const uint32_t* p, const uint32_t* p0) { return (uint32_t)(p - p0) >> 6; };
     const f16x zero = {};
-    // is the ray of this lane's column live, per half
-    const bool col0 = (live_mask >> (lane & 31u)) & 1u, col1 = (live_mask >> (32u + (lane & 31u))) & 1u;
 #ifdef RT_PROFILE
     uint32_t ecnt_ = 0;  // this lane's exact tests (c[13]: wave max, c[15]: lane sum)
 #endif
@@ -901,13 +922,16 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
         // a block adds at most 4 entries to each half's queue: make room first,
         // while no tile result is live (the lanes' own counts are compared
         // only when the scalar bound says the queue may be full)
-        if (max(ub0, ub1) + 4u > RT_MF_CAP && rt_ballot(max(cnt0, cnt1) + 4u > RT_MF_CAP) != 0) {
+        if (max(ub0, ub1) + 4u > RT_MF_CAP &&
+            rt_ballot(max(qcount(qp0, q0), qcount(qp1, q1)) + 4u > RT_MF_CAP) != 0) {
+            const uint32_t cnt0 = qcount(qp0, q0), cnt1 = qcount(qp1, q1);
             PROF_ADD(11, 1);  // queue flushes
             if (fast)
                 mfma_drain<true>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
             else
                 mfma_drain<false>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
-            cnt0 = cnt1 = 0;
+            qp0 = q0;
+            qp1 = q1;
             ub0 = ub1 = 0;
         }
         h8v A0, A1;
@@ -926,17 +950,26 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
             tile_or(H, gq, g);
             if (rt_ballot(g < 0) != 0) {
                 PROF_ADD(5, 1);  // tiles with a candidate
-                uint32_t& cnt = t ? cnt1 : cnt0;
-                uint32_t* qt = cq + t * (RT_MF_CAP * 64u);
+                uint32_t*& qp = t ? qp1 : qp0;
+                const uint32_t sb = mf_spread(b * 8u);  // wave-uniform (SALU)
 #pragma unroll
                 for (uint32_t q = 0; q < 4; ++q) {
                     if (rt_ballot(gq[q] < 0) == 0) continue;  // no lane has one in this group
                     ++(t ? ub1 : ub0);
-                    const uint32_t m4 = sgn4(H[4 * q], H[4 * q + 1], H[4 * q + 2], H[4 * q + 3]);
-                    if (m4 && (t ? col1 : col0)) {
-                        qt[cnt * 64u + lane] = (((b * 8u) + q * 2u + h) << 4) | m4;
-                        ++cnt;
-                    }
+                    const uint32_t m = mf_flags(H[4 * q], H[4 * q + 1], H[4 * q + 2], H[4 * q + 3]);
+                    // Branch-free append: every lane writes its next slot
+                    // (< RT_MF_CAP: the check above) and keeps it only with a
+                    // flag set. A lane whose column has no live ray has no
+                    // flags: its T0 = +inf makes every V = +inf (no -inf
+                    // term: the pad rows' S' = -inf meets the ray's -1).
+                    // b * 8 has its low 3 bits clear: spread(8b + 2q) = spread(8b) + 2q
+                    const uint32_t f = m & RT_MF_FLAGS;
+                    *qp = f | (sb + q * 2u);
+                    // one more entry iff a flag is set: min(f, 1) as one VALU
+                    // min (the compiler otherwise emits a compare and a select)
+                    uint32_t inc;
+                    asm("v_min_u32 %0, 1, %1" : "=v"(inc) : "v"(f));
+                    qp += 64u * inc;
                 }
             }
         }
@@ -957,6 +990,7 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
     }
     if (b < nblk) block(b, a0, a1);
     PROF_MARK(1);
+    const uint32_t cnt0 = qcount(qp0, q0), cnt1 = qcount(qp1, q1);
     if (fast)
         mfma_drain<true>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
     else

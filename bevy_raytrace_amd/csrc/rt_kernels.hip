@@ -326,6 +326,9 @@ __device__ __forceinline__ void render_body(
                     // a tail item stores every sample's colour for the collect
                     if (st.item & RT_TAIL_ITEM) {
                         const v3 c = add(mk(0.0f, 0.0f, 0.0f), st.color);
+#ifdef RT_DIAG_NO_BSTORE  // timing diagnostic only: no slot stores (wrong image)
+                        if (c.x == -1234.5f)
+#endif
                         block_sums[P.main_all +
                                    (st.s - P.sample_base - P.g0) * P.npix + (st.item & ~RT_TAIL_ITEM)] =
                             make_float4(c.x, c.y, c.z, 0.0f);
@@ -348,6 +351,9 @@ __device__ __forceinline__ void render_body(
                             st.s_end = min(st.s + RT_SAMPLE_BLOCK, iend);
                             next = true;
                         } else {
+#ifdef RT_DIAG_NO_BSTORE
+                            if (acc.x == -1234.5f)
+#endif
                             block_sums[st.item] = make_float4(acc.x, acc.y, acc.z, 0.0f);
                         }
                     }

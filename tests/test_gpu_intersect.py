@@ -165,3 +165,30 @@ def test_valu_and_matrix_waves_side_by_side(renderer, fast):
         bad = np.nonzero((gi != ci) | (gt.view(np.uint32) != ct.view(np.uint32)))[0]
         assert bad.size == 0, f"launch {rep}: {bad.size} rays differ, e.g. {bad[:8].tolist()}"
 
+
+
+@pytest.mark.parametrize("n", [65_536, 65_537])
+def test_largest_matrix_core_list(renderer, n):
+    """The matrix-core walk's queue entries hold a 14-bit group index
+    (rt_dev_intersect.h mf_spread): 2^16 spheres is the largest list it takes
+    (group indices up to 16,382, both index bytes in use), one more sphere
+    goes to the VALU filter (rt_api.cpp build_mfma). Rays aimed at spheres
+    spread over the whole list, half of them at the last 4,096."""
+    from bevy_raytrace_amd.abi import MATERIAL_DTYPE, SPHERE_DTYPE
+    rng = np.random.default_rng(n)
+    sp = np.zeros(n, dtype=SPHERE_DTYPE)
+    sp["center"] = rng.uniform(-400.0, 400.0, (n, 3)).astype(np.float32)
+    sp["radius"] = rng.uniform(0.2, 2.0, n).astype(np.float32)
+    mt = np.zeros(1, dtype=MATERIAL_DTYPE)
+    k = 8192
+    tgt = np.where(rng.random(k) < 0.5, rng.integers(n - 4096, n, k), rng.integers(0, n, k))
+    o = rng.uniform(-500.0, 500.0, (k, 3)).astype(np.float32)
+    aim = sp["center"][tgt] + rng.normal(0.0, 1.0, (k, 3)) * sp["radius"][tgt, None]
+    d = (aim - o).astype(np.float32)
+    rays = np.ascontiguousarray(np.hstack([o, d]), dtype=np.float32)
+    renderer.set_scene(sp, mt)
+    gi, gt = renderer.intersect(rays)
+    ci, ct = O.intersect_batch(sp, rays)
+    bad = np.nonzero((gi != ci) | (gt.view(np.uint32) != ct.view(np.uint32)))[0]
+    assert bad.size == 0, f"{bad.size} rays differ, e.g. {bad[:5].tolist()}"
+    assert (ci >= n - 4096).sum() > 600 and (ci >= 0).mean() > 0.5

@@ -1,0 +1,15 @@
+# round-3 GPU call 18: PMC counters of the full frame's and of an N=8
+# shard's render kernel (tools/shard_pmc.py), two passes.
+set -uo pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+mkdir -p "$R/gpurun_out"
+cd /tmp && export TMPDIR=/tmp
+i=0
+for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_INSTS_VALU_MFMA_F16" \
+           "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE"; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $grp -d "$R/gpurun_out/spmc_$i" -o run --output-format csv -- python3 "$R/tools/shard_pmc.py" 8 \
+      > "$R/gpurun_out/spmc_$i.log" 2>&1
+  rc=$?; echo "pass $i rc=$rc"
+  if [ $rc -ne 0 ]; then exit $rc; fi
+done
