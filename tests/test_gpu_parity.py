@@ -375,7 +375,9 @@ def test_full_1080p64_properties(renderer):
     check_exact(a, b)
     c, _ = renderer.render(cam, 1920, 1080, 64, 16)
     check_exact(a, c)
-    rows = [0, 1, 415, 540, 544, 558, 777, 1079]
+    # 64 rows spread over the frame plus the rows of the NaN paths below
+    rows = sorted(set(np.linspace(0, 1079, 64).round().astype(int).tolist()) |
+                  {1, 415, 540, 544, 558, 777})
     ref, _ = O.render_rows(cam, sp, mt, 1920, 1080, 64, 16, rows)
     check_exact(a[rows], ref)
     nan_px = np.isnan(a[..., 0])
@@ -388,7 +390,7 @@ def test_4k_sampled_rows(renderer):
     cam = default_camera_block()
     renderer.set_scene(sp, mt)
     img, st = renderer.render(cam, 3840, 2160, 256, 32)
-    rows = [3, 1500]
+    rows = np.linspace(3, 2157, 24).round().astype(int).tolist()  # 24 rows spread over the frame
     ref, _ = O.render_rows(cam, sp, mt, 3840, 2160, 256, 32, rows)
     check_exact(img[rows], ref)
 
