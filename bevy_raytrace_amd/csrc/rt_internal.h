@@ -19,6 +19,9 @@
 #define RT_CNT_WORK_OFFSET 36
 #define RT_TAIL_ITEM 0x80000000u  // PathState::item flag: a tail item (per-sample slots)
 #define RT_GROUP 8            // spheres per filter group (SoA, 128 B)
+#ifndef RT_SLOT_BUF_CAP
+#define RT_SLOT_BUF_CAP 32    // slot-store buffer entries per wave (rt_kernels.hip)
+#endif
 #ifndef RT_CQ_CAP
 #define RT_CQ_CAP 8           // candidate-queue entries per lane (LDS)
 #endif

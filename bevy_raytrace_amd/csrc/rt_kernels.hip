@@ -137,6 +137,26 @@ __device__ __forceinline__ void render_body(
 #endif
     __shared__ LaneLds s_lane[RT_BLOCK_THREADS];  // per-lane item state (rt_dev_path.h)
     const ItemLds lds = s_lane + wave * 64u + lane;
+#ifndef RT_NO_SLOT_BUF
+    // Slot-store buffer: a finished block / item / tail sample goes to the
+    // wave's LDS buffer, and the wave writes the buffer out with one store
+    // when it would overflow (and at the end). A vector store holds vmcnt
+    // until the memory acknowledges it, so a store issued on its own makes the
+    // wave's next wait on a load (table entry, A fragments) wait for the
+    // store too: one such wait per RT_SLOT_BUF_CAP slots instead of one per
+    // iteration that stores. sbn: entries held (wave-uniform).
+    __shared__ float4 s_sbv[(RT_BLOCK_THREADS / 64) * RT_SLOT_BUF_CAP];
+    __shared__ uint32_t s_sbs[(RT_BLOCK_THREADS / 64) * RT_SLOT_BUF_CAP];
+    float4* const sbv = s_sbv + wave * RT_SLOT_BUF_CAP;
+    uint32_t* const sbs = s_sbs + wave * RT_SLOT_BUF_CAP;
+    uint32_t sbn = 0;
+    auto sb_flush = [&]() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane < sbn) block_sums[sbs[lane]] = sbv[lane];
+        sbn = 0;
+    };
+#endif
 #ifdef RT_SPHERES_LDS
     // Experiment variant: the filter reads the sphere groups from LDS (staged
     // once per workgroup) instead of the scalar cache.
@@ -311,6 +331,11 @@ __device__ __forceinline__ void render_body(
         // ---- shade; a finished path starts the next sample, whose primary hit
         // is reused (result-identical) so the lane goes on to its bounce-1 ray.
         bool shading = has_item;
+#ifndef RT_NO_SLOT_BUF
+        bool spend = false;  // this round finished a slot: sslot <- sval
+        uint32_t sslot = 0;
+        float4 sval;
+#endif
         PROF_MARK(12);  // bookkeeping between the drain and the shading loop
         // uniform loop (the segment count is a wave total): one round per
         // path step, lanes without a step to shade idle through the round
@@ -326,12 +351,18 @@ __device__ __forceinline__ void render_body(
                     // a tail item stores every sample's colour for the collect
                     if (st.item & RT_TAIL_ITEM) {
                         const v3 c = add(mk(0.0f, 0.0f, 0.0f), st.color);
+                        const uint32_t slot =
+                            P.main_all + (st.s - P.sample_base - P.g0) * P.npix + (st.item & ~RT_TAIL_ITEM);
+#ifndef RT_NO_SLOT_BUF
+                        spend = true;
+                        sslot = slot;
+                        sval = make_float4(c.x, c.y, c.z, 0.0f);
+#else
 #ifdef RT_DIAG_NO_BSTORE  // timing diagnostic only: no slot stores (wrong image)
                         if (c.x == -1234.5f)
 #endif
-                        block_sums[P.main_all +
-                                   (st.s - P.sample_base - P.g0) * P.npix + (st.item & ~RT_TAIL_ITEM)] =
-                            make_float4(c.x, c.y, c.z, 0.0f);
+                        block_sums[slot] = make_float4(c.x, c.y, c.z, 0.0f);
+#endif
                     } else {
                         st.bsum = add(st.bsum, st.color);
                     }
@@ -351,10 +382,16 @@ __device__ __forceinline__ void render_body(
                             st.s_end = min(st.s + RT_SAMPLE_BLOCK, iend);
                             next = true;
                         } else {
+#ifndef RT_NO_SLOT_BUF
+                            spend = true;
+                            sslot = st.item;
+                            sval = make_float4(acc.x, acc.y, acc.z, 0.0f);
+#else
 #ifdef RT_DIAG_NO_BSTORE
                             if (acc.x == -1234.5f)
 #endif
                             block_sums[st.item] = make_float4(acc.x, acc.y, acc.z, 0.0f);
+#endif
                         }
                     }
                     if (next) {
@@ -370,9 +407,32 @@ __device__ __forceinline__ void render_body(
                     }
                 }
             }
+#ifndef RT_NO_SLOT_BUF
+            // this round's finished slots into the buffer (a burst larger
+            // than the buffer goes straight out)
+            const uint64_t sm = rt_ballot(spend);
+            if (sm != 0) {
+                const uint32_t n = (uint32_t)__popcll(sm);
+                if (sbn + n > RT_SLOT_BUF_CAP) sb_flush();
+                if (n > RT_SLOT_BUF_CAP) {
+                    if (spend) block_sums[sslot] = sval;
+                } else {
+                    if (spend) {
+                        const uint32_t r = sbn + lanemask_lt_count(sm);
+                        sbv[r] = sval;
+                        sbs[r] = sslot;
+                    }
+                    sbn = __builtin_amdgcn_readfirstlane(sbn + n);
+                }
+                spend = false;
+            }
+#endif
         }
         PROF_MARK(3);
     }
+#ifndef RT_NO_SLOT_BUF
+    sb_flush();
+#endif
 
 #ifdef RT_PROFILE
     PROF_MARK(7);
