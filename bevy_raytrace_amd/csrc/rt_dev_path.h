@@ -16,7 +16,7 @@ struct PathState {
 };
 
 // Per-lane item state that changes at most once per sample, kept in LDS (no
-// VGPRs at the 80-register occupancy limit), one record per lane so a single
+// VGPRs: the kernel sits at its occupancy's register limit), one record per lane so a single
 // VGPR address (+ immediate offsets) reaches every field: the pixel's primary
 // direction, the item's running fold of its block sums (xyz; w != 0 once a
 // block was folded), the primary hit (reuse mode) and the end of its samples.
