@@ -1,0 +1,5 @@
+# round-3 GPU call 28: the shipped tree -- smoke and the GPU suite.
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_final.log 2>&1 || exit 281
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_final.log 2>&1 || exit 282
