@@ -479,6 +479,12 @@ def main():
         torch.cuda.synchronize()
         if dist_on:
             dist.barrier()
+        if use_ipc and rank == 0:
+            # every rank's rows are in rank 0's image (system-scope stores +
+            # release, each rank's launch complete before the barrier): the
+            # acquire makes them visible to what rank 0 runs next
+            r.acquire(stream.cuda_stream)
+            torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         if dist_on:
             t = torch.tensor([dt], dtype=torch.float64, device=red_dev)

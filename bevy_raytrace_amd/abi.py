@@ -139,6 +139,7 @@ _PROTOS = {
                                              ctypes.POINTER(ctypes.c_uint64)]),
     "rt_encode_srgb8": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint64, _VP]),
     "rt_update_materials": (ctypes.c_int, [_VP, _U32, _VP, _U32]),
+    "rt_acquire": (ctypes.c_int, [_VP, _VP]),
     "rt_last_error": (ctypes.c_char_p, [_VP]),
 }
 

@@ -1069,6 +1069,11 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     }
     K_.scene_fast = ctx->scene_fast && tn.fast_exact ? 1u : 0u;
     K_.flags = p.flags;
+    // the buffers' sizes (RT_CHECK_BOUNDS builds check every index against them)
+    K_.chk_nsph = (uint32_t)((cull ? ctx->sph_c_cap : ctx->sph_cap) / sizeof(float4));
+    K_.chk_nrm = (uint32_t)((cull ? ctx->rm_c_cap : ctx->sph_rm_cap) / sizeof(float2));
+    K_.chk_nmat = ctx->m;
+    K_.chk_slots = f.bs_cap / sizeof(float4);
 #ifdef RT_MFMA_FILTER
     if (!cull && ctx->mf_ok && !(p.flags & RT_FLAG_VALU_FILTER)) {
         K_.mfA = ctx->d_mfA;
@@ -1179,6 +1184,8 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         const uint32_t grid = (uint32_t)(need_blocks < grid_full ? need_blocks : grid_full);
         const uint64_t tail_items = 2ull * RT_WAVE_CHUNK * grid * (RT_BLOCK_THREADS / 64);
         K_.tail_start = (uint32_t)(items > tail_items ? items - tail_items : 0);
+        K_.chk_items = (uint32_t)items;
+        K_.chk_out = (uint64_t)ps.nframes * fstride;
         HIP_TRY_Q(hipEventRecord(f.ev[2 * i], stream));
         HIP_TRY_Q(rt_launch_render(&K_, cull ? ctx->d_grp_c : ctx->d_grp,
                                       cull ? ctx->d_sph_c : ctx->d_sph,
@@ -1203,10 +1210,32 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     return RT_OK;
 }
 
+// Checked build (RT_CHECK_BOUNDS): the kernels' out-of-range index record
+// since the last call (rt_kernels.hip RT_IDX), reset; a violation fails the
+// call. The product library checks nothing here.
+static int check_bounds(rt_ctx* ctx, const char* who) {
+#ifdef RT_CHECK_BOUNDS
+    unsigned int v[4] = {};
+    if (rt_check_bounds_take(v) != 0) return fail(ctx, RT_ERR_DEVICE, "%s: bounds record unreadable", who);
+    if (v[0])
+        return fail(ctx, RT_ERR_DEVICE,
+                    "%s: %u out-of-range index(es); first at site %u: index %u, bound %u", who, v[0],
+                    v[1], v[2], v[3]);
+#else
+    (void)ctx;
+    (void)who;
+#endif
+    return RT_OK;
+}
+
 // f.ev_t1 has been recorded after the frame's last operation.
 static int finish(rt_ctx* ctx, Frame& f, rt_stats* st) {
     HIP_TRY(ctx, hipEventSynchronize(f.ev_t1));
     f.pending_stream = nullptr;
+    {
+        int rc = check_bounds(ctx, "render");
+        if (rc) return rc;
+    }
     for (int i = 0; i < 16; ++i) ctx->dbg[i] = f.h_segs[2 + i];
     if (!st) return RT_OK;
     std::memset(st, 0, sizeof(*st));
@@ -1398,6 +1427,8 @@ int rt_render_progressive(rt_ctx* ctx, const rt_camera* camera, const rt_params*
         HIP_TRY(ctx, hipMemcpyAsync(out_rgba, f.d_out, bytes, hipMemcpyDeviceToHost, f.stream));
     HIP_TRY(ctx, hipEventRecord(f.ev_t1, f.stream));
     HIP_TRY(ctx, hipEventSynchronize(f.ev_t1));
+    rc = check_bounds(ctx, "rt_render_progressive");
+    if (rc) return rc;
     ctx->prog_total = total;
     ctx->prog_key = key;
     if (total_spp) *total_spp = total;
@@ -1414,6 +1445,16 @@ int rt_encode_srgb8(rt_ctx* ctx, const float* rgba_device, uint8_t* rgba8_device
     hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
     HIP_TRY(ctx, rt_launch_srgb8(reinterpret_cast<const float4*>(rgba_device),
                                  reinterpret_cast<uchar4*>(rgba8_device), npix, s));
+    if (!stream) HIP_TRY(ctx, hipStreamSynchronize(s));
+    return RT_OK;
+}
+
+int rt_acquire(rt_ctx* ctx, void* stream) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_acquire: ctx is NULL");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    // a few waves per CU: every CU (and so every XCD's L2) runs the fence
+    HIP_TRY(ctx, rt_launch_acquire((uint32_t)std::max(ctx->cu_count, 1) * 8u, s));
     if (!stream) HIP_TRY(ctx, hipStreamSynchronize(s));
     return RT_OK;
 }
@@ -1506,7 +1547,7 @@ int rt_intersect_ex(rt_ctx* ctx, const float* rays, uint32_t n, uint32_t flags, 
     hipFree(buf);
     if (e != hipSuccess)
         return fail(ctx, RT_ERR_DEVICE, "rt_intersect: %s", hipGetErrorString(e));
-    return RT_OK;
+    return check_bounds(ctx, "rt_intersect");
 }
 
 // Internal (not in include/rt_hip.h; tests/test_cull.py, CPU): the culled

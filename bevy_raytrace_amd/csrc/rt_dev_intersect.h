@@ -312,18 +312,20 @@ __device__ __forceinline__ uint32_t cand_mask8(f2 g01, f2 g23, f2 g45, f2 g67, f
 
 template <bool FAST, bool CULL>
 __device__ __forceinline__ void drain_list(const uint32_t* cq, uint32_t cnt,
-                                           const float4* __restrict__ sph, v3 o, v3 d, float a,
+                                           const float4* __restrict__ sph, uint32_t nsph, v3 o,
+                                           v3 d, float a,
                                            float ya, float& best_t, int& best_i,
                                            const uint32_t* perm EXACT_ARGS) {
     const uint32_t lane = __lane_id();
     for (uint32_t k = 0; k < cnt; ++k) {
-        const uint32_t e = cq[k * 64 + lane];
+        const uint32_t e = cq[RT_IDX(k, RT_CQ_CAP, RT_SITE_CQ) * 64 + lane];
         uint32_t m = e & 0xFFu;
         const uint32_t base = (e >> 8) * RT_GROUP;
         while (m) {
             const uint32_t j = __builtin_ctz(m);
             m &= m - 1;
-            exact_body<FAST, CULL>(sph[base + j], (int)(base + j), o, d, a, ya, best_t, best_i,
+            exact_body<FAST, CULL>(sph[RT_IDX(base + j, nsph, RT_SITE_CQ_SPH)], (int)(base + j), o, d,
+                                   a, ya, best_t, best_i,
                                    perm EXACT_PASS);
         }
     }
@@ -333,14 +335,15 @@ __device__ __forceinline__ void drain_list(const uint32_t* cq, uint32_t cnt,
 // Queue entries are (group << 8 | 8-bit candidate mask), one column per lane.
 template <bool CULL>
 __device__ __forceinline__ void drain_candidates(const uint32_t* cq, uint32_t cnt,
-                                                 const float4* __restrict__ sph, v3 o, v3 d,
+                                                 const float4* __restrict__ sph, uint32_t nsph,
+                                                 v3 o, v3 d,
                                                  float a, bool fast, float& best_t,
                                                  int& best_i, const uint32_t* perm EXACT_ARGS) {
     if (fast)
-        drain_list<true, CULL>(cq, cnt, sph, o, d, a, rt_recip_rn(a), best_t, best_i,
+        drain_list<true, CULL>(cq, cnt, sph, nsph, o, d, a, rt_recip_rn(a), best_t, best_i,
                                perm EXACT_PASS);
     else
-        drain_list<false, CULL>(cq, cnt, sph, o, d, a, a, best_t, best_i, perm EXACT_PASS);
+        drain_list<false, CULL>(cq, cnt, sph, nsph, o, d, a, a, best_t, best_i, perm EXACT_PASS);
 }
 
 // Closest hit over the whole list (intersect.wgsl:133-143).
@@ -434,7 +437,8 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
             PROF_ADD(5, 1);
             if (rt_ballot(cnt >= RT_CQ_CAP) != 0) {  // a lane's queue is full: drain all
                 PROF_ADD(11, 1);
-                drain_candidates<CULL>(cq, cnt, sph, o, d, a, fast, best_t, best_i, perm EXACT_PASS);
+                drain_candidates<CULL>(cq, cnt, sph, ngroups * RT_GROUP, o, d, a, fast, best_t, best_i,
+                                       perm EXACT_PASS);
                 cnt = 0;
             }
             const float T = RT_T;
@@ -446,7 +450,7 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
                                (ge(g67.x, T) << 6) | (ge(g67.y, T) << 7);
 #endif
             if (m) {
-                cq[cnt * 64 + lane] = (g << 8) | m;
+                cq[RT_IDX(cnt, RT_CQ_CAP, RT_SITE_CQ) * 64 + lane] = (g << 8) | m;
                 ++cnt;
             }
         }
@@ -525,7 +529,8 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
     }
 #endif
 #endif
-    drain_candidates<CULL>(cq, cnt, sph, o, d, a, fast, best_t, best_i, perm EXACT_PASS);
+    drain_candidates<CULL>(cq, cnt, sph, ngroups * RT_GROUP, o, d, a, fast, best_t, best_i,
+                           perm EXACT_PASS);
     PROF_MARK(2);
 #ifdef RT_PROFILE
     PROF_ADD(13, wave_max_u32(ecnt[0]));
@@ -590,9 +595,10 @@ __device__ __forceinline__ void intersect_wide(const float4* __restrict__ sph, u
         for (uint32_t i = lane; i < n; i += 64) {
 #ifdef RT_PROFILE
             uint32_t ecnt[2];
-            exact_test<CULL>(sph[i], (int)i, ro, rd, a, ya, fast, bt, bi, perm, ecnt);
+            exact_test<CULL>(sph[RT_IDX(i, n, RT_SITE_WIDE_SPH)], (int)i, ro, rd, a, ya, fast, bt, bi, perm,
+                             ecnt);
 #else
-            exact_test<CULL>(sph[i], (int)i, ro, rd, a, ya, fast, bt, bi, perm);
+            exact_test<CULL>(sph[RT_IDX(i, n, RT_SITE_WIDE_SPH)], (int)i, ro, rd, a, ya, fast, bt, bi, perm);
 #endif
         }
         for (int off = 32; off > 0; off >>= 1) {
@@ -719,7 +725,8 @@ __device__ __forceinline__ bool mfma_wave_ok(v3 o, bool live) {
 #endif
 template <bool FAST>
 __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, uint32_t cnt1,
-                                           const float4* __restrict__ sph, v3 o, v3 d, float a,
+                                           const float4* __restrict__ sph, uint32_t nsph, v3 o,
+                                           v3 d, float a,
                                            float ya, float& best_t, int& best_i MF_ECNT) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     const uint32_t lane = __lane_id();
@@ -748,7 +755,8 @@ __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, ui
     while (m != 0 || i < total) {
         if (m == 0) {
             const bool s1 = i >= na;
-            const uint32_t e = q[(s1 ? i - na : i) * 64u + (s1 ? j + 32u : j)];
+            const uint32_t e =
+                q[RT_IDX(s1 ? i - na : i, RT_MF_CAP, RT_SITE_MFQ_READ) * 64u + (s1 ? j + 32u : j)];
             m = e & RT_MF_FLAGS;
             // group index 8b + 2q (mf_unspread), + h: the column's lane
             // j (h = 0) or j + 32 (h = 1) queued it
@@ -758,7 +766,8 @@ __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, ui
         const uint32_t b = __builtin_ctz(m) >> 3;
         m &= m - 1;
         MF_ECNT_INC;
-        exact_body<FAST, false, true>(sph[base + b], (int)(base + b), o, d, a, ya, best_t, best_i,
+        exact_body<FAST, false, true>(sph[RT_IDX(base + b, nsph, RT_SITE_MF_SPH)], (int)(base + b), o,
+                                      d, a, ya, best_t, best_i,
                                       nullptr EXACT_PASS);
     }
 }
@@ -927,9 +936,9 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
             const uint32_t cnt0 = qcount(qp0, q0), cnt1 = qcount(qp1, q1);
             PROF_ADD(11, 1);  // queue flushes
             if (fast)
-                mfma_drain<true>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
+                mfma_drain<true>(cq, cnt0, cnt1, sph, nblk * 32u, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
             else
-                mfma_drain<false>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
+                mfma_drain<false>(cq, cnt0, cnt1, sph, nblk * 32u, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
             qp0 = q0;
             qp1 = q1;
             ub0 = ub1 = 0;
@@ -964,6 +973,10 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
                     // term: the pad rows' S' = -inf meets the ray's -1).
                     // b * 8 has its low 3 bits clear: spread(8b + 2q) = spread(8b) + 2q
                     const uint32_t f = m & RT_MF_FLAGS;
+#ifdef RT_CHECK_BOUNDS
+                    RT_IDX(qcount(qp, t ? q1 : q0), RT_MF_CAP, RT_SITE_MFQ);
+                    if (qcount(qp, t ? q1 : q0) >= RT_MF_CAP) qp = t ? q1 : q0;
+#endif
                     *qp = f | (sb + q * 2u);
                     // one more entry iff a flag is set: min(f, 1) as one VALU
                     // min (the compiler otherwise emits a compare and a select)
@@ -992,9 +1005,9 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
     PROF_MARK(1);
     const uint32_t cnt0 = qcount(qp0, q0), cnt1 = qcount(qp1, q1);
     if (fast)
-        mfma_drain<true>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
+        mfma_drain<true>(cq, cnt0, cnt1, sph, nblk * 32u, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
     else
-        mfma_drain<false>(cq, cnt0, cnt1, sph, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
+        mfma_drain<false>(cq, cnt0, cnt1, sph, nblk * 32u, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
     PROF_MARK(2);
 #ifdef RT_PROFILE
     {

@@ -123,6 +123,7 @@ __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint
     // load from the kernarg segment on every item start).
     const uint32_t npix = P.npix, main_all = P.main_all, sample_base = P.sample_base;
     uint32_t k, s0, s1;  // pixel in processing order; the (first block's) samples [s0, s1)
+    item = RT_IDX(item, P.chk_items, RT_SITE_ITEM);
     uint32_t slot = item;  // a main item's output slot
     if (item < main_all) {
         const uint32_t main_pix = P.main_pix, nblocks = P.nblocks, qpix = P.qpix;
@@ -144,7 +145,7 @@ __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint
             // budget) continues the fold of the earlier passes (rt_collect_kernel
             // left it in acc_in): ((acc + b0) + b1) ..., the single-pass order
             if (block_begin) {
-                a0 = P.acc_in[order_to_pixel(P, k)];
+                a0 = P.acc_in[RT_IDX(order_to_pixel(P, k), npix, RT_SITE_ACC_IN)];
                 a0.w = 1.0f;
             }
         } else {
@@ -189,7 +190,7 @@ __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint
         s0 = sample_base + gb + g * z;
         s1 = sample_base + min(gb + g * z + z, ge);
     }
-    const float4 q4 = tab[k].d;
+    const float4 q4 = tab[RT_IDX(k, npix, RT_SITE_TAB)].d;
     // main item: its output slot; tail item: RT_TAIL_ITEM | k
     st.item = item < P.main_all ? slot : (RT_TAIL_ITEM | k);
     st.pix = __float_as_uint(q4.w);
@@ -227,8 +228,8 @@ __device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, f
     float fuzz, ior;
     int refl = -1;
     if (!miss) {
-        const float4 s = sph[hi];
-        const float2 rm = sph_rm[hi];
+        const float4 s = sph[RT_IDX(hi, P.chk_nsph, RT_SITE_SPH)];
+        const float2 rm = sph_rm[RT_IDX(hi, P.chk_nrm, RT_SITE_RM)];
         const float radius = rm.x;
         const uint32_t mi = __float_as_uint(rm.y);
         pos = add(st.o, scale(st.d, t));
@@ -239,7 +240,7 @@ __device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, f
             nrm = neg(nrm);
             front = false;
         }
-        const rt_material& m = mats[mi];
+        const rt_material& m = mats[RT_IDX(mi, P.chk_nmat, RT_SITE_MAT)];
         refl = m.reflectance;
         mc = *reinterpret_cast<const float4*>(m.color);
         fuzz = m.fuzziness;
@@ -353,7 +354,8 @@ __device__ __forceinline__ float4* out_pixel(const KParams& P, float4* out, uint
     if (P.flags & RT_FLAG_IMAGE_OUT) {
         uint32_t x, y;
         pixel_xy(P, p, x, y);
-        return out + (size_t)f * P.width * P.height + (size_t)y * P.width + x;
+        return out + RT_IDX((size_t)f * P.width * P.height + (size_t)y * P.width + x, P.chk_out,
+                            RT_SITE_OUT);
     }
-    return out + (size_t)f * P.npix + p;
+    return out + RT_IDX((size_t)f * P.npix + p, P.chk_out, RT_SITE_OUT);
 }

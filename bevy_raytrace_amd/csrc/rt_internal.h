@@ -116,6 +116,15 @@ struct KParams {
     // by the sample groups per pixel of the tail regions: (g1 - g0 + 3) / 4,
     // (g2 - g1 + 1) / 2, g_end - g2 (4-, 2-, 1-sample items)
     FastDiv div_ng4, div_ng2, div_ng1;
+    // Sizes of the buffers the kernels index, in records: the bounds the
+    // RT_CHECK_BOUNDS build checks every computed index against (rt_kernels.hip
+    // RT_IDX; the product build reads none of them).
+    uint32_t chk_nsph;   // sph / grp records (padded list)
+    uint32_t chk_nrm;    // sph_rm records
+    uint32_t chk_nmat;   // materials
+    uint32_t chk_items;  // work items of the launch (main_all + tail_items)
+    uint64_t chk_slots;  // block_sums slots
+    uint64_t chk_out;    // float4 pixels behind the launch's output pointer
 };
 
 // Row block b of the image -> owning shard (rt_params: serpentine deal).
@@ -138,6 +147,7 @@ hipError_t rt_launch_collect(const KParams* P, const float4* block_sums,
                              float4* acc, int first_pass, int last_pass, float spp, float4* out,
                              float4* prog, int prog_mode, float prog_total, hipStream_t stream);
 hipError_t rt_launch_srgb8(const float4* in, uchar4* out, uint64_t npix, hipStream_t stream);
+hipError_t rt_launch_acquire(uint32_t blocks, hipStream_t stream);
 hipError_t rt_launch_assemble(const float4* gathered, uint32_t max_rows, uint32_t frames,
                               float4* image, uint32_t width, uint32_t height, uint32_t row_block,
                               uint32_t shard_count, hipStream_t stream);
@@ -148,4 +158,7 @@ hipError_t rt_launch_intersect(const float4* grp, const float4* sph, uint32_t ng
                                hipStream_t stream);
 hipError_t rt_render_occupancy(int* blocks_per_cu, int* blocks_per_cu_cull);
 hipError_t rt_launch_primary(const KParams* P, float4* pd, hipStream_t stream);
+#ifdef RT_CHECK_BOUNDS
+int rt_check_bounds_take(unsigned int out[4]);  // checked build: read and reset the record
+#endif
 }

@@ -68,6 +68,56 @@ __device__ __forceinline__ float rt_cold(float x) {
 #define VERY_FAR 1e20f
 #define EPSILON 0.001f
 
+// ---- checked build (make checked: -DRT_CHECK_BOUNDS, librt_hip_checked.so;
+// never the product library). Every computed index into a buffer or an LDS
+// array goes through RT_IDX(i, n, site): out of range, the first violation's
+// (site, index, bound) is recorded in g_rt_check, the count incremented, and
+// index 0 used instead, so the launch completes and the host reports it
+// (rt_api.cpp check_bounds fails the call with RT_ERR_DEVICE) instead of the
+// GPU faulting. Sites: enum RtSite below.
+enum RtSite : uint32_t {
+    RT_SITE_ITEM = 1,        // work item index < items of the launch (start_item)
+    RT_SITE_TAB = 2,         // pixel table tab[k], k < npix
+    RT_SITE_ACC_IN = 3,      // acc_in[p] of a later pass, p < npix
+    RT_SITE_SPH = 4,         // sph[hi] in shade
+    RT_SITE_RM = 5,          // sph_rm[hi] in shade
+    RT_SITE_MAT = 6,         // mats[mi] in shade
+    RT_SITE_SLOT = 7,        // block_sums slot written by the render kernel
+    RT_SITE_SLOTBUF = 8,     // per-wave slot buffer entry
+    RT_SITE_MFQ = 9,         // matrix-core queue append (entries per lane and half)
+    RT_SITE_MFQ_READ = 10,   // matrix-core drain: queue entry read
+    RT_SITE_MF_SPH = 11,     // matrix-core drain: candidate sphere record
+    RT_SITE_CQ = 12,         // VALU-walk queue append
+    RT_SITE_CQ_SPH = 13,     // VALU-walk drain: candidate sphere record
+    RT_SITE_CACHE = 14,      // primary-hit cache: hi in [-1, nsph)
+    RT_SITE_COLLECT = 15,    // collect: slot read
+    RT_SITE_OUT = 16,        // collect: output pixel
+    RT_SITE_WIDE_SPH = 17,   // sphere-parallel walk: sph[i]
+    RT_SITE_PERM = 18,       // culled list: perm[idx]
+    RT_SITE_MFA = 19,        // matrix-core walk: A-fragment block
+};
+#ifdef RT_CHECK_BOUNDS
+__device__ unsigned int g_rt_check[4];  // violations, first (site, index, bound)
+__device__ __noinline__ void rt_check_fail(uint32_t site, uint64_t i, uint64_t n) {
+    if (atomicAdd(&g_rt_check[0], 1u) == 0u) {
+        g_rt_check[1] = site;
+        g_rt_check[2] = (unsigned int)min(i, (uint64_t)0xFFFFFFFFu);
+        g_rt_check[3] = (unsigned int)min(n, (uint64_t)0xFFFFFFFFu);
+    }
+}
+template <typename I>
+__device__ __forceinline__ I rt_idx(I i, uint64_t n, uint32_t site) {
+    if ((uint64_t)i >= n) {
+        rt_check_fail(site, (uint64_t)i, n);
+        return (I)0;
+    }
+    return i;
+}
+#define RT_IDX(i, n, site) rt_idx((i), (uint64_t)(n), (site))
+#else
+#define RT_IDX(i, n, site) (i)
+#endif
+
 #include "rt_dev_math.h"
 #include "rt_dev_intersect.h"
 #include "rt_dev_path.h"
@@ -153,7 +203,7 @@ __device__ __forceinline__ void render_body(
     auto sb_flush = [&]() {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (lane < sbn) block_sums[sbs[lane]] = sbv[lane];
+        if (lane < sbn) block_sums[RT_IDX(sbs[lane], P.chk_slots, RT_SITE_SLOT)] = sbv[lane];
         sbn = 0;
     };
 #endif
@@ -398,7 +448,8 @@ __device__ __forceinline__ void render_body(
                         start_sample(P, st, lds);
                         if (use_cache) {
                             const float2 c = lds->cache;
-                            hi = __float_as_int(c.x);
+                            hi = (int)RT_IDX((uint32_t)(__float_as_int(c.x) + 1), P.chk_nsph + 1u,
+                                             RT_SITE_CACHE) - 1;
                             t = c.y;
                             shading = true;
                         }
@@ -415,12 +466,12 @@ __device__ __forceinline__ void render_body(
                 const uint32_t n = (uint32_t)__popcll(sm);
                 if (sbn + n > RT_SLOT_BUF_CAP) sb_flush();
                 if (n > RT_SLOT_BUF_CAP) {
-                    if (spend) block_sums[sslot] = sval;
+                    if (spend) block_sums[RT_IDX(sslot, P.chk_slots, RT_SITE_SLOT)] = sval;
                 } else {
                     if (spend) {
                         const uint32_t r = sbn + lanemask_lt_count(sm);
-                        sbv[r] = sval;
-                        sbs[r] = sslot;
+                        sbv[RT_IDX(r, RT_SLOT_BUF_CAP, RT_SITE_SLOTBUF)] = sval;
+                        sbs[RT_IDX(r, RT_SLOT_BUF_CAP, RT_SITE_SLOTBUF)] = sslot;
                     }
                     sbn = __builtin_amdgcn_readfirstlane(sbn + n);
                 }
@@ -605,6 +656,16 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_mfma_kernel(
 }
 #endif
 
+// A 16-B store at system scope, write-through (global_store_dwordx4 ... sc0
+// sc1: the AMDGPU memory model's system-scope store; a vector store). Used for
+// rows that may belong to another device's image (RT_FLAG_IMAGE_OUT). hipcc
+// does not count an asm store in its waits: the caller waits (vmcnt(0)).
+__device__ __forceinline__ void store_system(float4* p, float4 v) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v x = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(p), "v"(x) : "memory");
+}
+
 // Fold one frame's results into acc (block order) and, on the frame's last
 // pass, write out = acc / spp with alpha 1 (collect.wgsl:115-125). One thread
 // per pixel of the processing order k (-> image pixel p = order_to_pixel).
@@ -626,26 +687,51 @@ __global__ void rt_collect_kernel(KParams P, const float4* __restrict__ block_su
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= P.npix) return;
     const uint32_t f = blockIdx.y;
-    const uint32_t p = order_to_pixel(P, k);
+    const uint32_t p = RT_IDX(order_to_pixel(P, k), P.npix, RT_SITE_OUT);
     float ax = 0.0f, ay = 0.0f, az = 0.0f;
     bool have = !first_pass;
     if (have) {
         const float4 v = acc[p];
         ax = v.x; ay = v.y; az = v.z;
     }
-    fold_frame(P, f, k, have, ax, ay, az, [&](size_t slot) { return block_sums[slot]; });
+    fold_frame(P, f, k, have, ax, ay, az,
+               [&](size_t slot) { return block_sums[RT_IDX(slot, P.chk_slots, RT_SITE_COLLECT)]; });
     if (!last_pass) {
         acc[p] = make_float4(ax, ay, az, 0.0f);
     } else if (prog_mode == 0) {
-        *out_pixel(P, out, f, p) = make_float4(ax / spp, ay / spp, az / spp, 1.0f);
+        const float4 v = make_float4(ax / spp, ay / spp, az / spp, 1.0f);
+        float4* const o = out_pixel(P, out, f, p);
+        if (P.flags & RT_FLAG_IMAGE_OUT)
+            store_system(o, v);  // possibly another device's image (xGMI): write-through
+        else
+            *o = v;
     } else {
         if (prog_mode == 2) {
             const float4 v = prog[p];
             ax = v.x + ax; ay = v.y + ay; az = v.z + az;
         }
         prog[p] = make_float4(ax, ay, az, 0.0f);
-        out[(size_t)f * P.npix + p] = make_float4(ax / prog_total, ay / prog_total, az / prog_total, 1.0f);
+        out[RT_IDX((size_t)f * P.npix + p, P.chk_out, RT_SITE_OUT)] = make_float4(ax / prog_total, ay / prog_total, az / prog_total, 1.0f);
     }
+    // RT_FLAG_IMAGE_OUT: the rows may live in another device's memory (rank
+    // 0's image mapped over HIP IPC, bevy_raytrace_amd/distributed.py). The
+    // wave's stores above are system-scope write-through; this system-scope
+    // release (buffer_wbl2 sc0 sc1 + the wait for every store of the wave) ends
+    // the wave's part of the hand-off; the reader acquires (rt_acquire) after
+    // the host has seen the launch complete (visibility).
+    if (P.flags & RT_FLAG_IMAGE_OUT) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the asm store is invisible to hipcc)
+    }
+}
+
+// System-scope acquire on every CU of the device (rt_acquire): invalidates
+// the vector L1 of the CU and the L2 lines the fence scope covers, so kernels
+// launched after it read what other devices wrote into this device's memory
+// (after the host observed those writers complete).
+__global__ void rt_acquire_kernel() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // Display encode: linear RGBA32F -> sRGB RGBA8 (IEC 61966-2-1 transfer curve),
@@ -719,6 +805,11 @@ hipError_t rt_launch_collect(const KParams* P, const float4* block_sums,
     hipLaunchKernelGGL(rt_collect_kernel, dim3((P->npix + T - 1) / T, P->nframes), dim3(T), 0, stream, *P,
                        block_sums, acc, first_pass, last_pass, spp, out, prog, prog_mode,
                        prog_total);
+    return hipGetLastError();
+}
+
+hipError_t rt_launch_acquire(uint32_t blocks, hipStream_t stream) {
+    hipLaunchKernelGGL(rt_acquire_kernel, dim3(blocks), dim3(64), 0, stream);
     return hipGetLastError();
 }
 
@@ -816,6 +907,15 @@ int rt_debug_math(int mode, const float* in_device, uint32_t n, float* out_devic
                        out_device);
     return hipDeviceSynchronize() == hipSuccess ? 0 : -3;
 }
+
+#ifdef RT_CHECK_BOUNDS
+int rt_check_bounds_take(unsigned int out[4]) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rt_check), 4 * sizeof(unsigned int)) != hipSuccess) return -1;
+    if (out[0] == 0) return 0;
+    const unsigned int zero[4] = {0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_rt_check), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // resident workgroups per CU of the brute-force and the culled kernel (their
 // register and LDS footprints differ: the matrix-core filter's tiles)

@@ -103,6 +103,13 @@ class Renderer:
                                       ctypes.c_void_p(int(stream)) if stream else None)
         check(self.lib, self.ctx, rc)
 
+    def acquire(self, stream=None):
+        """System-scope acquire on this device (rt_acquire): after other ranks
+        wrote their rows into this device's image (RT_FLAG_IMAGE_OUT) and the
+        host saw them complete, work enqueued after this on `stream` reads them."""
+        rc = self.lib.rt_acquire(self.ctx, ctypes.c_void_p(int(stream)) if stream else None)
+        check(self.lib, self.ctx, rc)
+
     def render_device(self, camera: np.ndarray, out_ptr: int, width, height, spp, max_depth,
                       frame0=0, row_block=8, shard_count=1, shard_index=0, flags=0, stream=None):
         """Enqueue a render into a device buffer (e.g. a torch tensor's data_ptr()).

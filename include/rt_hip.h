@@ -172,7 +172,11 @@ typedef struct rt_params {
  * instead of its rows packed. N row shards of one frame then write one image:
  * e.g. rank 0's buffer mapped into every rank (hipIpcOpenMemHandle), so the
  * row tiling needs no gather. The reference has no
- * counterpart (one device, ray_trace_node.rs:213-224). */
+ * counterpart (one device, ray_trace_node.rs:213-224). Visibility: the image
+ * rows are written with system-scope write-through stores and every writing
+ * wave ends with a system-scope release, so once the host has seen the call
+ * complete (rt_wait / a stream sync, then e.g. a process barrier) the device
+ * that owns the image reads them after rt_acquire(). */
 #define RT_FLAG_IMAGE_OUT 0x20u
 #define RT_JITTER_HASH_MUL 0x9E3779B1u
 #define RT_LENS_HASH_MUL   0x85EBCA77u
@@ -220,10 +224,12 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n,
  * the materials when their count changes, ray_trace_materials.rs:129-164).
  * Replace records [first, first+count) of the current scene; counts N and M
  * are unchanged. Only the touched sphere records and 8-sphere groups are
- * re-packed and uploaded; the matrix-core filter's f16 sphere rows are
- * rebuilt whole (their scale 2^-sq depends on every centre: O(N) on the host,
- * 64 B per sphere uploaded); the culled list (RT_FLAG_CULL), which depends on
- * every sphere, is rebuilt once, at the next culled call. */
+ * re-packed and uploaded. The matrix-core filter's f16 sphere rows (their
+ * scale 2^-sq depends on every centre: O(N) on the host, 64 B per sphere
+ * uploaded) are rebuilt once, at the next call that walks them (a caller that
+ * renders only the culled list never pays for them); the culled list
+ * (RT_FLAG_CULL), which depends on every sphere, likewise at the next culled
+ * call. */
 int rt_update_spheres(rt_ctx* ctx, uint32_t first, const rt_sphere* spheres, uint32_t count);
 int rt_update_materials(rt_ctx* ctx, uint32_t first, const rt_material* materials,
                         uint32_t count);
@@ -335,6 +341,14 @@ int rt_assemble_shard_frames(rt_ctx* ctx, const float* gathered_device, uint32_t
                              uint32_t frames, float* image_device, uint32_t width,
                              uint32_t height, uint32_t row_block, uint32_t shard_count,
                              void* stream);
+
+/* System-scope acquire on the ctx's device, enqueued on `stream` (NULL = ctx
+ * stream, synchronous): work enqueued after it on that stream reads what OTHER
+ * devices wrote into this device's memory (RT_FLAG_IMAGE_OUT rows of other
+ * ranks, written through a hipIpcOpenMemHandle mapping) once the host has
+ * seen those writers' calls complete. Row-tiled multi-GPU rendering only
+ * (DESIGN.md §7); the reference renders on one device. */
+int rt_acquire(rt_ctx* ctx, void* stream);
 
 /* Message for the last failing call on ctx (or on the library when ctx is NULL). */
 const char* rt_last_error(const rt_ctx* ctx);

@@ -8,8 +8,18 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+def pytest_addoption(parser):
+    parser.addoption("--rt-lib", default=None,
+                     help="run the in-process tests against another build of the C-ABI "
+                          "(e.g. bevy_raytrace_amd/librt_hip_checked.so, the bounds-checked build)")
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through librt_hip.so)")
+    lib = config.getoption("--rt-lib")
+    if lib:
+        from bevy_raytrace_amd import abi
+        abi.LIB_PATH = os.path.abspath(lib)
 
 
 @pytest.fixture(scope="session")

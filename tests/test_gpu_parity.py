@@ -297,6 +297,7 @@ def test_image_out_shards_fill_one_image(renderer, K, B):
             others = np.setdiff1d(np.arange(H), rows)
             assert (got[:, others] == -7.0).all()
             check_exact(got[:, rows], full.cpu().numpy()[:, rows])
+    renderer.acquire()  # the owner's system-scope acquire (rt_acquire), as rank 0 does
     check_exact(img.cpu().numpy(), full.cpu().numpy())
 
 

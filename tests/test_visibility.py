@@ -1,0 +1,67 @@
+"""The cross-device hand-off of RT_FLAG_IMAGE_OUT rows is in the shipped code
+(CPU: hipcc cross-compiles the device assembly of the library's sources with
+the library's flags, `make asm`).
+
+Protocol (visibility): a rank writing its rows into another
+device's image stores them with system-scope write-through stores and ends
+each writing wave with a system-scope release; the image's owner reads them
+after a system-scope acquire (rt_acquire), once the host has seen the writers
+complete."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "bevy_raytrace_amd", "csrc")
+
+pytestmark = pytest.mark.skipif(
+    shutil.which("make") is None or not os.path.exists("/opt/rocm/bin/hipcc"),
+    reason="needs hipcc")
+
+
+@pytest.fixture(scope="module")
+def asm(tmp_path_factory):
+    out = tmp_path_factory.mktemp("asm") / "rt.s"
+    subprocess.run(["make", "-s", "asm", f"ASM={out}"], cwd=CSRC, check=True,
+                   capture_output=True)
+    return out.read_text()
+
+
+def kernel_body(asm, name):
+    """Instructions of one kernel: from its label to its end marker."""
+    m = re.search(r"^" + re.escape(name) + r"[A-Za-z0-9_]*:", asm, re.M)
+    assert m, f"kernel {name} not in the assembly"
+    end = asm.find(".Lfunc_end", m.end())
+    lines = asm[m.end():end].split("\n")
+    return [ln.split(";")[0].strip() for ln in lines
+            if ln.strip() and not ln.strip().startswith((";", "."))]
+
+
+def test_collect_writes_image_rows_through_and_releases_at_system_scope(asm):
+    body = kernel_body(asm, "_Z17rt_collect_kernel")
+    stores = [i for i, ln in enumerate(body) if ln.startswith("global_store_dwordx4")]
+    through = [i for i in stores if re.search(r"\bsc0 sc1\b", body[i])]
+    assert through, "no system-scope write-through store of an image pixel"
+    wbl2 = [i for i, ln in enumerate(body) if ln == "buffer_wbl2 sc0 sc1"]
+    assert wbl2, "no system-scope release (buffer_wbl2 sc0 sc1)"
+    # the release follows the write-through store, and a vmcnt(0) wait
+    # follows the release (the store is inline asm: hipcc does not count it)
+    assert max(through) < wbl2[-1]
+    assert any(ln.startswith("s_waitcnt") and "vmcnt(0)" in ln
+               for ln in body[wbl2[-1] + 1:])
+
+
+def test_acquire_kernel_invalidates_at_system_scope(asm):
+    body = kernel_body(asm, "_Z17rt_acquire_kernel")
+    assert "buffer_inv sc0 sc1" in body
+    i = body.index("buffer_inv sc0 sc1")
+    assert any(ln.startswith("s_waitcnt") and "vmcnt(0)" in ln for ln in body[i + 1:])
+
+
+def test_render_kernel_has_no_system_scope_traffic(asm):
+    """The single-device hot path pays for none of it."""
+    body = kernel_body(asm, "_Z16rt_render_kernel")
+    assert not any("sc0 sc1" in ln for ln in body)
