@@ -71,14 +71,15 @@ class RtStats(ctypes.Structure):
     _fields_ = [("segments", ctypes.c_uint64), ("traced_segments", ctypes.c_uint64),
                 ("sphere_tests", ctypes.c_uint64), ("paths", ctypes.c_uint64),
                 ("kernel_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
-                ("kernel_launches", ctypes.c_uint32), ("short_math", ctypes.c_uint32)]
+                ("kernel_launches", ctypes.c_uint32), ("short_math", ctypes.c_uint32),
+                ("clock_ghz", ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_ if not k.startswith("_")}
 
 
 assert ctypes.sizeof(RtParams) == 48
-assert ctypes.sizeof(RtStats) == 56
+assert ctypes.sizeof(RtStats) == 64
 
 
 class RayTraceError(RuntimeError):

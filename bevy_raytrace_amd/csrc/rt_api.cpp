@@ -50,7 +50,7 @@ struct Frame {
     size_t out_cap = 0;
     uint32_t* d_counters = nullptr; // [0..3] 2 x u64 segment counters, [4..] per-pass work counters
     size_t counters_cap = 0;        // in u32 words
-    unsigned long long* h_segs = nullptr;  // pinned, 18 counters
+    unsigned long long* h_segs = nullptr;  // pinned, RT_CNT_U64 counters
     std::vector<hipEvent_t> ev;     // 2 per pass
     hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;
     // the pending call in this slot
@@ -83,6 +83,10 @@ struct Tuning {
     int64_t wide_max = -1;        // sphere-parallel threshold (-1 = cost model)
     bool fast_exact = true;       // short correctly-rounded exact test when in domain
     int64_t fail_alloc_after = -1;  // fault injection: device allocations left (-1 = off)
+    // positive control of the checked build: the bound of one RT_IDX site
+    // (4 sph, 6 mats, 7 slots, 16 output) given as 0, so its first index is
+    // reported (the product build reads no bound: no effect)
+    uint32_t chk_shrink = 0;
 };
 
 struct rt_ctx {
@@ -239,6 +243,9 @@ static bool tune_set(Tuning& t, const char* name, const char* v) {
         t.fast_exact = x != 0;
     } else if (!strcmp(name, "fail_alloc_after")) {
         t.fail_alloc_after = (int64_t)x;
+    } else if (!strcmp(name, "chk_shrink")) {
+        if (x != 0 && x != 4 && x != 6 && x != 7 && x != 16) return false;
+        t.chk_shrink = (uint32_t)x;
     } else {
         return false;
     }
@@ -287,7 +294,7 @@ int rt_create(int device, rt_ctx** out_ctx) {
         if ((e = rt_render_occupancy(&ctx->blocks_per_cu, &ctx->blocks_per_cu_c)) != hipSuccess) break;
         for (Frame& f : ctx->fr) {
             if ((e = hipStreamCreateWithFlags(&f.stream, hipStreamNonBlocking)) != hipSuccess) break;
-            if ((e = hipHostMalloc((void**)&f.h_segs, 18 * sizeof(unsigned long long))) != hipSuccess)
+            if ((e = hipHostMalloc((void**)&f.h_segs, RT_CNT_U64 * sizeof(unsigned long long))) != hipSuccess)
                 break;
             if ((e = hipEventCreate(&f.ev_t0)) != hipSuccess) break;
             if ((e = hipEventCreate(&f.ev_t1)) != hipSuccess) break;
@@ -1074,6 +1081,9 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     K_.chk_nrm = (uint32_t)((cull ? ctx->rm_c_cap : ctx->sph_rm_cap) / sizeof(float2));
     K_.chk_nmat = ctx->m;
     K_.chk_slots = f.bs_cap / sizeof(float4);
+    if (tn.chk_shrink == 4) K_.chk_nsph = 0;
+    if (tn.chk_shrink == 6) K_.chk_nmat = 0;
+    if (tn.chk_shrink == 7) K_.chk_slots = 0;
 #ifdef RT_MFMA_FILTER
     if (!cull && ctx->mf_ok && !(p.flags & RT_FLAG_VALU_FILTER)) {
         K_.mfA = ctx->d_mfA;
@@ -1185,7 +1195,7 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         const uint64_t tail_items = 2ull * RT_WAVE_CHUNK * grid * (RT_BLOCK_THREADS / 64);
         K_.tail_start = (uint32_t)(items > tail_items ? items - tail_items : 0);
         K_.chk_items = (uint32_t)items;
-        K_.chk_out = (uint64_t)ps.nframes * fstride;
+        K_.chk_out = tn.chk_shrink == 16 ? 0 : (uint64_t)ps.nframes * fstride;
         HIP_TRY_Q(hipEventRecord(f.ev[2 * i], stream));
         HIP_TRY_Q(rt_launch_render(&K_, cull ? ctx->d_grp_c : ctx->d_grp,
                                       cull ? ctx->d_sph_c : ctx->d_sph,
@@ -1201,7 +1211,7 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
                                        (float)p.spp, d_out + (size_t)ps.frame_begin * fstride,
                                        ctx->d_prog, prog_mode, prog_total, stream));
     }
-    HIP_TRY_Q(hipMemcpyAsync(f.h_segs, f.d_counters, 18 * sizeof(unsigned long long),
+    HIP_TRY_Q(hipMemcpyAsync(f.h_segs, f.d_counters, RT_CNT_U64 * sizeof(unsigned long long),
                                 hipMemcpyDeviceToHost, stream));
 #undef HIP_TRY_Q
     f.passes = (uint32_t)passes.size();
@@ -1255,6 +1265,10 @@ static int finish(rt_ctx* ctx, Frame& f, rt_stats* st) {
     st->total_ms = tms;
     st->kernel_launches = f.passes;
     st->short_math = f.short_math;
+    // the waves' summed shader-clock ticks over their summed 100 MHz ticks
+    const unsigned long long clk = f.h_segs[RT_CNT_CLOCK_OFFSET / 2],
+                             real = f.h_segs[RT_CNT_CLOCK_OFFSET / 2 + 1];
+    st->clock_ghz = real ? 0.1 * (double)clk / (double)real : 0.0;
     return RT_OK;
 }
 
@@ -1585,7 +1599,7 @@ int rt_debug_counters(const rt_ctx* ctx, uint64_t* out16) {
 // Internal (not in include/rt_hip.h): set one A/B or fault-injection knob of
 // ctx (struct Tuning above; names: scratch_bytes, split_all, tail_split, tail
 // "a4,a2,a1", prefetch, prio_mode, prio_shift, wg_per_cu, wide_max,
-// fast_exact, fail_alloc_after, block_region). name == NULL restores every default. Used by
+// fast_exact, fail_alloc_after, block_region, chk_shrink). name == NULL restores every default. Used by
 // the tests and tools/ only; the product path never calls it.
 int rt_debug_tune(rt_ctx* ctx, const char* name, const char* value) {
     if (!ctx) return RT_ERR_INVALID_ARG;

@@ -15,8 +15,12 @@
 #endif
 // Counter block at the start of the ctx's counter buffer (u32 words):
 // [0,4) two u64 segment counters, [4,36) 16 u64 diagnostic counters
-// (RT_PROFILE builds), [36, ...) one u32 work counter per pass.
-#define RT_CNT_WORK_OFFSET 36
+// (RT_PROFILE builds), [36,40) two u64 clock sums (the render waves'
+// s_memtime and s_memrealtime deltas: rt_stats.clock_ghz), [40, ...) one u32
+// work counter per pass.
+#define RT_CNT_CLOCK_OFFSET 36
+#define RT_CNT_WORK_OFFSET 40
+#define RT_CNT_U64 20  // u64 counters copied back per call (segments, diagnostics, clocks)
 #define RT_TAIL_ITEM 0x80000000u  // PathState::item flag: a tail item (per-sample slots)
 #define RT_GROUP 8            // spheres per filter group (SoA, 128 B)
 #ifndef RT_SLOT_BUF_CAP

@@ -167,6 +167,15 @@ __device__ __forceinline__ void render_body(
 #ifdef RT_PROFILE
     const unsigned long long t_begin = prof_.last;
 #endif
+    // the launch's shader clock (rt_stats.clock_ghz): every wave adds its
+    // lifetime in shader cycles (s_memtime) and in 100 MHz ticks
+    // (s_memrealtime) to two sums -- the start as a subtraction now, the end
+    // as an addition at the end, so nothing stays live across the loop
+    unsigned long long* const clk_sum = seg_counter + RT_CNT_CLOCK_OFFSET / 2;
+    if (lane == 0) {
+        atomicAdd(clk_sum, 0ull - (unsigned long long)__builtin_amdgcn_s_memtime());
+        atomicAdd(clk_sum + 1, 0ull - (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
     // the wave's slices of the workgroup's LDS arrays: wave-uniform bases
     // (SGPRs) indexed by the lane id, so no VGPR holds an LDS address
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
@@ -519,10 +528,12 @@ __device__ __forceinline__ void render_body(
         }
     }
 #endif
-    // ---- segment counts: one atomic per wave
+    // ---- segment counts and the wave's end stamps: one atomic each per wave
     if (lane == 0) {
         atomicAdd(seg_counter, (unsigned long long)segs);
         atomicAdd(seg_counter + 1, (unsigned long long)traced);
+        atomicAdd(clk_sum, (unsigned long long)__builtin_amdgcn_s_memtime());
+        atomicAdd(clk_sum + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
     }
 }
 

@@ -34,6 +34,7 @@ pub struct rt_stats {
     pub total_ms: f64,
     pub kernel_launches: u32,
     pub short_math: u32,
+    pub clock_ghz: f64,
 }
 
 pub const RT_FLAG_NO_PRIMARY_CACHE: u32 = 0x1;

@@ -195,6 +195,11 @@ typedef struct rt_stats {
                                   sphere test's short correctly-rounded sqrt and
                                   divide, which waves whose rays do too then use;
                                   0: IEEE operations only. Same bits either way. */
+    double   clock_ghz;        /* shader clock the render kernels ran at, averaged
+                                  over their waves' lifetimes: sum of the waves'
+                                  s_memtime deltas / sum of their s_memrealtime
+                                  deltas x 0.1 GHz (the SIMD-issue roofline's peak
+                                  is 1024 SIMDs x this clock)                    */
 } rt_stats;
 
 typedef struct rt_ctx rt_ctx;

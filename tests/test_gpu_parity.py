@@ -857,3 +857,25 @@ def test_failed_scene_upload_leaves_no_scene():
         r.tune(None)
         img, _ = r.render(cam, 32, 18, 2, 4, flags=CULL)
         check_exact(img, O.render(cam, big, bmt, 32, 18, 2, 4)[0])
+
+
+@pytest.mark.parametrize("site", [4, 6, 7, 16])
+def test_checked_build_reports_an_out_of_range_index(renderer, site):
+    """Positive control of the bounds-checked build (librt_hip_checked.so,
+    `--rt-lib`): with one site's bound given as 0 (knob chk_shrink) the render
+    fails with RT_ERR_DEVICE naming that site -- so a clean suite under it
+    means every checked index stayed in range. The product library checks
+    nothing: the same call succeeds, bit-exact."""
+    sp, mt = arrays(scene.rtiow_final_scene())
+    renderer.set_scene(sp, mt)
+    cam = default_camera_block()
+    ref, _ = renderer.render(cam, 32, 18, 4, 4)
+    renderer.tune("chk_shrink", str(site))
+    if hasattr(renderer.lib, "rt_check_bounds_take"):
+        with pytest.raises(Exception, match=f"first at site {site}:"):
+            renderer.render(cam, 32, 18, 4, 4)
+        renderer.tune(None)
+        img, _ = renderer.render(cam, 32, 18, 4, 4)  # the record was reset
+    else:
+        img, _ = renderer.render(cam, 32, 18, 4, 4)
+    check_exact(img, ref)
