@@ -160,31 +160,32 @@ def mfma_report(e):
     return out
 
 
-def simd_issue_roofline(e, frames_per_launch, kms_launch):
-    """The bound the kernel runs against: SIMD issue (DESIGN.md 4.7). Issue
-    cycles per launch from the PMC record (tools/pmc_summary.py: 4 per VALU
-    instruction, 2 per 32-bit integer one, 8 per MFMA; counts scale with the
-    frames of a launch), over this run's HIP-event launch time, against the
-    1024 SIMDs x the clock the profiled launch ran at."""
+def simd_issue_roofline(e, frames_per_launch, kms_launch, clock_run):
+    """The bound the kernel runs against: SIMD issue (DESIGN.md §5). Issue
+    cycles per launch from the PMC record (tools/pmc_summary.py; the
+    instruction counts scale with the frames of a launch) over this run's
+    launch time (HIP events on the kernel's stream) x this run's own shader
+    clock (rt_stats.clock_ghz, measured inside the timed launches) x 1024
+    SIMDs: frac = issue cycles / SIMD cycles of the run."""
     si = (e or {}).get("simd_issue")
-    if not si or not si.get("clock_ghz"):
+    if not si:
         return {"bound": "SIMD issue", "achieved": None, "peak": None,
-                "unit": "G SIMD-issue cycles/s", "frac": None,
+                "unit": "G SIMD-issue cycles/s", "frac": None, "clock_ghz_run": round(clock_run, 4),
                 "note": "no PMC record for this workload in profiles/pmc_traffic.json"}
     cycles = si["issue_cycles_per_launch"] / e["frames_per_launch"] * frames_per_launch
     achieved = cycles / (kms_launch * 1e-3) / 1e9
-    peak = 1024 * si["clock_ghz"]
+    clock = clock_run if clock_run > 0 else si["clock_ghz"]
+    peak = 1024 * clock
+    issue = {k: si[k] for k in ("formula", "prices", "price_source", "valu_share", "mfma_share",
+                                "busy", "clock_ghz", "kernel_ms_under_pmc") if k in si}
+    issue["issue_cycles_per_launch"] = cycles
+    issue["source"] = ("profiles/pmc_traffic.json (rocprofv3 --pmc, one launch of %d frames, "
+                       "tools/pmc_round.sh)" % e["frames_per_launch"])
     return {"bound": "SIMD issue", "achieved": round(achieved, 1), "peak": round(peak, 1),
             "unit": "G SIMD-issue cycles/s", "frac": round(achieved / peak, 4),
-            "issue": {"valu_share_under_pmc": round(si["valu_share"], 4),
-                      "mfma_share_under_pmc": round(si["mfma_share"], 4),
-                      "busy_under_pmc": round(si["busy"], 4),
-                      "clock_ghz_under_pmc": round(si["clock_ghz"], 4),
-                      "kernel_ms_under_pmc": round(si["kernel_ms_under_pmc"], 3),
-                      "issue_cycles_per_launch": cycles,
-                      "formula": si["formula"], "clock_formula": si["clock_formula"],
-                      "source": "profiles/pmc_traffic.json (rocprofv3 --pmc, one launch of %d "
-                                "frames, tools/pmc_round.sh)" % e["frames_per_launch"]}}
+            "clock_ghz_run": round(clock_run, 4),
+            "peak_formula": "1024 SIMDs x clock_ghz_run (this run's in-kernel clock)",
+            "issue": issue}
 
 
 def shim_sequence(r, cam, spheres, mats, W, H, S, D, nframes, host_work_ms=1.0):
@@ -565,8 +566,12 @@ def main():
     pmc = load_pmc(wl.key)
     traffic = load_traffic(pmc, args.steps / max(1, len(sizes)))
     kms_launch = kernel_ms_total / launches
+    # the shader clock the timed launches ran at (rt_stats.clock_ghz: the
+    # render waves' s_memtime ticks over their 100 MHz ticks), launch-time weighted
+    clock_run = (sum(s["kernel_ms"] * s["clock_ghz"] for s in stats) / kernel_ms_total
+                 if kernel_ms_total > 0 else 0.0)
 
-    roofline = simd_issue_roofline(pmc, args.steps / max(1, len(sizes)), kms_launch)
+    roofline = simd_issue_roofline(pmc, args.steps / max(1, len(sizes)), kms_launch, clock_run)
     roofline.update({
         "traffic": traffic,
         # HBM GB/s of the render kernel: PMC bytes per launch / this run's
