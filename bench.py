@@ -498,6 +498,13 @@ def main():
     # parity check below before the reuse / cull runs overwrite the buffer
     head_idx = args.steps - sizes[-1]
     head_frame = image[0].clone() if (rank == 0 and world == 1) else None
+    # --check: the headline run's last launch's frames, hashed now (the reuse
+    # and cull runs below render into the same buffer from frame 0 on)
+    check = None
+    if args.check and rank == 0:
+        import hashlib
+        check = {f"frame{head_idx + i}": hashlib.sha1(image[i].cpu().numpy().tobytes()).hexdigest()[:16]
+                 for i in range(sizes[-1])}
     segs_local = sum(s["segments"] for s in stats)
     traced_local = sum(s["traced_segments"] for s in stats)
     kms = [s["kernel_ms"] for s in stats]
@@ -626,12 +633,8 @@ def main():
     if per_rank is not None:
         out["ranks"] = per_rank
 
-    if args.check:
-        import hashlib
-        last = sizes[-1]
-        out["check"] = {f"frame{args.steps - last + i}":
-                        hashlib.sha1(image[i].cpu().numpy().tobytes()).hexdigest()[:16]
-                        for i in range(last)}
+    if check is not None:
+        out["check"] = check
     if args.tune:
         out["tune"] = args.tune
     if args.lib:

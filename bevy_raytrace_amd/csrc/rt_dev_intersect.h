@@ -785,13 +785,20 @@ __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, ui
 // need), so hipcc itself places the wait states between the MFMA that writes
 // V and the first VALU reading it (round 2 had this in inline asm opening
 // with a hand-placed s_nop 11, DESIGN.md 4.7 "hazards").
+// The 3-input ORs are v_bitop3_b32 (function 0xFE): gfx950 dual-issues it
+// like a 2-input v_or_b32 (0.58 quad-cycles per instruction at 4 waves per
+// SIMD), where v_or3_b32 -- which hipcc picks for a | b | c -- holds the SIMD
+// a full quad-cycle (tools/ubench/valu_forms, profiles/r04/valu_forms/).
+__device__ __forceinline__ uint32_t or3_dual(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0xFE);
+}
 __device__ __forceinline__ void tile_or(const f16x& H, int* gq, int& g) {
-    int v[16];
+    uint32_t v[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = __float_as_int(H[i]);
+    for (int i = 0; i < 16; ++i) v[i] = __float_as_uint(H[i]);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) gq[q] = (v[4 * q] | v[4 * q + 1] | v[4 * q + 2]) | v[4 * q + 3];
-    g = (gq[0] | gq[1] | gq[2]) | gq[3];
+    for (int q = 0; q < 4; ++q) gq[q] = (int)(or3_dual(v[4 * q], v[4 * q + 1], v[4 * q + 2]) | v[4 * q + 3]);
+    g = (int)(or3_dual((uint32_t)gq[0], (uint32_t)gq[1], (uint32_t)gq[2]) | (uint32_t)gq[3]);
 }
 
 // Called by the whole wave (the MFMA operands span all 64 lanes): lanes
@@ -975,9 +982,15 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
                     const uint32_t f = m & RT_MF_FLAGS;
 #ifdef RT_CHECK_BOUNDS
                     RT_IDX(qcount(qp, t ? q1 : q0), RT_MF_CAP, RT_SITE_MFQ);
+                    // a lane without a ray (T0 = +inf) never queues
+                    RT_IDX(f != 0u ? 1u : 0u, live ? 2u : 1u, RT_SITE_DEAD_QUEUE);
                     if (qcount(qp, t ? q1 : q0) >= RT_MF_CAP) qp = t ? q1 : q0;
 #endif
-                    *qp = f | (sb + q * 2u);
+                    // the group index as one opaque SGPR: v_or_b32 (dual-
+                    // issued) rather than v_or3_b32 with an inline constant
+                    uint32_t ge = sb + q * 2u;
+                    asm volatile("" : "+s"(ge));
+                    *qp = f | ge;
                     // one more entry iff a flag is set: min(f, 1) as one VALU
                     // min (the compiler otherwise emits a compare and a select)
                     uint32_t inc;
