@@ -215,55 +215,70 @@ def shim_sequence(r, cam, spheres, mats, W, H, S, D, nframes, host_work_ms=1.0):
     for fname, flags in (("brute", abi.RT_FLAG_NO_PRIMARY_CACHE), ("cull", abi.RT_FLAG_CULL)):
         r.reserve(1, W, H, S, D, flags=flags)
         res = {}
-        for mode in ("pageable", "registered", "pinned", "device", "pageable+host_work",
-                     "registered+host_work"):
-            base = mode.split("+")[0]
+        # mode: host buffer kind, + renders kept in flight ("_1inflight": the
+        # round-3 shim, one; otherwise RT_MAX_PENDING = 2, the shim now), +
+        # busy host work per frame
+        for mode in ("pageable_1inflight", "registered", "registered_1inflight", "pinned",
+                     "device", "device_1inflight", "pageable_1inflight+host_work",
+                     "registered+host_work", "registered_1inflight+host_work"):
+            base = mode.split("+")[0].replace("_1inflight", "")
+            depth = 1 if "_1inflight" in mode else abi.RT_MAX_PENDING
             work = host_work_ms if mode.endswith("host_work") else 0.0
+            nbuf = depth + 1  # the shown frame + the ones in flight
             if base in ("pageable", "registered"):
-                bufs = [np.empty((H, W, 4), np.float32) for _ in range(2)]
+                bufs = [np.empty((H, W, 4), np.float32) for _ in range(nbuf)]
                 if base == "registered":
                     for b in bufs:
                         r.host_register(b)
             elif base == "pinned":
                 bufs = [torch.empty((H, W, 4), dtype=torch.float32, pin_memory=True).numpy()
-                        for _ in range(2)]
+                        for _ in range(nbuf)]
             else:
                 bufs = [torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
-                        for _ in range(2)]
+                        for _ in range(nbuf)]
             calls, stats = [], []
-            pending, ready, t0 = None, None, 0.0
+            pending, ready, t0 = [], None, 0.0  # pending: (buffer, frame0) oldest first
+            shown = None
             for f in range(nframes + 8):  # 8 untimed frames first
                 if f == 8:
                     torch.cuda.synchronize()
                     calls, stats, t0 = [], [], time.perf_counter()
-                if pending is not None:  # step 1: rt_wait for last update's frame
+                while len(pending) >= depth:  # step 1: rt_wait for the oldest frame
                     stats.append(r.wait())
-                    ready, pending = pending, None
+                    ready, shown = pending.pop(0)
                 dirty = spheres.tobytes() != sp_bytes or mats.tobytes() != mt_bytes  # step 2
                 assert not dirty
-                i = 0 if ready is None else 1 - ready
+                i = next(k for k in range(nbuf)
+                         if k != ready and all(k != p for p, _ in pending))
                 tc = time.perf_counter()
                 if base == "device":
                     r.render_device(cam, bufs[i].data_ptr(), W, H, S, D, frame0=f, flags=flags)
                 else:
                     r.render_async(cam, bufs[i], W, H, S, D, frame0=f, flags=flags)
                 calls.append(time.perf_counter() - tc)
-                pending = i
+                pending.append((i, f))
                 busy(work)  # the rest of the app's frame
-            stats.append(r.wait())
+            while pending:
+                stats.append(r.wait())
+                ready, shown = pending.pop(0)
             dt = time.perf_counter() - t0
+            # the last frame the sequence delivered, against a plain render of it
+            last = (bufs[ready].cpu().numpy() if base == "device" else np.array(bufs[ready]))
+            ref, _ = r.render(cam, W, H, S, D, frame0=shown, flags=flags)
+            exact = bool(np.array_equal(last, ref, equal_nan=True))
             if base == "registered":
                 for b in bufs:
                     r.host_unregister(b)
             segs = float(np.mean([s["segments"] for s in stats]))
             res[mode] = {"frame_interval_ms": round(dt / nframes * 1e3, 4),
-                         "fps": round(nframes / dt, 1),
+                         "fps": round(nframes / dt, 1), "in_flight": depth,
                          "enqueue_call_ms": round(float(np.mean(calls)) * 1e3, 4),
                          "gpu_total_ms": round(float(np.mean([s["total_ms"] for s in stats])), 4),
                          "kernel_ms": round(float(np.mean([s["kernel_ms"] for s in stats])), 4),
-                         "mrays_per_s": round(segs / (dt / nframes) / 1e6, 1)}
-        dev = res["device"]["gpu_total_ms"]
-        for mode in ("pageable", "registered", "pinned"):
+                         "mrays_per_s": round(segs / (dt / nframes) / 1e6, 1),
+                         "last_frame_bit_exact": exact}
+        dev = res["device_1inflight"]["gpu_total_ms"]
+        for mode in ("pageable_1inflight", "registered_1inflight", "pinned"):
             d2h = res[mode]["gpu_total_ms"] - dev
             res[mode]["d2h_ms"] = round(d2h, 4)
             res[mode]["d2h_share_of_frame"] = round(d2h / res[mode]["frame_interval_ms"], 4)

@@ -6,18 +6,24 @@
 //! Per frame, in `update` (it has `&mut World`, runs after every RenderStage
 //! ::Prepare system, so sphere.rs / ray_trace_materials.rs / ray_trace_globals.rs
 //! have packed this frame's bytes):
-//!   1. rt_wait for the frame enqueued one frame ago (it had a whole frame of
-//!      wall time to finish) -- its texels become the frame `run` shows;
+//!   1. with RT_MAX_PENDING (2) renders in flight, rt_wait for the older one
+//!      (enqueued two frames ago) -- its texels become the frame `run` shows;
 //!   2. dirty-tracked scene upload: rt_update_* for a same-size edit,
 //!      rt_set_scene when the counts change, nothing when the bytes are equal
 //!      (the reference re-uploads everything every frame, sphere.rs:180-197);
 //!   3. rt_reserve when the output size changes (the reference sizes its
-//!      buffers in prepare, ray_trace_rays.rs:50-66, not in run);
-//!   4. rt_render_async of this frame into the other host buffer.
-//! `run` only copies the finished frame into the texture. The displayed frame
-//! is one frame behind the camera, and the CPU never blocks on a render it
-//! just enqueued. A failing call is logged and skipped (the previous image
-//! stays); nothing panics across the render thread.
+//!      buffers in prepare, ray_trace_rays.rs:50-66, not in run; it needs no
+//!      render in flight, so a resize first completes the pending ones);
+//!   4. rt_render_async of this frame into a host buffer that is neither shown
+//!      nor in flight (three buffers).
+//! Two renders in flight: each pending frame has its own stream in the
+//! library, so frame n's device->host copy overlaps frame n+1's render (the
+//! copy is 45 % of a 1080p frame at 1 spp, profiles/r03_bench_reference1080.json;
+//! bench.py shim_sequence measures both depths). `run` only copies the
+//! finished frame into the texture. The displayed frame is two frames behind
+//! the camera, and the CPU never blocks on a render it just enqueued. A
+//! failing call is logged and skipped (the previous image stays); nothing
+//! panics across the render thread.
 use std::num::NonZeroU32;
 
 use bevy::{
@@ -62,13 +68,16 @@ struct HostFrame {
     registered: Option<(usize, usize)>,
 }
 
+/// Host frame buffers: the shown one and RT_MAX_PENDING in flight.
+const NBUF: usize = RT_MAX_PENDING as usize + 1;
+
 pub struct RayTraceNode {
     ctx: RtContext,
     uploaded: Uploaded,
     camera: Vec<u8>,
-    frames: [HostFrame; 2],
-    /// index of the frame an rt_render_async is pending into
-    pending: Option<usize>,
+    frames: [HostFrame; NBUF],
+    /// buffers rt_render_async calls are pending into, oldest first
+    pending: std::collections::VecDeque<usize>,
     /// index of the last finished frame (what `run` shows)
     ready: Option<usize>,
 }
@@ -79,8 +88,8 @@ impl RayTraceNode {
             ctx,
             uploaded: Uploaded::default(),
             camera: Vec::new(),
-            frames: [HostFrame::default(), HostFrame::default()],
-            pending: None,
+            frames: Default::default(),
+            pending: std::collections::VecDeque::new(),
             ready: None,
         }
     }
@@ -103,14 +112,29 @@ impl RayTraceNode {
         }
     }
 
-    /// Step 1: complete the render enqueued last frame.
-    fn finish_pending(&mut self) {
-        if let Some(i) = self.pending.take() {
+    /// Complete the oldest render in flight (rt_wait completes the oldest).
+    fn finish_oldest(&mut self) {
+        if let Some(i) = self.pending.pop_front() {
             let mut st = rt_stats::default();
             match self.ctx.check(unsafe { rt_wait(self.ctx.0, &mut st) }) {
                 Ok(()) => self.ready = Some(i),
                 Err(e) => error!("rt_wait: {e}"),
             }
+        }
+    }
+
+    /// Step 1: keep at most RT_MAX_PENDING - 1 renders in flight before
+    /// enqueueing this frame's.
+    fn finish_pending(&mut self) {
+        while self.pending.len() >= RT_MAX_PENDING as usize {
+            self.finish_oldest();
+        }
+    }
+
+    /// Every render in flight (before rt_reserve, and on drop).
+    fn finish_all(&mut self) {
+        while !self.pending.is_empty() {
+            self.finish_oldest();
         }
     }
 
@@ -222,18 +246,27 @@ impl render_graph::Node for RayTraceNode {
         let frame = world.resource::<GlobalsGPUStorage>().buffer.get().frame;
         let params = self.params(size, frame);
         if size != self.uploaded.reserved {
+            self.finish_all(); // rt_reserve requires no render in flight
             match self.ctx.check(unsafe { rt_reserve(self.ctx.0, &params, 1) }) {
                 Ok(()) => self.uploaded.reserved = size,
                 Err(e) => error!("rt_reserve: {e}"),
             }
         }
-        // the buffer `run` does not show
-        let i = match self.ready {
-            Some(r) => 1 - r,
-            None => 0,
+        // a buffer `run` does not show and no render is pending into
+        let i = match (0..NBUF).find(|b| Some(*b) != self.ready && !self.pending.contains(b)) {
+            Some(i) => i,
+            None => return,
         };
         let buf = &mut self.frames[i];
-        buf.texels.resize((size.0 * size.1 * 4) as usize, 0.0);
+        let len = (size.0 * size.1 * 4) as usize;
+        if buf.texels.len() != len {
+            // resize() may move the allocation: unregister the old one first,
+            // while it is still ours (no render is pending into this buffer)
+            if let Some((p, _)) = buf.registered.take() {
+                let _ = self.ctx.check(unsafe { rt_host_unregister(self.ctx.0, p as *mut _) });
+            }
+            buf.texels.resize(len, 0.0);
+        }
         buf.size = size;
         // page-locked once per allocation: the device->host copy is then a DMA
         // and rt_render_async returns at once instead of waiting for the frame
@@ -256,7 +289,7 @@ impl render_graph::Node for RayTraceNode {
                             buf.texels.as_mut_ptr())
         };
         match self.ctx.check(rc) {
-            Ok(()) => self.pending = Some(i),
+            Ok(()) => self.pending.push_back(i),
             Err(e) => error!("rt_render_async: {e}"),
         }
     }
@@ -296,8 +329,8 @@ impl render_graph::Node for RayTraceNode {
 
 impl Drop for RayTraceNode {
     fn drop(&mut self) {
-        // the host buffer of a pending render must outlive it
-        self.finish_pending();
+        // the host buffers of pending renders must outlive them
+        self.finish_all();
         // self.ctx drops next: rt_destroy
     }
 }

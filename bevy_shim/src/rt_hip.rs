@@ -37,6 +37,8 @@ pub struct rt_stats {
     pub clock_ghz: f64,
 }
 
+/// Renders that may be in flight on one context (rt_hip.h RT_MAX_PENDING).
+pub const RT_MAX_PENDING: u32 = 2;
 pub const RT_FLAG_NO_PRIMARY_CACHE: u32 = 0x1;
 /// Opt-in camera sampling (rt_hip.h): sub-pixel jitter and thin-lens samples
 /// through the reference's thin_lens_ray (generate.wgsl:85-107).

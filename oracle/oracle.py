@@ -17,6 +17,20 @@ LIB = os.path.join(HERE, "build", "librt_oracle.so")
 _lib = None
 
 
+def default_threads():
+    """Threads the oracle runs on by default: the CPUs this process may use,
+    capped by the cgroup CPU quota (the GPU box shows 256 cores under a 16-CPU
+    quota; more threads than the quota only time-slice)."""
+    n = len(os.sched_getaffinity(0)) or os.cpu_count() or 1
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, -(-int(q) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 class _Params(ctypes.Structure):
     _fields_ = [("width", ctypes.c_uint32), ("height", ctypes.c_uint32),
                 ("spp", ctypes.c_uint32), ("max_depth", ctypes.c_uint32),
@@ -102,7 +116,7 @@ def intersect_batch(spheres, rays, nthreads=None):
     t = np.empty(r.shape[0], np.float32)
     load().rto_intersect_batch(_ptr(spheres), len(spheres), r.ctypes.data_as(ctypes.c_void_p),
                                r.shape[0], idx.ctypes.data_as(ctypes.c_void_p),
-                               t.ctypes.data_as(ctypes.c_void_p), nthreads or os.cpu_count() or 1)
+                               t.ctypes.data_as(ctypes.c_void_p), nthreads or default_threads())
     return idx, t
 
 
@@ -137,7 +151,7 @@ def render(cam, spheres, materials, width, height, spp, max_depth, frame0=0, row
     """Render the shard's rows -> (rows, W, 4) float32, segments.
     raw_sums: the block-folded sample sums instead of sum / spp (alpha 0)."""
     cam = np.ascontiguousarray(cam)
-    nthreads = nthreads or os.cpu_count() or 1
+    nthreads = nthreads or default_threads()
     B = max(1, row_block)
     nrows = sum(1 for y in range(height)
                 if _block_owner(y // B, shard_count) == shard_index)
@@ -156,7 +170,7 @@ def render(cam, spheres, materials, width, height, spp, max_depth, frame0=0, row
 def render_rows(cam, spheres, materials, width, height, spp, max_depth, rows, frame0=0,
                 nthreads=None, flags=0):
     cam = np.ascontiguousarray(cam)
-    nthreads = nthreads or os.cpu_count() or 1
+    nthreads = nthreads or default_threads()
     rows = np.ascontiguousarray(rows, dtype=np.uint32)
     out = np.zeros((rows.size, width, 4), dtype=np.float32)
     segs = ctypes.c_uint64(0)

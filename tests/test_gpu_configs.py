@@ -76,6 +76,26 @@ def test_config4_8k_shard_of_8(renderer, k):
     assert (img[..., 3] == 1).all()
 
 
+def test_config4_8k_shard_walks_identical(renderer):
+    """Every row of one rank's part of the 8-GPU 8K frame (shard 7 of 8, 540
+    rows x 7680, 1024 spp) through the three walks of the sphere list -- the
+    matrix-core filter (default), the packed VALU filter and the culled list:
+    bit-identical, segment counts equal."""
+    wl, sp, mt = _scene("rtiow8k")
+    W, H, S, D = wl.width, wl.height, wl.spp, wl.max_depth
+    K, k = 8, 7
+    B = pick_row_block(H, K)
+    cam = default_camera_block()
+    renderer.set_scene(sp, mt)
+    _, m, sm = _render_shard_device(renderer, cam, W, H, S, D, B, K, k, NO_REUSE)
+    _, v, sv = _render_shard_device(renderer, cam, W, H, S, D, B, K, k,
+                                    NO_REUSE | abi.RT_FLAG_VALU_FILTER)
+    check_exact(v, m)
+    _, c, sc = _render_shard_device(renderer, cam, W, H, S, D, B, K, k, NO_REUSE | CULL)
+    check_exact(c, m)
+    assert sm["segments"] == sv["segments"] == sc["segments"] == sm["traced_segments"]
+
+
 def test_config4_8k_segments_exact(renderer):
     """Segment count and pixels of a 4-row shard of the 8K frame (row blocks of
     1, K = 1080: rows 546, 1613, 2706, 3773 -- two of them past 2^24 / W)

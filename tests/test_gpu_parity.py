@@ -387,13 +387,33 @@ def test_full_1080p64_properties(renderer):
 
 
 def test_4k_sampled_rows(renderer):
+    """BASELINE config 3 (4K, 256 spp, depth 32): 64 rows spread over the
+    frame bit-exact against the oracle."""
     sp, mt = arrays(scene.rtiow_final_scene())
     cam = default_camera_block()
     renderer.set_scene(sp, mt)
     img, st = renderer.render(cam, 3840, 2160, 256, 32)
-    rows = np.linspace(3, 2157, 24).round().astype(int).tolist()  # 24 rows spread over the frame
+    rows = np.linspace(3, 2157, 64).round().astype(int).tolist()  # 64 rows spread over the frame
     ref, _ = O.render_rows(cam, sp, mt, 3840, 2160, 256, 32, rows)
     check_exact(img[rows], ref)
+
+
+def test_4k_full_frame_walks_identical(renderer):
+    """BASELINE config 3, one whole frame through the three walks of the
+    sphere list: the matrix-core filter (default), the packed VALU filter
+    (RT_FLAG_VALU_FILTER) and the culled list (RT_FLAG_CULL) -- every pixel
+    bit-identical and the segment counts equal, so no filter margin fails
+    anywhere in the frame (intersect.wgsl:133-143 is the one answer)."""
+    sp, mt = arrays(scene.rtiow_final_scene())
+    cam = default_camera_block()
+    renderer.set_scene(sp, mt)
+    m, sm = renderer.render(cam, 3840, 2160, 256, 32, flags=NO_REUSE)
+    v, sv = renderer.render(cam, 3840, 2160, 256, 32, flags=NO_REUSE | VALU)
+    check_exact(v, m)
+    del v
+    c, sc = renderer.render(cam, 3840, 2160, 256, 32, flags=NO_REUSE | CULL)
+    check_exact(c, m)
+    assert sm["segments"] == sv["segments"] == sc["segments"] == sm["traced_segments"]
 
 
 def test_errors(renderer):
