@@ -201,21 +201,25 @@ def test_flag_constants_agree_across_bindings():
 
 def test_bench_roofline_recomputes_from_committed_counters():
     """bench.py's roofline (SIMD issue) follows from the committed PMC record:
-    at the profiled launch time its frac is the record's issue busy, <= 1, and
-    the busy is the documented formula over the raw counters."""
+    at the profiled launch time and clock its frac is the record's issue busy
+    (<= 1), the busy is the documented formula over the raw counters, and a
+    run on a faster clock at the same cycle count reads the same frac."""
     import json
     import bench
     ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     e = bench.load_pmc("rtiow1080")
     assert e is not None and "simd_issue" in e
     si = e["simd_issue"]
-    r = bench.simd_issue_roofline(e, e["frames_per_launch"], si["kernel_ms_under_pmc"])
+    r = bench.simd_issue_roofline(e, e["frames_per_launch"], si["kernel_ms_under_pmc"],
+                                  si["clock_ghz"])
     assert r["bound"] == "SIMD issue"
     assert 0.5 < r["frac"] <= 1.0
     assert abs(r["frac"] - si["busy"]) < 1e-3
-    raw = json.load(open(os.path.join(ROOT, "profiles", "r03_pmc_rtiow1080.json")))
+    # the same cycles at another clock: the launch takes proportionally less time
+    f = 2.4 / si["clock_ghz"]
+    r2 = bench.simd_issue_roofline(e, e["frames_per_launch"], si["kernel_ms_under_pmc"] / f, 2.4)
+    assert abs(r2["frac"] - r["frac"]) < 1e-3
+    raw = json.load(open(os.path.join(ROOT, si["raw_record"])))
     c = raw["per_dispatch_mean"]["rt_render_kernel"]
-    cyc = (4 * (c["SQ_INSTS_VALU"] - c["SQ_INSTS_MFMA"] - c["SQ_INSTS_VALU_INT32"])
-           + 2 * c["SQ_INSTS_VALU_INT32"] + 8 * c["SQ_INSTS_MFMA"])
+    cyc = 4 * (c["SQ_ACTIVE_INST_VALU"] - c["SQ_ACTIVE_INST_VALU2"]) + 4 * c["SQ_INSTS_MFMA"]
     assert abs(cyc / (1024 * c["GRBM_GUI_ACTIVE"] / 8) - si["busy"]) < 1e-9
-

@@ -129,7 +129,8 @@ if "FETCH_SIZE" in rk and "WRITE_SIZE" in rk:
                        "other VALU forms": "4 cycles", "transcendental": "8 cycles",
                        "MFMA 32x32x16": "8 cycles of issue (32 of matrix pipe)"},
             "price_source": "tools/ubench/valu_forms at 4 waves/SIMD + its PMC passes "
-                            "(profiles/r04/valu_forms/)",
+                            "(profiles/r04/valu_forms/table.txt)",
+            "raw_record": f"profiles/{tag}_pmc_{wl}.json",
             "clock_formula": "GRBM_GUI_ACTIVE / 8 XCDs / render kernel time under the profiler",
         }
     json.dump(d, open(tp, "w"), indent=1)
