@@ -87,6 +87,9 @@ struct Tuning {
     // (4 sph, 6 mats, 7 slots, 16 output) given as 0, so its first index is
     // reported (the product build reads no bound: no effect)
     uint32_t chk_shrink = 0;
+    // whole items write their output pixel themselves (KParams::dout); off:
+    // every frame through the slots and rt_collect_kernel (same bits)
+    bool direct_out = true;
 };
 
 struct rt_ctx {
@@ -138,7 +141,12 @@ struct rt_ctx {
     hipStream_t stream = nullptr;  // = fr[0].stream: scene uploads, intersect, progressive
     unsigned long long dbg[16] = {};  // diagnostic counters of the last waited frame
 
-    std::vector<std::pair<void*, size_t>> host_regs;  // rt_host_register'd buffers
+    struct HostReg {
+        void* ptr;
+        size_t bytes;
+        void* dev;  // its device-visible address (hipHostGetDevicePointer)
+    };
+    std::vector<HostReg> host_regs;  // rt_host_register'd buffers
 
     float4* d_prog = nullptr;       // progressive running sum (rt_render_progressive)
     size_t prog_cap = 0;
@@ -243,6 +251,8 @@ static bool tune_set(Tuning& t, const char* name, const char* v) {
         t.fast_exact = x != 0;
     } else if (!strcmp(name, "fail_alloc_after")) {
         t.fail_alloc_after = (int64_t)x;
+    } else if (!strcmp(name, "direct_out")) {
+        t.direct_out = x != 0;
     } else if (!strcmp(name, "chk_shrink")) {
         if (x != 0 && x != 4 && x != 6 && x != 7 && x != 16) return false;
         t.chk_shrink = (uint32_t)x;
@@ -319,7 +329,7 @@ void rt_destroy(rt_ctx* ctx) {
         if (f.stream) hipStreamSynchronize(f.stream);
         if (f.pending_stream) hipStreamSynchronize(f.pending_stream);
     }
-    for (const auto& r : ctx->host_regs) hipHostUnregister(r.first);
+    for (const auto& r : ctx->host_regs) hipHostUnregister(r.ptr);
     hipFree(ctx->d_grp);
     hipFree(ctx->d_sph);
     hipFree(ctx->d_sph_rm);
@@ -913,7 +923,7 @@ int rt_update_materials(rt_ctx* ctx, uint32_t first, const rt_material* material
 // the launch would, then return without enqueueing any work.
 static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params* prm,
                    uint32_t nframes, float4* d_out, hipStream_t stream, int prog_mode = 0,
-                   float prog_total = 0.0f, bool reserve_only = false) {
+                   float prog_total = 0.0f, bool reserve_only = false, bool out_host = false) {
     if ((!cam && !reserve_only) || !prm)
         return fail(ctx, RT_ERR_INVALID_ARG, "camera or params is NULL");
     if (!ctx->has_scene) return fail(ctx, RT_ERR_NO_SCENE, "rt_render before rt_set_scene");
@@ -934,6 +944,9 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         return fail(ctx, RT_ERR_INVALID_ARG, "nframes * spp exceeds 2^32");
     const uint32_t rows = rt_shard_rows(p.height, B, K, p.shard_index);
     const uint32_t npix = rows * p.width;
+    if (npix >= RT_INDEX_LIMIT)
+        return fail(ctx, RT_ERR_INVALID_ARG, "%u x %u rows of pixels in one call exceed 2^30",
+                    p.width, rows);
     const uint32_t blocks_total = (p.spp + RT_SAMPLE_BLOCK - 1) / RT_SAMPLE_BLOCK;
     if (!d_out && !reserve_only) return fail(ctx, RT_ERR_INVALID_ARG, "output pointer is NULL");
 
@@ -999,7 +1012,9 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     };
     if (npix) {
         uint64_t slots_cap = tn.scratch_bytes / per_block;
-        const uint64_t by_index = 0x7FFFFFFFull / npix;  // work items fit in u32
+        // slot indices (and work items) stay below RT_INDEX_LIMIT: a slot
+        // entry's bit 30 marks a direct output (RT_DIRECT_ITEM)
+        const uint64_t by_index = (RT_INDEX_LIMIT - 1ull) / npix;
         if (slots_cap > by_index) slots_cap = by_index;
         if (slots_cap < 1) slots_cap = 1;
         uint64_t bs_slots = 0;
@@ -1076,6 +1091,19 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     }
     K_.scene_fast = ctx->scene_fast && tn.fast_exact ? 1u : 0u;
     K_.flags = p.flags;
+    // direct output (KParams::dout): one whole-frame pass per launch, plain
+    // frames (not progressive), an output pixel index the item knows (the
+    // image layout: one shard, or RT_FLAG_IMAGE_OUT); the launch's output
+    // indices below RT_INDEX_LIMIT
+    const bool direct = tn.direct_out && prog_mode == 0 && !passes.empty() &&
+                        passes[0].block_begin == 0 && passes[0].nblocks == blocks_total &&
+                        (K == 1 || (p.flags & RT_FLAG_IMAGE_OUT));
+    // host memory (a registered caller buffer) or another device's image:
+    // system-scope write-through stores and a release per wave
+    K_.dsys = (out_host || (p.flags & RT_FLAG_IMAGE_OUT)) ? 1u : 0u;
+    K_.dstride = (uint32_t)fstride;
+    K_.dwhole_blk = blocks_total == 1 ? 1u : 0u;
+    K_.dwhole_tail = p.spp == 1 ? 1u : 0u;
     // the buffers' sizes (RT_CHECK_BOUNDS builds check every index against them)
     K_.chk_nsph = (uint32_t)((cull ? ctx->sph_c_cap : ctx->sph_cap) / sizeof(float4));
     K_.chk_nrm = (uint32_t)((cull ? ctx->rm_c_cap : ctx->sph_rm_cap) / sizeof(float2));
@@ -1196,6 +1224,29 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         K_.tail_start = (uint32_t)(items > tail_items ? items - tail_items : 0);
         K_.chk_items = (uint32_t)items;
         K_.chk_out = tn.chk_shrink == 16 ? 0 : (uint64_t)ps.nframes * fstride;
+        // Direct output of the launch's whole items. A frame is written
+        // directly iff every item of it is whole: its pixel items cover all
+        // its blocks ((f + 1) nb <= qpix), or its block items are whole (one
+        // block per frame), or its tail samples are (spp == 1). Those frames
+        // are a prefix of the launch; the collect folds the rest.
+        K_.dout = nullptr;
+        K_.dfull = 0;
+        K_.collect_f0 = 0;
+        if (direct && (uint64_t)ps.nframes * fstride < RT_INDEX_LIMIT) {
+            const uint64_t nb = ps.nblocks;
+            uint32_t fc = 0;
+            while (fc < ps.nframes) {
+                const uint64_t q0 = fc * nb, q1 = q0 + nb;
+                const bool has_pix = q0 < K_.qpix, pix_whole = q1 <= K_.qpix;
+                const bool has_blk = std::max<uint64_t>(q0, K_.qpix) < std::min<uint64_t>(q1, K_.qmain);
+                const bool has_tail = q1 > K_.qmain;
+                if ((has_pix && !pix_whole) || (has_blk && nb != 1) || (has_tail && p.spp != 1)) break;
+                ++fc;
+            }
+            K_.dout = d_out + (size_t)ps.frame_begin * fstride;
+            K_.dfull = K_.qpix / ps.nblocks;
+            K_.collect_f0 = fc;
+        }
         HIP_TRY_Q(hipEventRecord(f.ev[2 * i], stream));
         HIP_TRY_Q(rt_launch_render(&K_, cull ? ctx->d_grp_c : ctx->d_grp,
                                       cull ? ctx->d_sph_c : ctx->d_sph,
@@ -1362,6 +1413,20 @@ int rt_render_async(rt_ctx* ctx, const rt_camera* camera, const rt_params* param
     Frame* f = next_slot(ctx, "rt_render_async");
     if (!f) return RT_ERR_INVALID_ARG;
     const size_t bytes = out_bytes(params);
+    // A registered buffer (rt_host_register) is written by the kernels
+    // themselves through its device-visible address -- whole items as they
+    // finish, during the render (system-scope write-through stores) -- so no
+    // staging buffer and no device->host copy after the render
+    for (const auto& r : ctx->host_regs) {
+        const char* lo = (const char*)r.ptr;
+        const char* o = (const char*)out_rgba;
+        if (r.dev && o >= lo && o + bytes <= lo + r.bytes) {
+            float4* dev = (float4*)((char*)r.dev + (o - lo));
+            int rc = enqueue(ctx, *f, camera, params, 1, dev, f->stream, 0, 0.0f, false, true);
+            if (rc) return rc;
+            return commit(ctx, *f, f->stream, nullptr, nullptr, 0);
+        }
+    }
     int rc = ensure(ctx, &f->d_out, &f->out_cap, std::max<size_t>(bytes, 16));
     if (rc) return rc;
     rc = enqueue(ctx, *f, camera, params, 1, f->d_out, f->stream);
@@ -1373,17 +1438,19 @@ int rt_host_register(rt_ctx* ctx, void* ptr, size_t bytes) {
     if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_host_register: ctx is NULL");
     if (!ptr || !bytes) return fail(ctx, RT_ERR_INVALID_ARG, "rt_host_register: empty buffer");
     for (const auto& r : ctx->host_regs)
-        if (r.first == ptr) return fail(ctx, RT_ERR_INVALID_ARG, "rt_host_register: %p already registered", ptr);
+        if (r.ptr == ptr) return fail(ctx, RT_ERR_INVALID_ARG, "rt_host_register: %p already registered", ptr);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    HIP_TRY(ctx, hipHostRegister(ptr, bytes, hipHostRegisterDefault));
-    ctx->host_regs.emplace_back(ptr, bytes);
+    HIP_TRY(ctx, hipHostRegister(ptr, bytes, hipHostRegisterMapped));
+    void* dev = nullptr;
+    if (hipHostGetDevicePointer(&dev, ptr, 0) != hipSuccess) dev = nullptr;  // (then staged)
+    ctx->host_regs.push_back({ptr, bytes, dev});
     return RT_OK;
 }
 
 int rt_host_unregister(rt_ctx* ctx, void* ptr) {
     if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_host_unregister: ctx is NULL");
     for (size_t i = 0; i < ctx->host_regs.size(); ++i) {
-        if (ctx->host_regs[i].first != ptr) continue;
+        if (ctx->host_regs[i].ptr != ptr) continue;
         int rc = quiesce(ctx);  // no pending copy may still target it
         if (rc) return rc;
         ctx->host_regs.erase(ctx->host_regs.begin() + (long)i);
@@ -1599,7 +1666,7 @@ int rt_debug_counters(const rt_ctx* ctx, uint64_t* out16) {
 // Internal (not in include/rt_hip.h): set one A/B or fault-injection knob of
 // ctx (struct Tuning above; names: scratch_bytes, split_all, tail_split, tail
 // "a4,a2,a1", prefetch, prio_mode, prio_shift, wg_per_cu, wide_max,
-// fast_exact, fail_alloc_after, block_region, chk_shrink). name == NULL restores every default. Used by
+// fast_exact, fail_alloc_after, block_region, chk_shrink, direct_out). name == NULL restores every default. Used by
 // the tests and tools/ only; the product path never calls it.
 int rt_debug_tune(rt_ctx* ctx, const char* name, const char* value) {
     if (!ctx) return RT_ERR_INVALID_ARG;

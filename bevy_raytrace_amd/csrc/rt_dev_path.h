@@ -10,7 +10,8 @@ struct PathState {
     v3 nseed;           // normalize(seed)
     float seedx;        // seed.x (dielectric Schlick test)
     uint32_t pix;       // global pixel x + W*y (the seed's pixel term, shade.wgsl:216-218)
-    uint32_t item;      // main item: its output slot; tail: RT_TAIL_ITEM | pixel
+    uint32_t item;      // main item: its output slot, or RT_DIRECT_ITEM | output index;
+                        // tail: RT_TAIL_ITEM [| RT_DIRECT_ITEM] | pixel
     uint32_t s, s_end;  // current sample, end of the current sample block
     uint32_t bounce;
 };
@@ -125,6 +126,8 @@ __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint
     uint32_t k, s0, s1;  // pixel in processing order; the (first block's) samples [s0, s1)
     item = RT_IDX(item, P.chk_items, RT_SITE_ITEM);
     uint32_t slot = item;  // a main item's output slot
+    bool whole = false;    // the item covers every sample of its (frame, pixel)
+    uint32_t fo = 0;       // its launch frame
     if (item < main_all) {
         const uint32_t main_pix = P.main_pix, nblocks = P.nblocks, qpix = P.qpix;
         const uint32_t block_begin = P.block_begin, spp = P.spp;
@@ -141,6 +144,7 @@ __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint
             }
             b0 = 0;
             b1 = min(nblocks, qpix - f * nblocks);
+            whole = f < P.dfull;
             // a later pass over the frame's blocks (frames above the scratch
             // budget) continues the fold of the earlier passes (rt_collect_kernel
             // left it in acc_in): ((acc + b0) + b1) ..., the single-pass order
@@ -163,7 +167,9 @@ __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint
             f = fdiv(q, P.div_nblocks);
             b0 = q - f * nblocks;
             b1 = b0 + 1;
+            whole = P.dwhole_blk != 0;
         }
+        fo = f;
         const uint32_t base = sample_base + f * spp;
         s0 = base + (block_begin + b0) * RT_SAMPLE_BLOCK;
         const uint32_t iend = base + min(spp, (block_begin + b1) * RT_SAMPLE_BLOCK);
@@ -189,11 +195,17 @@ __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint
         }
         s0 = sample_base + gb + g * z;
         s1 = sample_base + min(gb + g * z + z, ge);
+        whole = P.dwhole_tail != 0;  // (spp == 1: each sample is its frame's pixel)
     }
     const float4 q4 = tab[RT_IDX(k, npix, RT_SITE_TAB)].d;
-    // main item: its output slot; tail item: RT_TAIL_ITEM | k
-    st.item = item < P.main_all ? slot : (RT_TAIL_ITEM | k);
     st.pix = __float_as_uint(q4.w);
+    // main item: its output slot, or (whole, direct output) the output
+    // index; tail item: RT_TAIL_ITEM | k, RT_DIRECT_ITEM when whole (its
+    // samples' output indices follow from the sample, shade loop)
+    if (P.dout && whole && item < P.main_all)
+        slot = RT_DIRECT_ITEM | (fo * P.dstride + st.pix);
+    st.item = item < P.main_all ? slot
+                                : (RT_TAIL_ITEM | (P.dout && whole ? RT_DIRECT_ITEM : 0u) | k);
     st.s = s0;
     st.s_end = s1;
     st.bsum = mk(0.0f, 0.0f, 0.0f);

@@ -22,6 +22,11 @@
 #define RT_CNT_WORK_OFFSET 40
 #define RT_CNT_U64 20  // u64 counters copied back per call (segments, diagnostics, clocks)
 #define RT_TAIL_ITEM 0x80000000u  // PathState::item flag: a tail item (per-sample slots)
+// PathState::item / slot-buffer entry flag: the item covers every sample of
+// its (frame, pixel) and writes the output pixel itself (KParams::dout); the
+// entry's other bits are the output index f * dstride + pixel (< 2^30)
+#define RT_DIRECT_ITEM 0x40000000u
+#define RT_INDEX_LIMIT 0x40000000u  // slots, pixels and direct indices stay below it
 #define RT_GROUP 8            // spheres per filter group (SoA, 128 B)
 #ifndef RT_SLOT_BUF_CAP
 #define RT_SLOT_BUF_CAP 32    // slot-store buffer entries per wave (rt_kernels.hip)
@@ -129,6 +134,21 @@ struct KParams {
     uint32_t chk_items;  // work items of the launch (main_all + tail_items)
     uint64_t chk_slots;  // block_sums slots
     uint64_t chk_out;    // float4 pixels behind the launch's output pointer
+    // Direct output: an item that covers every
+    // sample of its (frame, pixel) -- a pixel item of a launch frame below
+    // dfull, a block item when the pass has one sample block (dwhole_blk), a
+    // tail item when spp == 1 (dwhole_tail) -- writes out = its fold / spp
+    // (rt_collect_kernel's own arithmetic, so the bits are the collect's) at
+    // dout + f * dstride + pixel through the wave's slot buffer: no slot, no
+    // slot re-read, no collect for its frame. Frames are either wholly direct
+    // or wholly collected (rt_api.cpp); the collect runs over launch frames
+    // [collect_f0, nframes). dout null: off.
+    float4* dout;
+    uint32_t dfull, dwhole_blk, dwhole_tail;
+    uint32_t dstride;     // float4 pixels per output frame (the image, or the packed rows)
+    uint32_t dsys;        // 1: the output is host memory or another device's image:
+                          // system-scope write-through stores + a release per wave
+    uint32_t collect_f0;  // first launch frame rt_collect_kernel folds
 };
 
 // Row block b of the image -> owning shard (rt_params: serpentine deal).

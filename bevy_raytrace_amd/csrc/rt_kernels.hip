@@ -152,6 +152,16 @@ __device__ __forceinline__ const KParams& fresh_params() {
 }
 #endif
 
+// A 16-B store at system scope, write-through (global_store_dwordx4 ... sc0
+// sc1: the AMDGPU memory model's system-scope store; a vector store). Used for
+// rows that may belong to another device's image (RT_FLAG_IMAGE_OUT). hipcc
+// does not count an asm store in its waits: the caller waits (vmcnt(0)).
+__device__ __forceinline__ void store_system(float4* p, float4 v) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v x = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(p), "v"(x) : "memory");
+}
+
 // The persistent render loop; CULL = false is rt_render_kernel (the brute-force
 // walk of the headline), CULL = true rt_render_cull_kernel (the permuted list
 // with group bounds, P.bnd / P.perm / P.nclusters; identical results).
@@ -210,10 +220,25 @@ __device__ __forceinline__ void render_body(
     float4* const sbv = s_sbv + wave * RT_SLOT_BUF_CAP;
     uint32_t* const sbs = s_sbs + wave * RT_SLOT_BUF_CAP;
     uint32_t sbn = 0;
+    // one finished slot: a block-sum slot, or (RT_DIRECT_ITEM) an output pixel
+    // = fold / spp, alpha 1 -- rt_collect_kernel's arithmetic
+    auto put = [&](uint32_t e, float4 v) {
+        if (e & RT_DIRECT_ITEM) {
+            const float spp = (float)P.spp;
+            const float4 o = make_float4(v.x / spp, v.y / spp, v.z / spp, 1.0f);
+            float4* const dst = P.dout + RT_IDX(e & ~RT_DIRECT_ITEM, P.chk_out, RT_SITE_OUT);
+            if (P.dsys)
+                store_system(dst, o);
+            else
+                *dst = o;
+        } else {
+            block_sums[RT_IDX(e, P.chk_slots, RT_SITE_SLOT)] = v;
+        }
+    };
     auto sb_flush = [&]() {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (lane < sbn) block_sums[RT_IDX(sbs[lane], P.chk_slots, RT_SITE_SLOT)] = sbv[lane];
+        if (lane < sbn) put(sbs[lane], sbv[lane]);
         sbn = 0;
     };
 #endif
@@ -411,8 +436,13 @@ __device__ __forceinline__ void render_body(
                     // a tail item stores every sample's colour for the collect
                     if (st.item & RT_TAIL_ITEM) {
                         const v3 c = add(mk(0.0f, 0.0f, 0.0f), st.color);
+                        // a whole (spp == 1) tail sample is its frame's pixel:
+                        // the output index of launch frame s - sample_base
                         const uint32_t slot =
-                            P.main_all + (st.s - P.sample_base - P.g0) * P.npix + (st.item & ~RT_TAIL_ITEM);
+                            (st.item & RT_DIRECT_ITEM)
+                                ? RT_DIRECT_ITEM | ((st.s - P.sample_base) * P.dstride + st.pix)
+                                : P.main_all + (st.s - P.sample_base - P.g0) * P.npix +
+                                      (st.item & ~(RT_TAIL_ITEM | RT_DIRECT_ITEM));
 #ifndef RT_NO_SLOT_BUF
                         spend = true;
                         sslot = slot;
@@ -476,7 +506,7 @@ __device__ __forceinline__ void render_body(
                 const uint32_t n = (uint32_t)__popcll(sm);
                 if (sbn + n > RT_SLOT_BUF_CAP) sb_flush();
                 if (n > RT_SLOT_BUF_CAP) {
-                    if (spend) block_sums[RT_IDX(sslot, P.chk_slots, RT_SITE_SLOT)] = sval;
+                    if (spend) put(sslot, sval);
                 } else {
                     if (spend) {
                         const uint32_t r = sbn + lanemask_lt_count(sm);
@@ -494,6 +524,10 @@ __device__ __forceinline__ void render_body(
 #ifndef RT_NO_SLOT_BUF
     sb_flush();
 #endif
+    if (P.dsys) {  // direct output into host memory / another device's image
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
 
 #ifdef RT_PROFILE
     PROF_MARK(7);
@@ -668,16 +702,6 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_mfma_kernel(
 }
 #endif
 
-// A 16-B store at system scope, write-through (global_store_dwordx4 ... sc0
-// sc1: the AMDGPU memory model's system-scope store; a vector store). Used for
-// rows that may belong to another device's image (RT_FLAG_IMAGE_OUT). hipcc
-// does not count an asm store in its waits: the caller waits (vmcnt(0)).
-__device__ __forceinline__ void store_system(float4* p, float4 v) {
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    const f4v x = {v.x, v.y, v.z, v.w};
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(p), "v"(x) : "memory");
-}
-
 // Fold one frame's results into acc (block order) and, on the frame's last
 // pass, write out = acc / spp with alpha 1 (collect.wgsl:115-125). One thread
 // per pixel of the processing order k (-> image pixel p = order_to_pixel).
@@ -698,7 +722,7 @@ __global__ void rt_collect_kernel(KParams P, const float4* __restrict__ block_su
                                   float4* __restrict__ prog, int prog_mode, float prog_total) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= P.npix) return;
-    const uint32_t f = blockIdx.y;
+    const uint32_t f = blockIdx.y + P.collect_f0;  // (earlier frames: written directly)
     const uint32_t p = RT_IDX(order_to_pixel(P, k), P.npix, RT_SITE_OUT);
     float ax = 0.0f, ay = 0.0f, az = 0.0f;
     bool have = !first_pass;
@@ -713,8 +737,8 @@ __global__ void rt_collect_kernel(KParams P, const float4* __restrict__ block_su
     } else if (prog_mode == 0) {
         const float4 v = make_float4(ax / spp, ay / spp, az / spp, 1.0f);
         float4* const o = out_pixel(P, out, f, p);
-        if (P.flags & RT_FLAG_IMAGE_OUT)
-            store_system(o, v);  // possibly another device's image (xGMI): write-through
+        if (P.dsys)
+            store_system(o, v);  // host memory or another device's image: write-through
         else
             *o = v;
     } else {
@@ -725,13 +749,14 @@ __global__ void rt_collect_kernel(KParams P, const float4* __restrict__ block_su
         prog[p] = make_float4(ax, ay, az, 0.0f);
         out[RT_IDX((size_t)f * P.npix + p, P.chk_out, RT_SITE_OUT)] = make_float4(ax / prog_total, ay / prog_total, az / prog_total, 1.0f);
     }
-    // RT_FLAG_IMAGE_OUT: the rows may live in another device's memory (rank
-    // 0's image mapped over HIP IPC, bevy_raytrace_amd/distributed.py). The
-    // wave's stores above are system-scope write-through; this system-scope
-    // release (buffer_wbl2 sc0 sc1 + the wait for every store of the wave) ends
-    // the wave's part of the hand-off; the reader acquires (rt_acquire) after
-    // the host has seen the launch complete (visibility).
-    if (P.flags & RT_FLAG_IMAGE_OUT) {
+    // P.dsys (RT_FLAG_IMAGE_OUT, or a host-output call writing the caller's
+    // registered buffer): the rows may live in another device's memory (rank
+    // 0's image mapped over HIP IPC, bevy_raytrace_amd/distributed.py) or in
+    // host memory. The wave's stores above are system-scope write-through;
+    // this system-scope release (buffer_wbl2 sc0 sc1 + the wait for every store
+    // of the wave) ends the wave's part of the hand-off; the reader acquires
+    // (rt_acquire) after the host has seen the launch complete.
+    if (P.dsys) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the asm store is invisible to hipcc)
     }
@@ -814,7 +839,9 @@ hipError_t rt_launch_collect(const KParams* P, const float4* block_sums,
                              float4* acc, int first_pass, int last_pass, float spp, float4* out,
                              float4* prog, int prog_mode, float prog_total, hipStream_t stream) {
     const uint32_t T = 256;
-    hipLaunchKernelGGL(rt_collect_kernel, dim3((P->npix + T - 1) / T, P->nframes), dim3(T), 0, stream, *P,
+    if (P->collect_f0 >= P->nframes) return hipSuccess;  // every frame written directly
+    hipLaunchKernelGGL(rt_collect_kernel, dim3((P->npix + T - 1) / T, P->nframes - P->collect_f0),
+                       dim3(T), 0, stream, *P,
                        block_sums, acc, first_pass, last_pass, spp, out, prog, prog_mode,
                        prog_total);
     return hipGetLastError();

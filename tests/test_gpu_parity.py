@@ -899,3 +899,64 @@ def test_checked_build_reports_an_out_of_range_index(renderer, site):
     else:
         img, _ = renderer.render(cam, 32, 18, 4, 4)
     check_exact(img, ref)
+
+
+@pytest.mark.parametrize("S,F,flags", [(1, 3, NO_REUSE), (1, 2, 0), (8, 2, NO_REUSE), (21, 3, NO_REUSE),
+                                       (64, 5, NO_REUSE), (64, 3, 0), (16, 4, NO_REUSE | CULL)],
+                         ids=["spp1", "spp1_reuse", "spp8", "spp21", "spp64", "spp64_reuse",
+                              "spp16_cull"])
+def test_direct_output_identical(renderer, S, F, flags):
+    """Whole items (a pixel item covering its frame's blocks, a block item of a
+    one-block frame, a spp-1 tail sample) write their output pixel themselves
+    (KParams::dout: fold / spp, rt_collect_kernel's arithmetic) and their
+    frames skip the slots and the collect; every frame is bit-identical to the
+    all-collect plan (knob direct_out=0), at several frame / sample mixes so
+    that direct and collected frames share launches."""
+    import torch
+    sp, mt = arrays(scene.rtiow_final_scene())
+    cam = default_camera_block()
+    renderer.set_scene(sp, mt)
+    W, H, D = 96, 54, 8
+    outs = []
+    for direct in (0, 1):
+        renderer.tune("direct_out", str(direct))
+        out = torch.full((F, H, W, 4), -3.0, dtype=torch.float32, device="cuda")
+        renderer.render_frames_device(cam, F, out.data_ptr(), W, H, S, D, frame0=7, flags=flags)
+        st = renderer.wait()
+        outs.append((out.cpu().numpy(), st["segments"]))
+    renderer.tune(None)
+    check_exact(outs[1][0], outs[0][0])
+    assert outs[1][1] == outs[0][1]
+    ref, _ = O.render(cam, sp, mt, W, H, S, D, frame0=7 + (F - 1) * S)
+    check_exact(outs[1][0][F - 1], ref)
+
+
+@pytest.mark.parametrize("S", [1, 64])
+def test_registered_host_output_written_by_the_kernels(renderer, S):
+    """rt_render_async into a registered host buffer: the kernels write it
+    through its mapped address (system-scope stores; no staging, no copy) --
+    bit-identical to the staged copy into a pageable buffer, for every frame of
+    a run with two renders in flight."""
+    sp, mt = arrays(scene.rtiow_final_scene())
+    cam = default_camera_block()
+    renderer.set_scene(sp, mt)
+    W, H, D = 160, 90, 6
+    reg = [np.full((H, W, 4), -5.0, np.float32) for _ in range(2)]
+    for b in reg:
+        renderer.host_register(b)
+    try:
+        got = []
+        for f in range(4):
+            if f >= 2:
+                renderer.wait()
+                got.append(reg[f % 2].copy())
+            renderer.render_async(cam, reg[f % 2], W, H, S, D, frame0=f * S)
+        for f in (2, 3):
+            renderer.wait()
+            got.append(reg[f % 2].copy())
+    finally:
+        for b in reg:
+            renderer.host_unregister(b)
+    for f in range(4):
+        ref, _ = renderer.render(cam, W, H, S, D, frame0=f * S)  # pageable: staged + copied
+        check_exact(got[f], ref)
