@@ -982,8 +982,12 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
                     const uint32_t f = m & RT_MF_FLAGS;
 #ifdef RT_CHECK_BOUNDS
                     RT_IDX(qcount(qp, t ? q1 : q0), RT_MF_CAP, RT_SITE_MFQ);
-                    // a lane without a ray (T0 = +inf) never queues
-                    RT_IDX(f != 0u ? 1u : 0u, live ? 2u : 1u, RT_SITE_DEAD_QUEUE);
+                    // a column without a live ray (T0 = +inf) never queues:
+                    // this lane holds column lane & 31 of half t, the ray of
+                    // lane 32 t + (lane & 31)
+                    RT_IDX(f != 0u ? 1u : 0u,
+                           ((live_mask >> (32u * t + (lane & 31u))) & 1u) ? 2u : 1u,
+                           RT_SITE_DEAD_QUEUE);
                     if (qcount(qp, t ? q1 : q0) >= RT_MF_CAP) qp = t ? q1 : q0;
 #endif
                     // the group index as one opaque SGPR: v_or_b32 (dual-
