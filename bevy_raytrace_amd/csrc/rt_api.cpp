@@ -1095,12 +1095,17 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     // frames (not progressive), an output pixel index the item knows (the
     // image layout: one shard, or RT_FLAG_IMAGE_OUT); the launch's output
     // indices below RT_INDEX_LIMIT
-    const bool direct = tn.direct_out && prog_mode == 0 && !passes.empty() &&
+    // host memory (a registered caller buffer) or another device's image:
+    // system-scope write-through stores and a release per wave (collect)
+    K_.dsys = (out_host || (p.flags & RT_FLAG_IMAGE_OUT)) ? 1u : 0u;
+    // ... and then no direct output from the render kernel: a store that
+    // crosses PCIe or xGMI is acknowledged so late that the wave's next load
+    // wait stalls on it (measured: the reference's 1-spp frame written into a
+    // registered host buffer by the render kernel took 2.8 ms of kernel
+    // instead of 0.77, profiles/r04/direct/); the collect writes those frames
+    const bool direct = tn.direct_out && prog_mode == 0 && !passes.empty() && !K_.dsys &&
                         passes[0].block_begin == 0 && passes[0].nblocks == blocks_total &&
                         (K == 1 || (p.flags & RT_FLAG_IMAGE_OUT));
-    // host memory (a registered caller buffer) or another device's image:
-    // system-scope write-through stores and a release per wave
-    K_.dsys = (out_host || (p.flags & RT_FLAG_IMAGE_OUT)) ? 1u : 0u;
     K_.dstride = (uint32_t)fstride;
     K_.dwhole_blk = blocks_total == 1 ? 1u : 0u;
     K_.dwhole_tail = p.spp == 1 ? 1u : 0u;
@@ -1413,10 +1418,11 @@ int rt_render_async(rt_ctx* ctx, const rt_camera* camera, const rt_params* param
     Frame* f = next_slot(ctx, "rt_render_async");
     if (!f) return RT_ERR_INVALID_ARG;
     const size_t bytes = out_bytes(params);
-    // A registered buffer (rt_host_register) is written by the kernels
-    // themselves through its device-visible address -- whole items as they
-    // finish, during the render (system-scope write-through stores) -- so no
-    // staging buffer and no device->host copy after the render
+    // A registered buffer (rt_host_register) is written by the collect kernel
+    // itself through its device-visible address (system-scope write-through
+    // stores), so no staging buffer and no device->host copy after it: the
+    // frame's PCIe transfer is the collect, which the next frame's render (the
+    // other pending slot's stream) can overlap
     for (const auto& r : ctx->host_regs) {
         const char* lo = (const char*)r.ptr;
         const char* o = (const char*)out_rgba;
