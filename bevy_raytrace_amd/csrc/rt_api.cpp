@@ -144,7 +144,6 @@ struct rt_ctx {
     struct HostReg {
         void* ptr;
         size_t bytes;
-        void* dev;  // its device-visible address (hipHostGetDevicePointer)
     };
     std::vector<HostReg> host_regs;  // rt_host_register'd buffers
 
@@ -923,7 +922,7 @@ int rt_update_materials(rt_ctx* ctx, uint32_t first, const rt_material* material
 // the launch would, then return without enqueueing any work.
 static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params* prm,
                    uint32_t nframes, float4* d_out, hipStream_t stream, int prog_mode = 0,
-                   float prog_total = 0.0f, bool reserve_only = false, bool out_host = false) {
+                   float prog_total = 0.0f, bool reserve_only = false) {
     if ((!cam && !reserve_only) || !prm)
         return fail(ctx, RT_ERR_INVALID_ARG, "camera or params is NULL");
     if (!ctx->has_scene) return fail(ctx, RT_ERR_NO_SCENE, "rt_render before rt_set_scene");
@@ -1095,14 +1094,13 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     // frames (not progressive), an output pixel index the item knows (the
     // image layout: one shard, or RT_FLAG_IMAGE_OUT); the launch's output
     // indices below RT_INDEX_LIMIT
-    // host memory (a registered caller buffer) or another device's image:
-    // system-scope write-through stores and a release per wave (collect)
-    K_.dsys = (out_host || (p.flags & RT_FLAG_IMAGE_OUT)) ? 1u : 0u;
-    // ... and then no direct output from the render kernel: a store that
-    // crosses PCIe or xGMI is acknowledged so late that the wave's next load
-    // wait stalls on it (measured: the reference's 1-spp frame written into a
-    // registered host buffer by the render kernel took 2.8 ms of kernel
-    // instead of 0.77, profiles/r04/direct/); the collect writes those frames
+    // another device's image (RT_FLAG_IMAGE_OUT): system-scope write-through
+    // stores and a release per wave (collect) -- and no direct output from the
+    // render kernel: a store that crosses xGMI or PCIe is acknowledged so late
+    // that the wave's next load wait stalls on it (measured: the reference's
+    // 1-spp frame written into a registered host buffer by the render kernel
+    // took 2.8 ms of kernel instead of 0.77, profiles/r04/direct/)
+    K_.dsys = (p.flags & RT_FLAG_IMAGE_OUT) ? 1u : 0u;
     const bool direct = tn.direct_out && prog_mode == 0 && !passes.empty() && !K_.dsys &&
                         passes[0].block_begin == 0 && passes[0].nblocks == blocks_total &&
                         (K == 1 || (p.flags & RT_FLAG_IMAGE_OUT));
@@ -1418,21 +1416,6 @@ int rt_render_async(rt_ctx* ctx, const rt_camera* camera, const rt_params* param
     Frame* f = next_slot(ctx, "rt_render_async");
     if (!f) return RT_ERR_INVALID_ARG;
     const size_t bytes = out_bytes(params);
-    // A registered buffer (rt_host_register) is written by the collect kernel
-    // itself through its device-visible address (system-scope write-through
-    // stores), so no staging buffer and no device->host copy after it: the
-    // frame's PCIe transfer is the collect, which the next frame's render (the
-    // other pending slot's stream) can overlap
-    for (const auto& r : ctx->host_regs) {
-        const char* lo = (const char*)r.ptr;
-        const char* o = (const char*)out_rgba;
-        if (r.dev && o >= lo && o + bytes <= lo + r.bytes) {
-            float4* dev = (float4*)((char*)r.dev + (o - lo));
-            int rc = enqueue(ctx, *f, camera, params, 1, dev, f->stream, 0, 0.0f, false, true);
-            if (rc) return rc;
-            return commit(ctx, *f, f->stream, nullptr, nullptr, 0);
-        }
-    }
     int rc = ensure(ctx, &f->d_out, &f->out_cap, std::max<size_t>(bytes, 16));
     if (rc) return rc;
     rc = enqueue(ctx, *f, camera, params, 1, f->d_out, f->stream);
@@ -1446,10 +1429,8 @@ int rt_host_register(rt_ctx* ctx, void* ptr, size_t bytes) {
     for (const auto& r : ctx->host_regs)
         if (r.ptr == ptr) return fail(ctx, RT_ERR_INVALID_ARG, "rt_host_register: %p already registered", ptr);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    HIP_TRY(ctx, hipHostRegister(ptr, bytes, hipHostRegisterMapped));
-    void* dev = nullptr;
-    if (hipHostGetDevicePointer(&dev, ptr, 0) != hipSuccess) dev = nullptr;  // (then staged)
-    ctx->host_regs.push_back({ptr, bytes, dev});
+    HIP_TRY(ctx, hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    ctx->host_regs.push_back({ptr, bytes});
     return RT_OK;
 }
 

@@ -146,8 +146,9 @@ struct KParams {
     float4* dout;
     uint32_t dfull, dwhole_blk, dwhole_tail;
     uint32_t dstride;     // float4 pixels per output frame (the image, or the packed rows)
-    uint32_t dsys;        // 1: the output is host memory or another device's image:
-                          // system-scope write-through stores + a release per wave
+    uint32_t dsys;        // 1: the output is another device's image (RT_FLAG_IMAGE_OUT):
+                          // the collect's system-scope write-through stores + a
+                          // release per wave; no direct output then
     uint32_t collect_f0;  // first launch frame rt_collect_kernel folds
 };
 

@@ -226,11 +226,9 @@ __device__ __forceinline__ void render_body(
         if (e & RT_DIRECT_ITEM) {
             const float spp = (float)P.spp;
             const float4 o = make_float4(v.x / spp, v.y / spp, v.z / spp, 1.0f);
-            float4* const dst = P.dout + RT_IDX(e & ~RT_DIRECT_ITEM, P.chk_out, RT_SITE_OUT);
-            if (P.dsys)
-                store_system(dst, o);
-            else
-                *dst = o;
+            // (device-local outputs only: rt_api.cpp turns direct output off
+            // for another device's image)
+            P.dout[RT_IDX(e & ~RT_DIRECT_ITEM, P.chk_out, RT_SITE_OUT)] = o;
         } else {
             block_sums[RT_IDX(e, P.chk_slots, RT_SITE_SLOT)] = v;
         }
@@ -524,10 +522,6 @@ __device__ __forceinline__ void render_body(
 #ifndef RT_NO_SLOT_BUF
     sb_flush();
 #endif
-    if (P.dsys) {  // direct output into host memory / another device's image
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
 
 #ifdef RT_PROFILE
     PROF_MARK(7);

@@ -932,11 +932,10 @@ def test_direct_output_identical(renderer, S, F, flags):
 
 
 @pytest.mark.parametrize("S", [1, 64])
-def test_registered_host_output_written_by_the_kernels(renderer, S):
-    """rt_render_async into a registered host buffer: the kernels write it
-    through its mapped address (system-scope stores; no staging, no copy) --
-    bit-identical to the staged copy into a pageable buffer, for every frame of
-    a run with two renders in flight."""
+def test_registered_host_output_two_in_flight(renderer, S):
+    """rt_render_async into registered host buffers with two renders in
+    flight (the Bevy shim's sequence): every frame bit-identical to a
+    synchronous render into a pageable buffer."""
     sp, mt = arrays(scene.rtiow_final_scene())
     cam = default_camera_block()
     renderer.set_scene(sp, mt)
