@@ -79,7 +79,7 @@ struct Tuning {
     bool prefetch = true;         // waves prefetch their next work chunk
     uint32_t prio_mode = 1;       // s_setprio rotation: 0 off, 1 by iteration, 3 by wall time
     uint32_t prio_shift = 14;     // mode 3 step: 2^prio_shift ticks of 10 ns
-    uint32_t wg_per_cu = 0;       // resident workgroups per CU (0 = occupancy limit)
+    uint32_t wg_per_cu = 0;       // resident workgroups per CU (0 = by the call's size, enqueue)
     int64_t wide_max = -1;        // sphere-parallel threshold (-1 = cost model)
     bool fast_exact = true;       // short correctly-rounded exact test when in domain
     int64_t fail_alloc_after = -1;  // fault injection: device allocations left (-1 = off)
@@ -963,7 +963,26 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     // short path per lane to drain. In samples per pixel:
     const Tuning& tn = ctx->tune;
     const int bpc = (p.flags & RT_FLAG_CULL) ? ctx->blocks_per_cu_c : ctx->blocks_per_cu;
-    const uint64_t lanes = (uint64_t)ctx->cu_count * bpc * RT_BLOCK_THREADS;
+    // Resident workgroups per CU. A small call does better on fewer: with
+    // few samples per lane the launch's ramp and drain dominate, and the
+    // clock runs higher. Measured (tools/grid_probe.py, profiles/r04/grid/,
+    // render-kernel ms at 4 / 3 / 2 / 1 workgroups per CU): 1080p 1 spp
+    // depth 3 0.768 / 0.672 / 0.574 / 0.512; 1080p 1 spp depth 16 1.053 /
+    // 0.953 / 0.867 / 0.981; 4 spp 2.139 / 2.031 / 1.973 / 2.802; 16 spp
+    // 5.51 / 5.36 / 5.67 / 10.2; 64 spp 14.2 / 15.3 / 20.3 / 38.9. By the
+    // call's samples per lane at full occupancy x depth (x): x < 64 -> 1,
+    // < 1024 -> 2, < 4096 -> 3, else the occupancy limit. Knob wg_per_cu
+    // overrides (A/B).
+    uint32_t wg_run = (uint32_t)bpc;
+    {
+        const double x = (double)npix * p.spp * nframes /
+                         ((double)std::max(ctx->cu_count, 1) * std::max(bpc, 1) * RT_BLOCK_THREADS) *
+                         p.max_depth;
+        const uint32_t want = x < 64.0 ? 1u : x < 1024.0 ? 2u : x < 4096.0 ? 3u : (uint32_t)bpc;
+        wg_run = std::max<uint32_t>(1u, std::min<uint32_t>(want, (uint32_t)bpc));
+        if (ctx->tune.wg_per_cu) wg_run = std::min<uint32_t>(ctx->tune.wg_per_cu, (uint32_t)bpc);
+    }
+    const uint64_t lanes = (uint64_t)ctx->cu_count * wg_run * RT_BLOCK_THREADS;
     bool tail_on = tn.tail_split;
     const double* ta = tn.tail;
     auto per_px = [&](double a, uint64_t mult) -> uint64_t {
@@ -1182,10 +1201,7 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     } while (0)
     HIP_TRY_Q(hipEventRecord(f.ev_t0, stream));
     HIP_TRY_Q(hipMemsetAsync(f.d_counters, 0, words_pad * sizeof(uint32_t), stream));
-    // wg_per_cu < occupancy: fewer co-resident waves per SIMD (A/B)
-    const uint32_t wg_per_cu = std::min<uint32_t>(
-        ctx->tune.wg_per_cu ? ctx->tune.wg_per_cu : (uint32_t)bpc, (uint32_t)bpc);
-    const uint32_t grid_full = (uint32_t)(ctx->cu_count * (wg_per_cu ? wg_per_cu : 1));
+    const uint32_t grid_full = (uint32_t)(ctx->cu_count * wg_run);
     if (npix) HIP_TRY_Q(rt_launch_primary(&K_, f.d_pd, stream));
     for (size_t i = 0; i < passes.size(); ++i) {
         const Pass& ps = passes[i];
