@@ -84,7 +84,7 @@ struct Tuning {
     bool fast_exact = true;       // short correctly-rounded exact test when in domain
     int64_t fail_alloc_after = -1;  // fault injection: device allocations left (-1 = off)
     // positive control of the checked build: the bound of one RT_IDX site
-    // (4 sph, 6 mats, 7 slots, 16 output) given as 0, so its first index is
+    // (4 sph, 5 shading records, 7 slots, 16 output) given as 0, so its first index is
     // reported (the product build reads no bound: no effect)
     uint32_t chk_shrink = 0;
     // whole items write their output pixel themselves (KParams::dout); off:
@@ -108,9 +108,12 @@ struct rt_ctx {
     uint32_t n = 0, ngroups = 0, m = 0;
     float4* d_grp = nullptr;        // groups of RT_GROUP=8 spheres, SoA (cx[8], cy[8], cz[8], S[8])
     float4* d_sph = nullptr;        // (cx, cy, cz, r*r)
-    float2* d_sph_rm = nullptr;     // (radius, material bits)
-    rt_material* d_mats = nullptr;
-    size_t grp_cap = 0, sph_cap = 0, sph_rm_cap = 0, mat_cap = 0;
+    // per-sphere shading record, 2 float4: (radius, reflectance bits,
+    // fuzziness, index of refraction), (material colour) -- the sphere's
+    // radius and its material in one place, so shading issues its loads
+    // together (no sphere -> material index -> material chain)
+    float4* d_shd = nullptr;
+    size_t grp_cap = 0, sph_cap = 0, shd_cap = 0;
     std::vector<float4> h_sph, h_grp;  // host mirrors of the packed scene
     std::vector<float> h_S;
     std::vector<float2> h_rm;
@@ -120,10 +123,10 @@ struct rt_ctx {
     uint32_t n_c = 0, ngroups_c = 0, nclusters_c = 0;
     float4* d_grp_c = nullptr;
     float4* d_sph_c = nullptr;
-    float2* d_rm_c = nullptr;
+    float4* d_shd_c = nullptr;      // shading records in the culled order
     float4* d_bnd_c = nullptr;
     uint32_t* d_perm_c = nullptr;
-    size_t grp_c_cap = 0, sph_c_cap = 0, rm_c_cap = 0, bnd_c_cap = 0, perm_c_cap = 0;
+    size_t grp_c_cap = 0, sph_c_cap = 0, shd_c_cap = 0, bnd_c_cap = 0, perm_c_cap = 0;
     // matrix-core filter (RT_MFMA_FILTER builds, build_mfma): f16 A fragments
     bool mf_ok = false;
     bool mf_dirty = false;          // rt_update_spheres: fragments rebuilt by mfma_ready
@@ -253,7 +256,7 @@ static bool tune_set(Tuning& t, const char* name, const char* v) {
     } else if (!strcmp(name, "direct_out")) {
         t.direct_out = x != 0;
     } else if (!strcmp(name, "chk_shrink")) {
-        if (x != 0 && x != 4 && x != 6 && x != 7 && x != 16) return false;
+        if (x != 0 && x != 4 && x != 5 && x != 7 && x != 16) return false;
         t.chk_shrink = (uint32_t)x;
     } else {
         return false;
@@ -331,12 +334,12 @@ void rt_destroy(rt_ctx* ctx) {
     for (const auto& r : ctx->host_regs) hipHostUnregister(r.ptr);
     hipFree(ctx->d_grp);
     hipFree(ctx->d_sph);
-    hipFree(ctx->d_sph_rm);
-    hipFree(ctx->d_mats);
+    hipFree(ctx->d_shd);
+
     hipFree(ctx->d_prog);
     hipFree(ctx->d_grp_c);
     hipFree(ctx->d_sph_c);
-    hipFree(ctx->d_rm_c);
+    hipFree(ctx->d_shd_c);
     hipFree(ctx->d_bnd_c);
     hipFree(ctx->d_perm_c);
     hipFree(ctx->d_mfA);
@@ -376,6 +379,33 @@ static void pack_record_to(const rt_sphere& s, float4& q, float& S, float2& rm) 
 
 static void pack_record(rt_ctx* ctx, uint32_t i, const rt_sphere& s) {
     pack_record_to(s, ctx->h_sph[i], ctx->h_S[i], ctx->h_rm[i]);
+}
+
+// Shading records of n spheres from their (radius, material bits) and the
+// materials (validated: every sphere's index is below mats.size(); a pad
+// record's index 0 with no materials gives zeros -- pads are never shaded).
+static void shade_records(const float2* rm, size_t n, const std::vector<rt_material>& mats,
+                          float4* out) {
+    for (size_t i = 0; i < n; ++i) {
+        uint32_t mi;
+        std::memcpy(&mi, &rm[i].y, 4);
+        rt_material m{};
+        if (mi < mats.size()) m = mats[mi];
+        float refl;
+        std::memcpy(&refl, &m.reflectance, 4);
+        out[2 * i] = make_float4(rm[i].x, refl, m.fuzziness, m.index_of_refraction);
+        out[2 * i + 1] = make_float4(m.color[0], m.color[1], m.color[2], m.color[3]);
+    }
+}
+
+// Upload the shading records of spheres [first, first + count) (quiesced).
+static int upload_shd(rt_ctx* ctx, size_t first, size_t count) {
+    if (!count) return RT_OK;
+    std::vector<float4> rec(2 * count);
+    shade_records(&ctx->h_rm[first], count, ctx->h_mats, rec.data());
+    HIP_TRY(ctx, hipMemcpy(ctx->d_shd + 2 * first, rec.data(), sizeof(float4) * rec.size(),
+                           hipMemcpyHostToDevice));
+    return RT_OK;
 }
 
 // The exact sphere test's short correctly-rounded sqrt/divide forms (rt_math.h)
@@ -613,13 +643,18 @@ static int build_cull(rt_ctx* ctx) {
     cull_layout(ctx->h_sph.data(), ctx->h_S.data(), ctx->h_rm.data(), ctx->n, L);
     int rc = ensure(ctx, &ctx->d_grp_c, &ctx->grp_c_cap, sizeof(float4) * L.nrec);
     if (!rc) rc = ensure(ctx, &ctx->d_sph_c, &ctx->sph_c_cap, sizeof(float4) * L.nrec);
-    if (!rc) rc = ensure(ctx, &ctx->d_rm_c, &ctx->rm_c_cap, sizeof(float2) * L.nrec);
+    if (!rc) rc = ensure(ctx, &ctx->d_shd_c, &ctx->shd_c_cap, 2 * sizeof(float4) * L.nrec);
     if (!rc) rc = ensure(ctx, &ctx->d_bnd_c, &ctx->bnd_c_cap, sizeof(float4) * L.bnd.size());
     if (!rc) rc = ensure(ctx, &ctx->d_perm_c, &ctx->perm_c_cap, sizeof(uint32_t) * L.nrec);
     if (rc) return rc;
     HIP_TRY(ctx, hipMemcpy(ctx->d_grp_c, L.grp.data(), sizeof(float4) * L.nrec, hipMemcpyHostToDevice));
     HIP_TRY(ctx, hipMemcpy(ctx->d_sph_c, L.sph.data(), sizeof(float4) * L.nrec, hipMemcpyHostToDevice));
-    HIP_TRY(ctx, hipMemcpy(ctx->d_rm_c, L.rm.data(), sizeof(float2) * L.nrec, hipMemcpyHostToDevice));
+    {
+        std::vector<float4> rec(2 * (size_t)L.nrec);
+        shade_records(L.rm.data(), L.nrec, ctx->h_mats, rec.data());
+        HIP_TRY(ctx, hipMemcpy(ctx->d_shd_c, rec.data(), sizeof(float4) * rec.size(),
+                               hipMemcpyHostToDevice));
+    }
     if (!L.bnd.empty())
         HIP_TRY(ctx, hipMemcpy(ctx->d_bnd_c, L.bnd.data(), sizeof(float4) * L.bnd.size(),
                                hipMemcpyHostToDevice));
@@ -795,16 +830,12 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n, const rt_mat
     if (rc) return rc;
     rc = ensure(ctx, &ctx->d_grp, &ctx->grp_cap, sizeof(float4) * nrec);
     if (rc) return rc;
-    rc = ensure(ctx, &ctx->d_sph_rm, &ctx->sph_rm_cap, sizeof(float2) * ctx->h_rm.size());
-    if (rc) return rc;
-    rc = ensure(ctx, &ctx->d_mats, &ctx->mat_cap, sizeof(rt_material) * (size_t)m);
+    rc = ensure(ctx, &ctx->d_shd, &ctx->shd_cap, 2 * sizeof(float4) * ctx->h_rm.size());
     if (rc) return rc;
     HIP_TRY(ctx, hipMemcpy(ctx->d_sph, ctx->h_sph.data(), sizeof(float4) * nrec, hipMemcpyHostToDevice));
     HIP_TRY(ctx, hipMemcpy(ctx->d_grp, ctx->h_grp.data(), sizeof(float4) * nrec, hipMemcpyHostToDevice));
-    HIP_TRY(ctx, hipMemcpy(ctx->d_sph_rm, ctx->h_rm.data(), sizeof(float2) * ctx->h_rm.size(),
-                           hipMemcpyHostToDevice));
-    if (m)
-        HIP_TRY(ctx, hipMemcpy(ctx->d_mats, materials, sizeof(rt_material) * m, hipMemcpyHostToDevice));
+    rc = upload_shd(ctx, 0, ctx->h_rm.size());
+    if (rc) return rc;
     ctx->n = n;
     ctx->ngroups = ngroups;
     ctx->m = m;
@@ -872,8 +903,8 @@ int rt_update_spheres(rt_ctx* ctx, uint32_t first, const rt_sphere* spheres, uin
     if (rc) return rc;
     HIP_TRY(ctx, hipMemcpy(ctx->d_sph + first, &ctx->h_sph[first], sizeof(float4) * count,
                            hipMemcpyHostToDevice));
-    HIP_TRY(ctx, hipMemcpy(ctx->d_sph_rm + first, &ctx->h_rm[first], sizeof(float2) * count,
-                           hipMemcpyHostToDevice));
+    rc = upload_shd(ctx, first, count);
+    if (rc) return rc;
     HIP_TRY(ctx, hipMemcpy(ctx->d_grp + RT_GROUP * g0, &ctx->h_grp[RT_GROUP * g0],
                            sizeof(float4) * RT_GROUP * (g1 - g0), hipMemcpyHostToDevice));
     ctx->scene_fast = scene_fast_ok(ctx);
@@ -900,8 +931,12 @@ int rt_update_materials(rt_ctx* ctx, uint32_t first, const rt_material* material
     std::copy(materials, materials + count, ctx->h_mats.begin() + first);
     rc = quiesce(ctx);
     if (rc) return rc;
-    HIP_TRY(ctx, hipMemcpy(ctx->d_mats + first, materials, sizeof(rt_material) * count,
-                           hipMemcpyHostToDevice));
+    // every sphere's shading record carries its material: all are rebuilt
+    // (O(N) on the host, 32 B per sphere), the culled order's at the next
+    // culled call
+    rc = upload_shd(ctx, 0, ctx->h_rm.size());
+    if (rc) return rc;
+    ctx->cull_dirty = true;
     return RT_OK;
 }
 
@@ -1128,11 +1163,10 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     K_.dwhole_tail = p.spp == 1 ? 1u : 0u;
     // the buffers' sizes (RT_CHECK_BOUNDS builds check every index against them)
     K_.chk_nsph = (uint32_t)((cull ? ctx->sph_c_cap : ctx->sph_cap) / sizeof(float4));
-    K_.chk_nrm = (uint32_t)((cull ? ctx->rm_c_cap : ctx->sph_rm_cap) / sizeof(float2));
-    K_.chk_nmat = ctx->m;
+    K_.chk_nrm = (uint32_t)((cull ? ctx->shd_c_cap : ctx->shd_cap) / (2 * sizeof(float4)));
     K_.chk_slots = f.bs_cap / sizeof(float4);
     if (tn.chk_shrink == 4) K_.chk_nsph = 0;
-    if (tn.chk_shrink == 6) K_.chk_nmat = 0;
+    if (tn.chk_shrink == 5) K_.chk_nrm = 0;
     if (tn.chk_shrink == 7) K_.chk_slots = 0;
 #ifdef RT_MFMA_FILTER
     if (!cull && ctx->mf_ok && !(p.flags & RT_FLAG_VALU_FILTER)) {
@@ -1269,7 +1303,7 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         HIP_TRY_Q(hipEventRecord(f.ev[2 * i], stream));
         HIP_TRY_Q(rt_launch_render(&K_, cull ? ctx->d_grp_c : ctx->d_grp,
                                       cull ? ctx->d_sph_c : ctx->d_sph,
-                                      cull ? ctx->d_rm_c : ctx->d_sph_rm, ctx->d_mats, f.d_pd,
+                                      cull ? ctx->d_shd_c : ctx->d_shd, f.d_pd,
                                       f.d_block_sums,
                                       f.d_counters + RT_CNT_WORK_OFFSET + i,
                                       reinterpret_cast<unsigned long long*>(f.d_counters),

@@ -224,8 +224,7 @@ __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint
 // Every lane performs exactly the reference's op sequence for its case.
 __device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, float t,
                                       const float4* __restrict__ sph,
-                                      const float2* __restrict__ sph_rm,
-                                      const rt_material* __restrict__ mats) {
+                                      const float4* __restrict__ shd) {
     const bool miss = hi < 0;
     if (!miss && st.bounce == P.max_depth - 1) {  // shade.wgsl:236-238
         st.color = mk(0.0f, 0.0f, 0.0f);
@@ -240,10 +239,14 @@ __device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, f
     float fuzz, ior;
     int refl = -1;
     if (!miss) {
+        // the centre (exact-test record) and the shading record (radius, the
+        // material's reflectance / fuzziness / index of refraction, colour):
+        // three independent loads (rt_api.cpp shade_records)
         const float4 s = sph[RT_IDX(hi, P.chk_nsph, RT_SITE_SPH)];
-        const float2 rm = sph_rm[RT_IDX(hi, P.chk_nrm, RT_SITE_RM)];
-        const float radius = rm.x;
-        const uint32_t mi = __float_as_uint(rm.y);
+        const uint32_t r = RT_IDX((uint32_t)hi, P.chk_nrm, RT_SITE_RM);
+        const float4 a = shd[2 * r];
+        mc = shd[2 * r + 1];
+        const float radius = a.x;
         pos = add(st.o, scale(st.d, t));
         const v3 q = sub(pos, mk(s.x, s.y, s.z));
         nrm = normalize_x(div3_x(q, radius));
@@ -252,11 +255,9 @@ __device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, f
             nrm = neg(nrm);
             front = false;
         }
-        const rt_material& m = mats[RT_IDX(mi, P.chk_nmat, RT_SITE_MAT)];
-        refl = m.reflectance;
-        mc = *reinterpret_cast<const float4*>(m.color);
-        fuzz = m.fuzziness;
-        ior = m.index_of_refraction;
+        refl = __float_as_int(a.y);
+        fuzz = a.z;
+        ior = a.w;
     }
     // ---- pre-normalize: metal normalize(reflect(d, n)) (shade.wgsl:140),
     //      dielectric unit_dir = normalize(d) (shade.wgsl:169)

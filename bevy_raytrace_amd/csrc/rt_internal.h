@@ -129,8 +129,7 @@ struct KParams {
     // RT_CHECK_BOUNDS build checks every computed index against (rt_kernels.hip
     // RT_IDX; the product build reads none of them).
     uint32_t chk_nsph;   // sph / grp records (padded list)
-    uint32_t chk_nrm;    // sph_rm records
-    uint32_t chk_nmat;   // materials
+    uint32_t chk_nrm;    // shading records (2 float4 each)
     uint32_t chk_items;  // work items of the launch (main_all + tail_items)
     uint64_t chk_slots;  // block_sums slots
     uint64_t chk_out;    // float4 pixels behind the launch's output pointer
@@ -164,7 +163,7 @@ __host__ __device__ inline uint32_t rt_shard_block(uint32_t j, uint32_t K, uint3
 
 extern "C" {
 hipError_t rt_launch_render(const KParams* P, const float4* grp, const float4* sph,
-                            const float2* sph_rm, const rt_material* mats, const float4* pd,
+                            const float4* shd, const float4* pd,
                             float4* block_sums,
                             uint32_t* work_counter, unsigned long long* seg_counter, uint32_t grid,
                             hipStream_t stream);

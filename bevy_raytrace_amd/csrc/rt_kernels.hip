@@ -80,8 +80,7 @@ enum RtSite : uint32_t {
     RT_SITE_TAB = 2,         // pixel table tab[k], k < npix
     RT_SITE_ACC_IN = 3,      // acc_in[p] of a later pass, p < npix
     RT_SITE_SPH = 4,         // sph[hi] in shade
-    RT_SITE_RM = 5,          // sph_rm[hi] in shade
-    RT_SITE_MAT = 6,         // mats[mi] in shade
+    RT_SITE_RM = 5,          // shd[2 hi], shd[2 hi + 1] (shading record) in shade
     RT_SITE_SLOT = 7,        // block_sums slot written by the render kernel
     RT_SITE_SLOTBUF = 8,     // per-wave slot buffer entry
     RT_SITE_MFQ = 9,         // matrix-core queue append (entries per lane and half)
@@ -168,7 +167,7 @@ __device__ __forceinline__ void store_system(float4* p, float4 v) {
 template <bool CULL>
 __device__ __forceinline__ void render_body(
     const KParams& P, const float4* grp, const float4* __restrict__ sph,
-    const float2* __restrict__ sph_rm, const rt_material* __restrict__ mats,
+    const float4* __restrict__ shd,
     const PixelEntry* __restrict__ tab, float4* __restrict__ block_sums,
     uint32_t* __restrict__ work_counter,
     unsigned long long* __restrict__ seg_counter, unsigned long long* __restrict__ dbg) {
@@ -427,7 +426,7 @@ __device__ __forceinline__ void render_body(
             if (sh == 0) break;
             segs = __builtin_amdgcn_readfirstlane(segs + (uint32_t)__popcll(sh));
             if (shading) {
-                const bool done = shade(P, st, hi, t, sph, sph_rm, mats);
+                const bool done = shade(P, st, hi, t, sph, shd);
                 shading = false;
                 if (done) {
                     // path finished: accumulate (collect.wgsl:115-120, blocked);
@@ -568,20 +567,20 @@ __device__ __forceinline__ void render_body(
 
 __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_render_kernel(
     KParams P, const float4* grp, const float4* __restrict__ sph,
-    const float2* __restrict__ sph_rm, const rt_material* __restrict__ mats,
+    const float4* __restrict__ shd,
     const PixelEntry* __restrict__ tab, float4* __restrict__ block_sums,
     uint32_t* __restrict__ work_counter,
     unsigned long long* __restrict__ seg_counter, unsigned long long* __restrict__ dbg) {
-    render_body<false>(P, grp, sph, sph_rm, mats, tab, block_sums, work_counter, seg_counter, dbg);
+    render_body<false>(P, grp, sph, shd, tab, block_sums, work_counter, seg_counter, dbg);
 }
 
 __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD_CULL) void rt_render_cull_kernel(
     KParams P, const float4* grp, const float4* __restrict__ sph,
-    const float2* __restrict__ sph_rm, const rt_material* __restrict__ mats,
+    const float4* __restrict__ shd,
     const PixelEntry* __restrict__ tab, float4* __restrict__ block_sums,
     uint32_t* __restrict__ work_counter,
     unsigned long long* __restrict__ seg_counter, unsigned long long* __restrict__ dbg) {
-    render_body<true>(P, grp, sph, sph_rm, mats, tab, block_sums, work_counter, seg_counter, dbg);
+    render_body<true>(P, grp, sph, shd, tab, block_sums, work_counter, seg_counter, dbg);
 }
 
 // Pixel table, once per frame: for the k-th pixel of the processing order
@@ -803,7 +802,7 @@ __global__ void rt_assemble_kernel(const float4* __restrict__ gathered, uint32_t
 extern "C" {
 
 hipError_t rt_launch_render(const KParams* P, const float4* grp, const float4* sph,
-                            const float2* sph_rm, const rt_material* mats, const float4* pd,
+                            const float4* shd, const float4* pd,
                             float4* block_sums, uint32_t* work_counter,
                             unsigned long long* seg_counter, uint32_t grid, hipStream_t stream) {
 #ifdef RT_SPHERES_LDS
@@ -813,11 +812,11 @@ hipError_t rt_launch_render(const KParams* P, const float4* grp, const float4* s
 #endif
     if (P->bnd)
         hipLaunchKernelGGL(rt_render_cull_kernel, dim3(grid), dim3(RT_BLOCK_THREADS), dyn, stream,
-                           *P, grp, sph, sph_rm, mats, reinterpret_cast<const PixelEntry*>(pd),
+                           *P, grp, sph, shd, reinterpret_cast<const PixelEntry*>(pd),
                            block_sums, work_counter, seg_counter, seg_counter + 2);
     else
         hipLaunchKernelGGL(rt_render_kernel, dim3(grid), dim3(RT_BLOCK_THREADS), dyn, stream, *P,
-                           grp, sph, sph_rm, mats, reinterpret_cast<const PixelEntry*>(pd),
+                           grp, sph, shd, reinterpret_cast<const PixelEntry*>(pd),
                            block_sums, work_counter, seg_counter, seg_counter + 2);
     return hipGetLastError();
 }

@@ -879,7 +879,7 @@ def test_failed_scene_upload_leaves_no_scene():
         check_exact(img, O.render(cam, big, bmt, 32, 18, 2, 4)[0])
 
 
-@pytest.mark.parametrize("site", [4, 6, 7, 16])
+@pytest.mark.parametrize("site", [4, 5, 7, 16])
 def test_checked_build_reports_an_out_of_range_index(renderer, site):
     """Positive control of the bounds-checked build (librt_hip_checked.so,
     `--rt-lib`): with one site's bound given as 0 (knob chk_shrink) the render
