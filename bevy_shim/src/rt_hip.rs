@@ -81,6 +81,9 @@ extern "C" {
     pub fn rt_host_unregister(ctx: *mut rt_ctx, ptr: *mut c_void) -> c_int;
     pub fn rt_intersect(ctx: *mut rt_ctx, rays: *const f32, n: u32, hit_index: *mut i32,
                         hit_t: *mut f32) -> c_int;
+    // multi-GPU only: system-scope acquire on the image owner's device
+    // before it reads rows other ranks wrote with RT_FLAG_IMAGE_OUT
+    pub fn rt_acquire(ctx: *mut rt_ctx, stream: *mut c_void) -> c_int;
     pub fn rt_last_error(ctx: *const rt_ctx) -> *const c_char;
 }
 
