@@ -19,7 +19,7 @@ max over ranks. value = algorithmic ray segments of the whole frame (all ranks)
 per second, every segment traced (primary-hit reuse off for the headline;
 its frame time is reported separately as `primary_reuse`).
 
-Roofline: SIMD issue, the resource the kernel executes on (DESIGN.md 4.7):
+Roofline: SIMD issue, the resource the kernel executes on (DESIGN.md §5):
 the render kernel's issue cycles per launch (rocprofv3 PMC record in
 profiles/pmc_traffic.json: 4 per VALU instruction, 2 per 32-bit integer one,
 8 per MFMA) over that launch's duration (HIP events on the stream the kernel
@@ -608,7 +608,7 @@ def main():
         # algorithm's 18 x N fp32 flops per traced segment at this rate over
         # the 157.3 TF fp32 peak -- above 1 because the kernel does not execute
         # them (the filter runs as f16 MFMA tiles, the exact fp32 test only on
-        # candidates, DESIGN.md 4.7)
+        # candidates, DESIGN.md 4.2)
         "fp32_algorithm_tflops": round(achieved, 3),
         "fp32_algorithm_ratio": round(achieved / PEAK_FP32_TFLOPS, 4),
         "fp32_algorithm_basis": ("traced segments x 18 x N_spheres (intersect.wgsl:97-102, SURVEY "

@@ -204,7 +204,7 @@ __device__ __forceinline__ f2 filter2(f2 cx, f2 cy, f2 cz, f2 S, const RayF& r) 
 // matrix-core filter on the same SIMDs (tools/isect_diag.py: ~10-100 of
 // 400,000 adversarial rays per launch, every one in a VALU-walk wave; the
 // same asm without op_sel, or the compiler's filter2, exact over 8 launches;
-// DESIGN.md §4.7).
+// DESIGN.md §4.2).
 struct RayP {
     f2 dx, dy, dz, k1, ox, oy, oz;  // (-dn, k1, o2) duplicated in both halves
     float T;
@@ -629,7 +629,7 @@ __device__ __forceinline__ uint32_t lanemask_lt_count(uint64_t m) {
 
 
 #ifdef RT_MFMA_FILTER
-// ---- the filter on the matrix cores (RT_MFMA_FILTER builds; DESIGN.md §4.7) ----
+// ---- the filter on the matrix cores (RT_MFMA_FILTER builds; DESIGN.md §4.2) ----
 // The VALU filter's value H = hb^2 + S + o2.c (hb = k1 + e.c, e = -dn) is a
 // quadratic form in the sphere centre, so with the ray's k1^2 moved into its
 // threshold it is ONE dot product of a sphere row and a ray column:
@@ -784,7 +784,7 @@ __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, ui
 // Integer ORs of the bits in C++ (no canonicalisation as a float max would
 // need), so hipcc itself places the wait states between the MFMA that writes
 // V and the first VALU reading it (round 2 had this in inline asm opening
-// with a hand-placed s_nop 11, DESIGN.md 4.7 "hazards").
+// with a hand-placed s_nop 11).
 // The 3-input ORs are v_bitop3_b32 (function 0xFE): gfx950 dual-issues it
 // like a 2-input v_or_b32 (0.58 quad-cycles per instruction at 4 waves per
 // SIMD), where v_or3_b32 -- which hipcc picks for a | b | c -- holds the SIMD

@@ -8,14 +8,18 @@
 // (ray, throughput, seed, sample-block sum) in VGPRs.
 //
 // Work decomposition: a launch covers F frames; its work
-// queue holds (frame, pixel, sample block of RT_SAMPLE_BLOCK samples) *block
-// items* followed by single-sample *tail items* (so no lane holds a long item
-// when the queue runs dry). Waves take chunks of items with one atomic
-// (prefetched a chunk ahead); a lane whose path ends starts the next sample of
-// its item, a lane whose item ends stores its block sum (or, for a tail item,
-// each sample's colour) and takes the next item (wave-ballot refill), so lanes
-// do not idle while the wave's longest path finishes. rt_collect_kernel folds
-// a pixel's slots in sample order -- the oracle's summation order.
+// queue is pixel-major and holds three regions: *pixel items* (one per
+// (frame, pixel), covering the frame's sample blocks of RT_SAMPLE_BLOCK
+// samples in the region, folded in block order in LDS), then *block items*
+// (pixel, one block), then *tail items* (2-sample, then single-sample; knob
+// `tail`, default 0,1,1), so no lane holds a long item when the queue runs
+// dry. Waves take chunks of items with one atomic (prefetched a chunk ahead);
+// a lane whose path ends starts the next sample of its item, a lane whose item
+// ends stores its slot (through a per-wave LDS buffer) and takes the next
+// item (wave-ballot refill), so lanes do not idle while the wave's longest
+// path finishes. An item covering every sample of its (frame, pixel) writes
+// the output pixel itself (direct output); rt_collect_kernel folds the other
+// frames' slots in block / sample order -- the oracle's summation order.
 //
 // Intersection (the hot loop, intersect.wgsl:133-143): every sphere of the
 // list is tested for every live ray (brute force), in two stages. A
@@ -23,7 +27,7 @@
 // matrix cores, one 32-term f16 hi/lo dot product per pair -- two chained
 // v_mfma_f32_32x32x16_f16 per 32-sphere x 32-ray tile give V = T0 - H0 and a
 // pair is a candidate iff V < 0 (rt_dev_intersect.h intersect_world_mfma,
-// DESIGN.md 4.7); the culled list, and waves with a ray outside the f16
+// DESIGN.md 4.2); the culled list, and waves with a ray outside the f16
 // split's range, run the same test as packed fp32 FMAs over groups of 8
 // spheres read with scalar loads (filter8):
 //   H - T = hb^2 + r^2 - (1 - m)|o - c|^2 + mu (|o|^2 + |c|^2),  hb = dn.(o - c)

@@ -152,14 +152,14 @@ typedef struct rt_params {
 #define RT_FLAG_THIN_LENS 0x4u
 /* RT_FLAG_CULL: trace against the culled list -- the spheres permuted into
  * spatial groups of 8 with a conservative bounding sphere per group, so a
- * wave filters only the groups near some lane's ray (DESIGN.md §4.6). Hits,
+ * wave filters only the groups near some lane's ray (DESIGN.md §4.3). Hits,
  * segment counts and images are identical to the brute-force walk of
  * intersect.wgsl:133-143 (ties still go to the lower sphere index); only the
  * work differs, so it is opt-in like the other non-reference modes. */
 #define RT_FLAG_CULL      0x8u
 /* RT_FLAG_VALU_FILTER: run the brute-force walk's conservative sphere filter
  * as packed fp32 FMAs on the vector ALUs instead of the default f16 hi/lo
- * tiles on the matrix cores (DESIGN.md §4.7; the matrix-core filter is used
+ * tiles on the matrix cores (DESIGN.md §4.2; the matrix-core filter is used
  * whenever the scene fits its range). Both filters only decide which spheres
  * get the reference's exact test, so hits, segment counts and images are
  * identical; the flag exists for A/B timing and for checking one filter

@@ -131,7 +131,7 @@ def test_matches_reference_intersect_world(renderer, path, flags):
 @pytest.mark.parametrize("fast", [True, False], ids=["short_math", "ieee"])
 def test_valu_and_matrix_waves_side_by_side(renderer, fast):
     """Round 2 saw VALU-walk waves miss hits only while other waves of the same
-    kernel ran the matrix-core walk (hazards). Here every other
+    kernel ran the matrix-core walk. Here every other
     wave of 64 rays holds one ray whose origin is outside the f16 split's range
     (|o| > 2^12: that wave takes the packed VALU filter) and the rest are near
     (the matrix-core filter), so the two walks run side by side on every CU;

@@ -25,7 +25,7 @@ following control flow backwards through every predecessor of a block:
       may select a VGPR source's halves with op_sel / op_sel_hi (anything but
       op_sel:0, op_sel_hi:1 on a VGPR operand). Measured on gfx950: such
       half-broadcasts return wrong values while other waves of the kernel run
-      MFMAs (tools/ubench/opsel_mfma.hip, tools/isect_diag.py; DESIGN.md 4.8).
+      MFMAs (tools/ubench/opsel_mfma.hip, tools/isect_diag.py; DESIGN.md 4.4).
       hipcc itself emits these forms for f2{x, x} operands, so the rule is
       checked on compiler code as well as on inline asm.
 

@@ -1,4 +1,4 @@
-"""Diagnostic builds for the op_sel finding (hazards): the
+"""Diagnostic builds for the op_sel finding: the
 current tree with filter8's ray constants read through op_sel / op_sel_hi
 half-broadcasts of 4 VGPR pairs (round 2's first form) instead of 7
 duplicated pairs, in two register forms:

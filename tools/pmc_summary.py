@@ -56,12 +56,13 @@ if "FETCH_SIZE" in rk and "WRITE_SIZE" in rk:
              "source": f"profiles/{tag}_pmc_{wl}.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
                        "separate passes; FETCH_SIZE x2 per gfx950 correction, x1024 KB->B)",
              "note": f"per {fpl}-frame render launch"}
-    # VALU issue occupancy of the same launch (separate --pmc pass). gfx950:
-    # SQ_ACTIVE_INST_VALU counts one quad-cycle per VALU instruction whatever
-    # its issue cost; v_pk_fma_f32 / v_fma_f32 / v_max3_f32 issue in ~4 cycles
-    # per wave64 instruction, 32-bit integer ops in ~2 (tools/ubench/valu_busy,
-    # profiles/r02_valu_calibration.txt), so AMD's VALUBusy (the first form)
-    # can exceed 1; the second prices INT32 ops at 2 cycles.
+    # VALU occupancy of the same launch (separate --pmc pass), two historical
+    # forms kept for comparison with rounds 1-3: AMD's VALUBusy (one quad-cycle
+    # per counted SQ_ACTIVE_INST_VALU, which ignores gfx950's dual issue and
+    # can exceed 1) and round 3's price form (every non-INT32 op 4 cycles,
+    # INT32 2). Neither is the roofline: the measured SIMD-issue busy below
+    # subtracts the dual-issued quad-cycles (SQ_ACTIVE_INST_VALU2) instead of
+    # pricing by class (profiles/r04/valu_forms/table.txt).
     if rk.get("SQ_ACTIVE_INST_VALU") and rk.get("GRBM_GUI_ACTIVE"):
         simd_cycles = 1024 * rk["GRBM_GUI_ACTIVE"] / 8
         ent = d[wl]
