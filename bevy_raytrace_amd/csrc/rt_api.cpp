@@ -752,7 +752,7 @@ static int build_mfma(rt_ctx* ctx) {
     int sq = 0;
     while (qmax * std::ldexp(1.0, -sq) > 0x1p14) ++sq;  // <= 10 for |c| <= 2^12
     const uint32_t nblk = (n + 31) / 32;
-    std::vector<uint16_t> h((size_t)nblk * 2 * 64 * 8);
+    std::vector<uint16_t> h((size_t)nblk * RT_MF_BLK * 8);
     static const int QA[6] = {0, 1, 2, 0, 0, 1}, QB[6] = {0, 1, 2, 1, 2, 2};
     for (uint32_t b = 0; b < nblk; ++b)
         for (uint32_t l = 0; l < 64; ++l) {
@@ -779,8 +779,13 @@ static int build_mfma(rt_ctx* ctx) {
                 row[29] = f16_bits(-INFINITY);
             }
             row[27] = row[28] = f16_bits(1.0);  // against the ray's T0 hi, lo
-            for (int half = 0; half < 2; ++half)  // A0: K 0..15, A1: K 16..31
-                std::memcpy(&h[(((size_t)b * 2 + half) * 64 + l) * 8], &row[16 * half + 8 * hh], 16);
+            // A0 (K 0..15) of every lane at entry l; A1 (K 16..31) of lanes
+            // 32..63 at entry 64 + (l - 32). Lanes 0..31 of A1 hold K 16..23 =
+            // the hi parts again, equal to their A0 (K 0..7): the kernel reads
+            // A0's entry for them (rt_dev_intersect.h intersect_world_mfma)
+            uint16_t* blk = &h[(size_t)b * RT_MF_BLK * 8];
+            std::memcpy(&blk[(size_t)l * 8], &row[8 * hh], 16);
+            if (hh) std::memcpy(&blk[(size_t)(64 + l - 32) * 8], &row[16 + 8], 16);
         }
     int rc = ensure(ctx, &ctx->d_mfA, &ctx->mfA_cap, h.size() * sizeof(uint16_t));
     if (rc) return rc;

@@ -1005,17 +1005,22 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
         }
     };
     // blocks in pairs: the next block's fragments load while this one runs,
-    // into the other register set (no fragment copies per block); block p's
-    // fragments at mfA + 128 p (uniform base) + lane
-    uint4 a0 = mfA[lane], a1 = mfA[64u + lane];
+    // into the other register set (no fragment copies per block). Block p's
+    // fragments at mfA + RT_MF_BLK p (uniform base): A0 (K 0..15) for the 64
+    // lanes, then A1 (K 16..31) for lanes 32..63 only -- lanes 0..31 hold K
+    // 16..23 of A1, the sphere's hi parts again (= their K 0..7 of A0), so
+    // they load their A0 entry a second time (the same cache lines, no new
+    // bytes): 1.5 KB per block instead of 2 (rt_api.cpp build_mfma).
+    const uint32_t off1 = lane < 32u ? lane : lane + 32u;
+    uint4 a0 = mfA[lane], a1 = mfA[off1];
     uint32_t b = 0;
     for (; b + 2u <= nblk; b += 2u) {
-        const uint4* p1 = mfA + (size_t)(b + 1u) * 128u;
-        const uint4 n0 = p1[lane], n1 = p1[64u + lane];
+        const uint4* p1 = mfA + (size_t)(b + 1u) * RT_MF_BLK;
+        const uint4 n0 = p1[lane], n1 = p1[off1];
         block(b, a0, a1);
-        const uint4* p2 = mfA + (size_t)(b + 2u < nblk ? b + 2u : b + 1u) * 128u;
+        const uint4* p2 = mfA + (size_t)(b + 2u < nblk ? b + 2u : b + 1u) * RT_MF_BLK;
         a0 = p2[lane];
-        a1 = p2[64u + lane];
+        a1 = p2[off1];
         block(b + 1u, n0, n1);
     }
     if (b < nblk) block(b, a0, a1);
