@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
+#include <functional>
 #include <vector>
 
 #include "rt_internal.h"
@@ -90,6 +91,9 @@ struct Tuning {
     // whole items write their output pixel themselves (KParams::dout); off:
     // every frame through the slots and rt_collect_kernel (same bits)
     bool direct_out = true;
+    // the matrix-core walk skips the 32-sphere blocks whose bound no ray of
+    // the half-wave passes (MfScene::B); off: every block (same bits)
+    bool mf_cull = true;
 };
 
 struct rt_ctx {
@@ -135,6 +139,12 @@ struct rt_ctx {
     float mf_abs = 0.0f;  // absolute margin of the threshold, 2^(sq - 20)
     uint4* d_mfA = nullptr;
     size_t mfA_cap = 0;
+    // the walk's spatial order (cull_layout's): block-bound fragments, the
+    // records the drain reads, and the walk position -> original index map
+    uint4* d_mfB = nullptr;
+    float4* d_mf_sph = nullptr;
+    uint32_t* d_mf_perm = nullptr;
+    size_t mfB_cap = 0, mf_sph_cap = 0, mf_perm_cap = 0;
 
     // frames in flight: RT_MAX_PENDING slots of per-frame work buffers, each
     // with its own stream, so frame i+1 can start while frame i drains
@@ -255,6 +265,8 @@ static bool tune_set(Tuning& t, const char* name, const char* v) {
         t.fail_alloc_after = (int64_t)x;
     } else if (!strcmp(name, "direct_out")) {
         t.direct_out = x != 0;
+    } else if (!strcmp(name, "mf_cull")) {
+        t.mf_cull = x != 0;
     } else if (!strcmp(name, "chk_shrink")) {
         if (x != 0 && x != 4 && x != 5 && x != 7 && x != 16) return false;
         t.chk_shrink = (uint32_t)x;
@@ -343,6 +355,9 @@ void rt_destroy(rt_ctx* ctx) {
     hipFree(ctx->d_bnd_c);
     hipFree(ctx->d_perm_c);
     hipFree(ctx->d_mfA);
+    hipFree(ctx->d_mfB);
+    hipFree(ctx->d_mf_sph);
+    hipFree(ctx->d_mf_perm);
     for (Frame& f : ctx->fr) {
         hipFree(f.d_block_sums);
         hipFree(f.d_acc);
@@ -432,7 +447,7 @@ static void pack_group(rt_ctx* ctx, size_t g) {
 
 // ---- culled list (RT_FLAG_CULL) ---------------------------------------------
 // The spheres permuted into spatial groups of RT_GROUP (large spheres first, in
-// groups of their own; the rest in Morton order of their centres), clusters of
+// groups of their own; the rest in k-d order of their centres), clusters of
 // 8 consecutive groups, supers of 8 clusters, and per group and per cluster a
 // bounding sphere (C, R) stored in the group layout -- SoA (Cx[8], Cy[8],
 // Cz[8], S_B[8]) per super (its clusters) and per cluster (its groups) -- so
@@ -472,15 +487,6 @@ struct CullLayout {
     std::vector<float2> rm;
 };
 
-static uint32_t morton_spread10(uint32_t v) {
-    v &= 0x3FFu;
-    v = (v | (v << 16)) & 0x030000FFu;
-    v = (v | (v << 8)) & 0x0300F00Fu;
-    v = (v | (v << 4)) & 0x030C30C3u;
-    v = (v | (v << 2)) & 0x09249249u;
-    return v;
-}
-
 static void pack_group_soa(const float4* q, const float* sg, float4* o) {
     o[0] = make_float4(q[0].x, q[1].x, q[2].x, q[3].x);
     o[1] = make_float4(q[4].x, q[5].x, q[6].x, q[7].x);
@@ -518,39 +524,42 @@ static void cull_layout(const float4* sph, const float* S, const float2* rm, uin
         thr = 4.0 * radii[radii.size() / 2];
     }
     std::vector<uint32_t> big, rest;
-    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (uint32_t i = 0; i < n; ++i) {
-        if (!finite_rec(i) || std::sqrt((double)sph[i].w) > thr) {
-            big.push_back(i);
-            continue;
-        }
-        rest.push_back(i);
-        const double c[3] = {sph[i].x, sph[i].y, sph[i].z};
-        for (int k = 0; k < 3; ++k) {
-            lo[k] = std::min(lo[k], c[k]);
-            hi[k] = std::max(hi[k], c[k]);
-        }
+        if (!finite_rec(i) || std::sqrt((double)sph[i].w) > thr) big.push_back(i);
+        else rest.push_back(i);
     }
-    std::vector<std::pair<uint32_t, uint32_t>> key;  // (Morton code, index)
-    key.reserve(rest.size());
-    for (uint32_t i : rest) {
-        const double c[3] = {sph[i].x, sph[i].y, sph[i].z};
-        uint32_t code = 0;
-        for (int k = 0; k < 3; ++k) {
-            const double ext = hi[k] - lo[k];
-            uint32_t qk = 0;
-            if (ext > 0) {
-                const double t = (c[k] - lo[k]) / ext * 1024.0;
-                qk = t >= 1023.0 ? 1023u : (t <= 0 ? 0u : (uint32_t)t);
+    // the rest in k-d order: split the box's longest axis at a multiple of
+    // 64 / 32 / 8 positions near the median (clusters, matrix-core blocks and
+    // groups stay whole subtrees), leaves of <= 8 sorted along their longest
+    // axis -- compact groups, blocks and clusters (the matrix-core walk's block
+    // bounds: radius ~3.8 vs 4-11 in Morton order for RTIOW's small spheres)
+    std::vector<uint32_t> kd(rest);
+    auto centre = [&](uint32_t i, int a) { return (double)(a == 0 ? sph[i].x : a == 1 ? sph[i].y : sph[i].z); };
+    std::function<void(size_t, size_t)> split = [&](size_t b, size_t e) {
+        const size_t n2 = e - b;
+        if (n2 <= 1) return;
+        double blo[3] = {INFINITY, INFINITY, INFINITY}, bhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (size_t p = b; p < e; ++p)
+            for (int a = 0; a < 3; ++a) {
+                blo[a] = std::min(blo[a], centre(kd[p], a));
+                bhi[a] = std::max(bhi[a], centre(kd[p], a));
             }
-            code |= morton_spread10(qk) << k;
-        }
-        key.emplace_back(code, i);
-    }
-    std::sort(key.begin(), key.end());
+        int ax = 0;
+        for (int a = 1; a < 3; ++a)
+            if (bhi[a] - blo[a] > bhi[ax] - blo[ax]) ax = a;
+        std::stable_sort(kd.begin() + b, kd.begin() + e,
+                         [&](uint32_t x, uint32_t y) { return centre(x, ax) < centre(y, ax); });
+        if (n2 <= RT_GROUP) return;
+        const size_t unit = n2 > 64 ? 64 : (n2 > 32 ? 32 : RT_GROUP);
+        size_t cut = std::max(unit, (size_t)std::llround((double)n2 / 2.0 / (double)unit) * unit);
+        if (cut >= n2) cut = (n2 / 2 + RT_GROUP - 1) / RT_GROUP * RT_GROUP;
+        split(b, b + cut);
+        split(b + cut, e);
+    };
+    split(0, kd.size());
     std::vector<uint32_t> order = big;
     while (order.size() % RT_GROUP) order.push_back(0xFFFFFFFFu);
-    for (const auto& kv : key) order.push_back(kv.second);
+    for (uint32_t i : kd) order.push_back(i);
     while (order.size() % RT_GROUP) order.push_back(0xFFFFFFFFu);
     L.ngroups = (uint32_t)(order.size() / RT_GROUP);
     L.nclusters = (L.ngroups + 7) / 8;
@@ -735,9 +744,7 @@ static void f16_split(double x, uint16_t& hi, uint16_t& lo) {
 static int build_mfma(rt_ctx* ctx) {
     const uint32_t n = ctx->n;
     ctx->mf_ok = false;
-    // queue entries hold a 14-bit group index (rt_dev_intersect.h mf_spread):
-    // larger lists use the VALU filter
-    if (!n || n > (1u << 16)) return RT_OK;
+    if (!n) return RT_OK;
     const double kS = 1.0 - 0x1p-16 - 0x1p-16;  // 1 - m - mu' (RT_MF_MU)
     double qmax = 1.0;
     for (uint32_t j = 0; j < n; ++j) {
@@ -751,45 +758,114 @@ static int build_mfma(rt_ctx* ctx) {
     }
     int sq = 0;
     while (qmax * std::ldexp(1.0, -sq) > 0x1p14) ++sq;  // <= 10 for |c| <= 2^12
-    const uint32_t nblk = (n + 31) / 32;
-    std::vector<uint16_t> h((size_t)nblk * RT_MF_BLK * 8);
+    // the walk's order: the culled list's (large spheres first in groups of
+    // their own, the rest in k-d order), walked in 32-sphere blocks
+    CullLayout L;
+    cull_layout(ctx->h_sph.data(), ctx->h_S.data(), ctx->h_rm.data(), n, L);
+    const uint32_t nblk = (L.ngroups * RT_GROUP + 31) / 32;
+    // queue entries hold a 14-bit group index (rt_dev_intersect.h mf_spread):
+    // larger lists use the VALU filter
+    if (nblk > 2048u) return RT_OK;
+    const uint32_t npos = nblk * 32;  // <= L.nrec (whole clusters + a pad group)
     static const int QA[6] = {0, 1, 2, 0, 0, 1}, QB[6] = {0, 1, 2, 1, 2, 2};
-    for (uint32_t b = 0; b < nblk; ++b)
-        for (uint32_t l = 0; l < 64; ++l) {
-            const uint32_t j = 32 * b + (l & 31), hh = l >> 5;
-            uint16_t row[32] = {};
-            if (j < n) {
-                const float4 q = ctx->h_sph[j];
-                const double c[3] = {q.x, q.y, q.z};
-                uint16_t hi[9], lo[9];
-                for (int a = 0; a < 3; ++a) f16_split(c[a], hi[a], lo[a]);
-                for (int f = 0; f < 6; ++f)
-                    f16_split(std::ldexp(c[QA[f]] * c[QB[f]], -sq), hi[3 + f], lo[3 + f]);
-                for (int f = 0; f < 8; ++f) {
-                    row[f] = hi[f];       // w0..w3
-                    row[8 + f] = lo[f];   // w4..w7
-                    row[16 + f] = hi[f];  // w8..w11
-                }
-                row[24] = row[25] = hi[8];  // w12
-                row[26] = lo[8];            // w13
-                const double S = (double)q.w - kS * (c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
-                if (!(std::fabs(S) <= 0x1p15)) return RT_OK;
-                f16_split(S, row[29], row[30]);  // w14 hi half, w15 lo half
-            } else {
-                row[29] = f16_bits(-INFINITY);
-            }
-            row[27] = row[28] = f16_bits(1.0);  // against the ray's T0 hi, lo
-            // A0 (K 0..15) of every lane at entry l; A1 (K 16..31) of lanes
-            // 32..63 at entry 64 + (l - 32). Lanes 0..31 of A1 hold K 16..23 =
-            // the hi parts again, equal to their A0 (K 0..7): the kernel reads
-            // A0's entry for them (rt_dev_intersect.h intersect_world_mfma)
-            uint16_t* blk = &h[(size_t)b * RT_MF_BLK * 8];
-            std::memcpy(&blk[(size_t)l * 8], &row[8 * hh], 16);
-            if (hh) std::memcpy(&blk[(size_t)(64 + l - 32) * 8], &row[16 + 8], 16);
+    // the row of a sphere or bound (c, S'): K 0..31 (f16 bits); pad: S' = -inf
+    auto make_row = [&](const double c[3], double S, uint16_t row[32]) {
+        std::memset(row, 0, 64);
+        uint16_t hi[9], lo[9];
+        for (int a = 0; a < 3; ++a) f16_split(c[a], hi[a], lo[a]);
+        for (int f = 0; f < 6; ++f) f16_split(std::ldexp(c[QA[f]] * c[QB[f]], -sq), hi[3 + f], lo[3 + f]);
+        for (int f = 0; f < 8; ++f) {
+            row[f] = hi[f];       // w0..w3
+            row[8 + f] = lo[f];   // w4..w7
+            row[16 + f] = hi[f];  // w8..w11
         }
+        row[24] = row[25] = hi[8];  // w12
+        row[26] = lo[8];            // w13
+        row[27] = row[28] = f16_bits(1.0);  // against the ray's T0 hi, lo
+        if (std::isinf(S)) row[29] = f16_bits(S);
+        else f16_split(S, row[29], row[30]);  // w14 hi half, w15 lo half
+    };
+    std::vector<uint16_t> h((size_t)nblk * RT_MF_BLK * 8);
+    std::vector<float4> msph(npos, make_float4(0.0f, 0.0f, 0.0f, -INFINITY));
+    std::vector<uint32_t> mperm(npos, 0u);
+    for (uint32_t p = 0; p < npos; ++p) {
+        const uint32_t b = p / 32, l0 = p & 31;
+        uint16_t row[32];
+        const uint32_t i = L.perm[p];
+        if (i != 0xFFFFFFFFu) {
+            const float4 q = ctx->h_sph[i];
+            msph[p] = q;
+            mperm[p] = i;
+            const double c[3] = {q.x, q.y, q.z};
+            const double S = (double)q.w - kS * (c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+            if (!(std::fabs(S) <= 0x1p15)) return RT_OK;
+            make_row(c, S, row);
+        } else {
+            const double c[3] = {0.0, 0.0, 0.0};
+            make_row(c, -INFINITY, row);
+        }
+        // A0 (K 0..15) of every lane at entry l; A1 (K 16..31) of lanes
+        // 32..63 at entry 64 + (l - 32). Lanes 0..31 of A1 hold K 16..23 =
+        // the hi parts again, equal to their A0 (K 0..7): the kernel reads
+        // A0's entry for them (rt_dev_intersect.h intersect_world_mfma)
+        uint16_t* blk = &h[(size_t)b * RT_MF_BLK * 8];
+        std::memcpy(&blk[(size_t)l0 * 8], &row[0], 16);            // lane l0 (hh = 0)
+        std::memcpy(&blk[(size_t)(l0 + 32) * 8], &row[8], 16);     // lane l0 + 32 (hh = 1)
+        std::memcpy(&blk[(size_t)(64 + l0) * 8], &row[24], 16);   // A1 of lane l0 + 32
+    }
+    // block bounds (rt_dev_intersect.h "Block bounds"): per chunk of 32
+    // blocks, rows = the blocks' bounding spheres in the sphere rows' layout
+    const uint32_t nchunk = (nblk + 31) / 32;
+    std::vector<uint16_t> hb((size_t)nchunk * 128 * 8);
+    const double kB = 1.0 - 0x1p-16 - 0x1p-16 - 0x1p-7;  // 1 - m - mu' - muB
+    for (uint32_t r = 0; r < nchunk * 32; ++r) {
+        const uint32_t k = r / 32, j = r & 31;
+        double lo3[3] = {INFINITY, INFINITY, INFINITY}, hi3[3] = {-INFINITY, -INFINITY, -INFINITY};
+        bool any = false;
+        if (r < nblk)
+            for (uint32_t p = 32 * r; p < 32 * r + 32; ++p) {
+                if (L.perm[p] == 0xFFFFFFFFu) continue;
+                any = true;
+                const float4 q = msph[p];
+                const double c[3] = {q.x, q.y, q.z};
+                for (int a = 0; a < 3; ++a) {
+                    lo3[a] = std::min(lo3[a], c[a]);
+                    hi3[a] = std::max(hi3[a], c[a]);
+                }
+            }
+        double C[3] = {0.0, 0.0, 0.0}, SB = -INFINITY;  // empty: never passes
+        if (any) {
+            for (int a = 0; a < 3; ++a) C[a] = (double)(float)((lo3[a] + hi3[a]) * 0.5);
+            double Lm = 0.0;
+            for (uint32_t p = 32 * r; p < 32 * r + 32; ++p) {
+                if (L.perm[p] == 0xFFFFFFFFu) continue;
+                const float4 q = msph[p];
+                const double dx = q.x - C[0], dy = q.y - C[1], dz = q.z - C[2];
+                Lm = std::max(Lm, std::sqrt(dx * dx + dy * dy + dz * dz) * (1.0 + 0x1p-40) +
+                                      std::sqrt((double)q.w) * (1.0 + 0x1p-18));
+            }
+            const double R2 = (1.0 + 0x1p-3) * Lm * Lm * (1.0 + 0x1p-40) + 0x1p-60;
+            const double CC = C[0] * C[0] + C[1] * C[1] + C[2] * C[2];
+            SB = (double)round_up_f32((R2 - kB * CC) * (1.0 + 0x1p-40) + 0x1p-60);
+            if (!(std::fabs(SB) <= 0x1p15)) SB = INFINITY;  // out of the split's range: always passes
+        }
+        uint16_t row[32];
+        make_row(C, SB, row);
+        uint16_t* blk = &hb[(size_t)k * 128 * 8];
+        for (int hh = 0; hh < 2; ++hh)
+            for (int half = 0; half < 2; ++half)  // B0: K 0..15, B1: K 16..31
+                std::memcpy(&blk[((size_t)half * 64 + 32 * hh + j) * 8], &row[16 * half + 8 * hh], 16);
+    }
     int rc = ensure(ctx, &ctx->d_mfA, &ctx->mfA_cap, h.size() * sizeof(uint16_t));
+    if (!rc) rc = ensure(ctx, &ctx->d_mfB, &ctx->mfB_cap, hb.size() * sizeof(uint16_t));
+    if (!rc) rc = ensure(ctx, &ctx->d_mf_sph, &ctx->mf_sph_cap, msph.size() * sizeof(float4));
+    if (!rc) rc = ensure(ctx, &ctx->d_mf_perm, &ctx->mf_perm_cap, mperm.size() * sizeof(uint32_t));
     if (rc) return rc;
     HIP_TRY(ctx, hipMemcpy(ctx->d_mfA, h.data(), h.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(ctx->d_mfB, hb.data(), hb.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(ctx->d_mf_sph, msph.data(), msph.size() * sizeof(float4), hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(ctx->d_mf_perm, mperm.data(), mperm.size() * sizeof(uint32_t),
+                           hipMemcpyHostToDevice));
     ctx->mf_nblk = nblk;
     ctx->mf_qs = (float)std::ldexp(1.0, sq);
     ctx->mf_abs = (float)std::ldexp(1.0, sq - 20);
@@ -855,6 +931,21 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n, const rt_mat
     ctx->has_scene = true;  // the culled list follows lazily (cull_ready)
     return RT_OK;
 }
+
+#ifdef RT_MFMA_FILTER
+// The matrix-core walk's scene as the kernels take it (mf_ok).
+static MfScene mf_scene(const rt_ctx* ctx) {
+    MfScene mf = {};
+    mf.A = ctx->d_mfA;
+    mf.B = ctx->tune.mf_cull ? ctx->d_mfB : nullptr;
+    mf.sph = ctx->d_mf_sph;
+    mf.perm = ctx->d_mf_perm;
+    mf.nblk = ctx->mf_nblk;
+    mf.qs = ctx->mf_qs;
+    mf.abs = ctx->mf_abs;
+    return mf;
+}
+#endif
 
 // The culled list of the current scene, (re)built on the first RT_FLAG_CULL
 // call after rt_set_scene / rt_update_spheres. No kernel can be reading the
@@ -1174,12 +1265,7 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     if (tn.chk_shrink == 5) K_.chk_nrm = 0;
     if (tn.chk_shrink == 7) K_.chk_slots = 0;
 #ifdef RT_MFMA_FILTER
-    if (!cull && ctx->mf_ok && !(p.flags & RT_FLAG_VALU_FILTER)) {
-        K_.mfA = ctx->d_mfA;
-        K_.mf_nblk = ctx->mf_nblk;
-        K_.mf_qs = ctx->mf_qs;
-        K_.mf_abs = ctx->mf_abs;
-    }
+    if (!cull && ctx->mf_ok && !(p.flags & RT_FLAG_VALU_FILTER)) K_.mf = mf_scene(ctx);
 #endif
     std::memcpy(K_.T, cam->transform, sizeof(K_.T));
     K_.tan_half = (float)std::tan((double)(cam->fov / 2.0f));                 // generate.wgsl:67
@@ -1641,16 +1727,9 @@ int rt_intersect_ex(rt_ctx* ctx, const float* rays, uint32_t n, uint32_t flags, 
     hipError_t e = hipMemcpyAsync(b, rays, rb, hipMemcpyHostToDevice, ctx->stream);
     // the brute-force walk takes the render's filter: the matrix-core tiles
     // when the scene fits them (unless RT_FLAG_VALU_FILTER)
-    const uint4* mfA = nullptr;
-    uint32_t mf_nblk = 0;
-    float mf_qs = 1.0f, mf_abs = 0.0f;
+    MfScene mf = {};
 #ifdef RT_MFMA_FILTER
-    if (!cull && ctx->mf_ok && !(flags & RT_FLAG_VALU_FILTER)) {
-        mfA = ctx->d_mfA;
-        mf_nblk = ctx->mf_nblk;
-        mf_qs = ctx->mf_qs;
-        mf_abs = ctx->mf_abs;
-    }
+    if (!cull && ctx->mf_ok && !(flags & RT_FLAG_VALU_FILTER)) mf = mf_scene(ctx);
 #endif
     if (e == hipSuccess)
     {
@@ -1659,8 +1738,7 @@ int rt_intersect_ex(rt_ctx* ctx, const float* rays, uint32_t n, uint32_t flags, 
                                 ctx->scene_fast && ctx->tune.fast_exact ? 1u : 0u,
                                 (const float*)b, n, (int*)(b + rb), (float*)(b + rb + ob),
                                 cull ? ctx->d_bnd_c : nullptr, cull ? ctx->d_perm_c : nullptr,
-                                cull ? ctx->nclusters_c : 0u, mfA, mf_nblk, mf_qs, mf_abs,
-                                ctx->stream);
+                                cull ? ctx->nclusters_c : 0u, &mf, ctx->stream);
     }
     if (e == hipSuccess)
         e = hipMemcpyAsync(hit_index, b + rb, ob, hipMemcpyDeviceToHost, ctx->stream);

@@ -673,7 +673,30 @@ typedef float f16x __attribute__((ext_vector_type(16)));
 // (rt_api.cpp: mf_abs). Range: |c_i| <= 2^12, |S'| <= 2^15 (build_mfma) and
 // per wave |o_i| <= 2^12, |o|^2 <= 2^15 (mfma_wave_ok: T0 in f16 range).
 // tests/test_mfma_filter.py restates this arithmetic and checks it.
+//
+// Block bounds (mf.B). The list is walked in the culled list's spatial order
+// (rt_api.cpp build_mfma), and each 32-sphere block has a bounding sphere (C,
+// L = max_i (|C - c_i| + r_i (1 + 2^-18)), R^2 = (1 + 2^-3) L^2 + 2^-60) whose
+// bound row is a sphere row with S'_B = R^2 - (1 - m - mu' - muB)|C|^2 (rounded
+// up; muB = 2^-7), tested against the ray column with T0_B = (1 - m - mu' -
+// muB)|o|^2 - k1^2 - abs'. A half-wave skips a block whose bound no ray of
+// the half passes (V_B >= 0 in every lane). Why a skipped block holds no hit:
+// a member sphere i the exact test hits is a candidate of the packed VALU
+// filter (its proof, ray_filter_consts), so by the culled list's bound proof
+// (rt_api.cpp, above cull_layout; it holds for any member set) the line's
+// distance from C has dist_C^2 <= (1 + 2^-4 + 2^-8) L^2 + 2^-8 (|o|^2 + |C|^2).
+// The bound row's exact value is F_B = hb~_C^2 + R^2 - (1 - m)|o - C|^2 +
+// (mu' + muB)(|o|^2 + |C|^2) + abs' >= R^2 - dist_C^2 + (mu' + muB - 2^-18)
+// (|o|^2 + |C|^2) >= (2^-4 - 2^-8) L^2 + 2^-60 + (mu' + 2^-7 - 2^-8 - 2^-18)
+// (|o|^2 + |C|^2), which exceeds the tile's rounding (<= 2^-16.02 (|o|^2 +
+// |C|^2) + 2^-20.4 |S'_B|, the analysis above; |C_i| <= 2^12 as the members',
+// |S'_B| <= 2^15 or the bound row always passes): V_B = T0_B - H0_B < 0. The
+// proof's domain: |o_i| <= 2^12 (mfma_wave_ok) and |d|^2 in [2^-100, 2^100]
+// for every live lane, else the wave walks every block. Bound rows of blocks
+// with an out-of-range bound always pass (S'_B hi = +inf), of empty blocks
+// never (-inf).
 #define RT_MF_MU 0x1p-16f
+#define RT_MF_MUB 0x1p-7f  // the block-bound tile's extra margin (see "Block bounds")
 #ifndef RT_MF_CAP
 #define RT_MF_CAP 12  // queue entries per lane and half (LDS)
 #endif
@@ -725,7 +748,8 @@ __device__ __forceinline__ bool mfma_wave_ok(v3 o, bool live) {
 #endif
 template <bool FAST>
 __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, uint32_t cnt1,
-                                           const float4* __restrict__ sph, uint32_t nsph, v3 o,
+                                           const float4* __restrict__ sph, uint32_t nsph,
+                                           const uint32_t* __restrict__ perm, v3 o,
                                            v3 d, float a,
                                            float ya, float& best_t, int& best_i MF_ECNT) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -766,9 +790,10 @@ __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, ui
         const uint32_t b = __builtin_ctz(m) >> 3;
         m &= m - 1;
         MF_ECNT_INC;
-        exact_body<FAST, false, true>(sph[RT_IDX(base + b, nsph, RT_SITE_MF_SPH)], (int)(base + b), o,
-                                      d, a, ya, best_t, best_i,
-                                      nullptr EXACT_PASS);
+        // the walk's order is spatial: an exact tie goes to the lower
+        // ORIGINAL index (perm, read on ties only)
+        exact_body<FAST, true>(sph[RT_IDX(base + b, nsph, RT_SITE_MF_SPH)], (int)(base + b), o,
+                               d, a, ya, best_t, best_i, perm EXACT_PASS);
     }
 }
 
@@ -804,9 +829,7 @@ __device__ __forceinline__ void tile_or(const f16x& H, int* gq, int& g) {
 // Called by the whole wave (the MFMA operands span all 64 lanes): lanes
 // without a ray (live false) trace a dummy ray whose threshold is +inf.
 // mf_qs = 2^sq, mf_abs = abs' (build_mfma).
-__device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mfA, uint32_t nblk,
-                                                    float mf_qs, float mf_abs,
-                                                    const float4* __restrict__ sph,
+__device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
                                                     uint32_t scene_fast, v3 o, v3 d, bool live,
                                                     uint64_t live_mask, float& t_out,
                                                     uint32_t* cq
@@ -814,17 +837,27 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
                                                     , Prof& prof_
 #endif
                                                     ) {
+    const uint4* __restrict__ mfA = mf.A;
+    const uint32_t nblk = mf.nblk;
+    const float mf_qs = mf.qs, mf_abs = mf.abs;
+    const float4* __restrict__ sph = mf.sph;
     if (!live) {
         o = mk(0.0f, 0.0f, 0.0f);
         d = mk(0.0f, 0.0f, 1.0f);
     }
-    const float l = sqrt_x(dot(d, d));
+    // chunk 0's block-bound fragments, loaded first so that the ray features
+    // cover their latency (from the A fragments when there are no bounds: the
+    // load stays unconditional, so hipcc's vmcnt waits count exactly)
+    const uint4* pb0 = mf.B != nullptr ? mf.B : mfA;
+    uint4 bq0 = pb0[__lane_id()], bq1 = pb0[64u + __lane_id()];
+    const float dd = dot(d, d);
+    const float l = sqrt_x(dd);
     const float a = l * l;  // sqr(length(r.dir)), intersect.wgsl:98
     const bool fast = ray_fast(scene_fast, o, a);
     const float ya = fast ? rt_recip_rn(a) : a;
     const uint32_t lane = __lane_id();
     // ray constants (ray_filter_consts, with the wider mu'), then the features
-    const float rs = __builtin_amdgcn_rsqf(dot(d, d));
+    const float rs = __builtin_amdgcn_rsqf(dd);
     const float ex = -(d.x * rs), ey = -(d.y * rs), ez = -(d.z * rs);  // e = -dn
     const float m_ = 0x1p-16f;
     const float oo = __builtin_fmaf(o.z, o.z, __builtin_fmaf(o.y, o.y, o.x * o.x));
@@ -915,6 +948,56 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
     };
     const h8v B00 = as_h8(b0[0]), B01 = as_h8(b0[1]);  // half 0: K 0..15, K 16..31
     const h8v B10 = as_h8(b1[0]), B11 = as_h8(b1[1]);  // half 1
+    const f16x zero = {};
+
+    // ---- block bounds (mf.B): which 32-sphere blocks some ray of each half
+    // passes near. The bound tile is the TRANSPOSED product -- the rays'
+    // fragments as the A operand (rows), the chunk's 32 block bounds as B
+    // (columns; their fragments have the sphere rows' layout, which is B's) --
+    // so lane l holds bound l & 31 against 16 of the half's rays and one OR
+    // tree + one ballot give the half's 32-bit block mask. The ray column is
+    // the filter's with the bound margin muB in its threshold (T0_B; proof in
+    // the header above). A wave with a live ray outside |d|^2 in [2^-100,
+    // 2^100] (the proof's domain) walks every block.
+    const uint32_t nchunk = (nblk + 31u) >> 5;
+    uint32_t mv0 = 0xFFFFFFFFu, mv1 = 0xFFFFFFFFu;  // lane k: chunk k's masks, halves 0 / 1
+    if (mf.B != nullptr && rt_ballot(live && !(dd >= 0x1p-100f && dd <= 0x1p100f)) == 0) {
+        const float TB =
+            live ? __builtin_fmaf(-k1, k1, (1.0f - m_ - RT_MF_MU - RT_MF_MUB) * oo) - mf_abs : INFINITY;
+        uint32_t h8b = pk(-f[8], TB);  // (hi x8, T0_B hi)
+        asm volatile("" : "+v"(h8b));
+        const float tlb = live ? TB - half_f32(h8b, 1) : 0.0f;
+        const auto r13 = __builtin_amdgcn_permlane32_swap(w[9], h8b, false, false);
+        const auto r14 = __builtin_amdgcn_permlane32_swap(w[10], pk(tlb, -1.0f), false, false);
+        const uint32_t c0[4] = {b0[1][0], r13[0], r14[0], b0[1][3]};
+        const uint32_t c1[4] = {b1[1][0], r13[1], r14[1], b1[1][3]};
+        const h8v C01 = as_h8(c0), C11 = as_h8(c1);
+        for (uint32_t k = 0; k < nchunk; ++k) {
+            // the next chunk's fragments load while this chunk's tiles run
+            const uint4* pb = mf.B + (size_t)(k + 1u < nchunk ? k + 1u : k) * 128u;
+            const uint4 nq0 = pb[lane], nq1 = pb[64u + lane];
+            h8v F0, F1;
+            __builtin_memcpy(&F0, &bq0, 16);
+            __builtin_memcpy(&F1, &bq1, 16);
+            bq0 = nq0;
+            bq1 = nq1;
+            uint32_t mk2[2];
+#pragma unroll
+            for (uint32_t t = 0; t < 2; ++t) {
+                const f16x V = __builtin_amdgcn_mfma_f32_32x32x16_f16(
+                    t ? C11 : C01, F1, __builtin_amdgcn_mfma_f32_32x32x16_f16(t ? B10 : B00, F0, zero, 0, 0, 0),
+                    0, 0, 0);
+                int gq[4], g;
+                tile_or(V, gq, g);
+                const uint64_t bm = rt_ballot(g < 0);
+                mk2[t] = (uint32_t)bm | (uint32_t)(bm >> 32);
+            }
+            if (lane == k) {
+                mv0 = mk2[0];
+                mv1 = mk2[1];
+            }
+        }
+    }
 
     float best_t = VERY_FAR;
     int best_i = -1;
@@ -925,7 +1008,10 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
     uint32_t* const q1 = cq + RT_MF_CAP * 64u + lane;
     uint32_t *qp0 = q0, *qp1 = q1;
     auto qcount = [](const uint32_t* p, const uint32_t* p0) { return (uint32_t)(p - p0) >> 6; };
-    const f16x zero = {};
+#ifdef RT_SENS_MFMA
+    h8v zeroB = {};
+    asm volatile("" : "+v"(zeroB));
+#endif
 #ifdef RT_PROFILE
     uint32_t ecnt_ = 0;  // this lane's exact tests (c[13]: wave max, c[15]: lane sum)
 #endif
@@ -934,7 +1020,7 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
     uint32_t ub0 = 0, ub1 = 0;
     // one 32-sphere block: both ray halves against A fragments x0 (K 0..15),
     // x1 (K 16..31)
-    auto block = [&](uint32_t b, const uint4 x0, const uint4 x1) {
+    auto block = [&](uint32_t b, const uint4 x0, const uint4 x1, uint32_t m0, uint32_t m1) {
         // a block adds at most 4 entries to each half's queue: make room first,
         // while no tile result is live (the lanes' own counts are compared
         // only when the scalar bound says the queue may be full)
@@ -943,9 +1029,11 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
             const uint32_t cnt0 = qcount(qp0, q0), cnt1 = qcount(qp1, q1);
             PROF_ADD(11, 1);  // queue flushes
             if (fast)
-                mfma_drain<true>(cq, cnt0, cnt1, sph, nblk * 32u, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
+                mfma_drain<true>(cq, cnt0, cnt1, sph, nblk * 32u, mf.perm, o, d, a, ya, best_t,
+                                 best_i MF_ECNT_PASS);
             else
-                mfma_drain<false>(cq, cnt0, cnt1, sph, nblk * 32u, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
+                mfma_drain<false>(cq, cnt0, cnt1, sph, nblk * 32u, mf.perm, o, d, a, ya, best_t,
+                                  best_i MF_ECNT_PASS);
             qp0 = q0;
             qp1 = q1;
             ub0 = ub1 = 0;
@@ -958,9 +1046,25 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
 #pragma unroll
         for (uint32_t t = 0; t < 2; ++t) {
             if (t) __builtin_amdgcn_sched_barrier(0);
+            if ((((t ? m1 : m0) >> (b & 31u)) & 1u) == 0u) continue;  // no ray of the half near the block
+#if defined(RT_SENS_MFMA) || defined(RT_SENS_VALU)
+            f16x H = __builtin_amdgcn_mfma_f32_32x32x16_f16(
+#else
             const f16x H = __builtin_amdgcn_mfma_f32_32x32x16_f16(
+#endif
                 A1, t ? B11 : B01,
                 __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, t ? B10 : B00, zero, 0, 0, 0), 0, 0, 0);
+#ifdef RT_SENS_MFMA
+            // sensitivity probe (timing only, same bits): one more MFMA per
+            // tile on the matrix pipe, adding zero products to V
+            H = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, zeroB, H, 0, 0, 0);
+#endif
+#ifdef RT_SENS_VALU
+            // sensitivity probe (timing only): RT_SENS_VALU dual-issued moves
+            // per tile on the VALU issue port
+#pragma unroll
+            for (int k = 0; k < RT_SENS_VALU; ++k) asm volatile("v_mov_b32 %0, %0" : "+v"(H[k & 15]));
+#endif
             // per-group ORs (the lane's 4 groups of 4 spheres), then the tile's
             int gq[4], g;
             tile_or(H, gq, g);
@@ -1004,7 +1108,8 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
             }
         }
     };
-    // blocks in pairs: the next block's fragments load while this one runs,
+    // The blocks some ray of the wave passes near (all blocks without bound
+    // tiles), in pairs: the next block's fragments load while this one runs,
     // into the other register set (no fragment copies per block). Block p's
     // fragments at mfA + RT_MF_BLK p (uniform base): A0 (K 0..15) for the 64
     // lanes, then A1 (K 16..31) for lanes 32..63 only -- lanes 0..31 hold K
@@ -1012,24 +1117,50 @@ __device__ __forceinline__ int intersect_world_mfma(const uint4* __restrict__ mf
     // they load their A0 entry a second time (the same cache lines, no new
     // bytes): 1.5 KB per block instead of 2 (rt_api.cpp build_mfma).
     const uint32_t off1 = lane < 32u ? lane : lane + 32u;
-    uint4 a0 = mfA[lane], a1 = mfA[off1];
-    uint32_t b = 0;
-    for (; b + 2u <= nblk; b += 2u) {
-        const uint4* p1 = mfA + (size_t)(b + 1u) * RT_MF_BLK;
-        const uint4 n0 = p1[lane], n1 = p1[off1];
-        block(b, a0, a1);
-        const uint4* p2 = mfA + (size_t)(b + 2u < nblk ? b + 2u : b + 1u) * RT_MF_BLK;
-        a0 = p2[lane];
-        a1 = p2[off1];
-        block(b + 1u, n0, n1);
+    auto load = [&](uint32_t p, uint4& x0, uint4& x1) {
+        const uint4* pa = mfA + (size_t)p * RT_MF_BLK;
+        x0 = pa[lane];
+        x1 = pa[off1];
+    };
+    for (uint32_t k = 0; k < nchunk; ++k) {
+        const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)mv0, (int)k);
+        const uint32_t m1 = (uint32_t)__builtin_amdgcn_readlane((int)mv1, (int)k);
+        const uint32_t rem = nblk - 32u * k;
+        uint32_t todo = (m0 | m1) & (rem >= 32u ? 0xFFFFFFFFu : ((1u << rem) - 1u));
+        if (todo == 0u) continue;
+        // the next block to walk (the last one again when none is left: its
+        // fragments reload from L1, and every load stays unconditional, so
+        // hipcc's vmcnt waits count exactly -- a conditional prefetch made it
+        // wait for the prefetch too)
+        auto next = [&](uint32_t cur) {
+            const uint32_t nb = todo != 0u ? 32u * k + (uint32_t)__builtin_ctz(todo) : cur;
+            todo &= todo - 1u;
+            return nb;
+        };
+        uint32_t b = next(0u);
+        uint4 a0, a1, n0, n1;
+        load(b, a0, a1);
+        for (;;) {
+            const bool more = todo != 0u;
+            const uint32_t bn = next(b);
+            load(bn, n0, n1);
+            block(b, a0, a1, m0, m1);
+            if (!more) break;
+            const bool more2 = todo != 0u;
+            b = next(bn);
+            load(b, a0, a1);
+            block(bn, n0, n1, m0, m1);
+            if (!more2) break;
+        }
     }
-    if (b < nblk) block(b, a0, a1);
     PROF_MARK(1);
     const uint32_t cnt0 = qcount(qp0, q0), cnt1 = qcount(qp1, q1);
     if (fast)
-        mfma_drain<true>(cq, cnt0, cnt1, sph, nblk * 32u, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
+        mfma_drain<true>(cq, cnt0, cnt1, sph, nblk * 32u, mf.perm, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
     else
-        mfma_drain<false>(cq, cnt0, cnt1, sph, nblk * 32u, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
+        mfma_drain<false>(cq, cnt0, cnt1, sph, nblk * 32u, mf.perm, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
+    // the walk position of the winner -> its original index
+    if (best_i >= 0) best_i = (int)mf.perm[RT_IDX((uint32_t)best_i, nblk * 32u, RT_SITE_PERM)];
     PROF_MARK(2);
 #ifdef RT_PROFILE
     {

@@ -52,6 +52,25 @@ struct FastDiv {
 
 // Kernel parameters (by value; lands in SGPRs). Camera constants are
 // precomputed on the host exactly as generate.wgsl:67-95 computes them.
+// The matrix-core walk's scene (RT_MFMA_FILTER builds; rt_api.cpp build_mfma):
+// the list in the culled list's spatial order (large spheres first, the rest
+// in k-d order of their centres) as f16 A fragments of
+// v_mfma_f32_32x32x16_f16, RT_MF_BLK uint4 per 32-sphere block; per chunk of
+// 32 blocks the blocks' bounding spheres as fragments of the same layout (2 x
+// 64 uint4), tested against the wave's rays on the matrix cores so that a
+// half-wave skips every block none of its rays passes near
+// (rt_dev_intersect.h intersect_world_mfma); the records the drain's exact
+// tests read, in the walk's order; and the walk position -> original index
+// map (exact ties, the result).
+struct MfScene {
+    const uint4* A;         // null: no matrix-core walk
+    const uint4* B;         // null: every block is walked (knob mf_cull 0)
+    const float4* sph;      // (cx, cy, cz, r^2) in the walk's order, nblk * 32 records
+    const uint32_t* perm;   // walk position -> original sphere index
+    uint32_t nblk;          // 32-sphere blocks (<= 2048)
+    float qs, abs;          // 2^sq (quadratic features' ray-side scale), threshold margin
+};
+
 struct KParams {
     uint32_t width, height, spp, max_depth, frame0;
     uint32_t row_block, shard_count, shard_index;
@@ -112,12 +131,9 @@ struct KParams {
     uint32_t nclusters;
     uint32_t cull_supers;   // 1: test the cluster bounds (many clusters); 0: walk every cluster
     const float4* acc_in;   // passes after the first (block_begin > 0): the fold so far, per pixel
-    // matrix-core filter (RT_MFMA_FILTER builds, brute-force walk): the list as
-    // f16 A fragments of v_mfma_f32_32x32x16_f16, per 32-sphere block 2 x 64
-    // lanes x 16 B (rt_api.cpp build_mfma); null: the packed VALU filter
-    const uint4* mfA;
-    uint32_t mf_nblk;
-    float mf_qs, mf_abs;  // 2^sq (quadratic features' ray-side scale), threshold margin
+    // matrix-core filter (RT_MFMA_FILTER builds, brute-force walk; mf.A null:
+    // the packed VALU filter)
+    MfScene mf;
     // queue order (knob item_order, bits; default 3): bit 0 the block items
     // and the tail items, bit 1 the pixel items, pixel-major
     // (consecutive items: one pixel's pairs / samples / frames) instead of
@@ -181,8 +197,7 @@ hipError_t rt_launch_assemble(const float4* gathered, uint32_t max_rows, uint32_
 hipError_t rt_launch_intersect(const float4* grp, const float4* sph, uint32_t ngroups,
                                uint32_t scene_fast, const float* rays, uint32_t n, int* out_i, float* out_t,
                                const float4* bnd, const uint32_t* perm, uint32_t nclusters,
-                               const uint4* mfA, uint32_t mf_nblk, float mf_qs, float mf_abs,
-                               hipStream_t stream);
+                               const MfScene* mf, hipStream_t stream);
 hipError_t rt_render_occupancy(int* blocks_per_cu, int* blocks_per_cu_cull);
 hipError_t rt_launch_primary(const KParams* P, float4* pd, hipStream_t stream);
 #ifdef RT_CHECK_BOUNDS

@@ -393,9 +393,8 @@ __device__ __forceinline__ void render_body(
         if ((uint32_t)__popcll(live) <= P.wide_max) {  // nearly empty wave: sphere-parallel
             intersect_wide<CULL>(sph, P.nspheres, P.scene_fast, live, st.o, st.d, hi, t, P.perm);
 #ifdef RT_MFMA_FILTER
-        } else if (!CULL && P.mfA && mfma_wave_ok(st.o, has_item)) {  // the whole wave
-            const int h2 = intersect_world_mfma(P.mfA, P.mf_nblk, P.mf_qs, P.mf_abs, sph,
-                                                P.scene_fast, st.o, st.d,
+        } else if (!CULL && P.mf.A && mfma_wave_ok(st.o, has_item)) {  // the whole wave
+            const int h2 = intersect_world_mfma(P.mf, P.scene_fast, st.o, st.d,
                                                 has_item, live, t, cqm
 #ifdef RT_PROFILE
                                                 , prof_
@@ -649,8 +648,7 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_cull_kernel(
 // runs the tiles, lanes past n trace a dummy ray that never has a candidate; a
 // wave with a ray outside the range takes the VALU filter, as in the render.
 __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_mfma_kernel(
-    const uint4* __restrict__ mfA, uint32_t nblk, float mf_qs, float mf_abs,
-    const float4* __restrict__ grp,
+    const MfScene mf, const float4* __restrict__ grp,
     const float4* __restrict__ sph, uint32_t ngroups, uint32_t scene_fast,
     const float* __restrict__ rays, uint32_t n, int* __restrict__ out_i, float* __restrict__ out_t) {
     __shared__ uint32_t s_cq[RT_BLOCK_THREADS * RT_CQ_CAP];
@@ -675,7 +673,7 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_mfma_kernel(
 #else
     if (mfma_wave_ok(o, live)) {
 #endif
-        hi = intersect_world_mfma(mfA, nblk, mf_qs, mf_abs, sph, scene_fast, o, d, live, lm, t,
+        hi = intersect_world_mfma(mf, scene_fast, o, d, live, lm, t,
                                   s_cqm + wave * RT_MF_QW
 #ifdef RT_PROFILE
                                   , prof_
@@ -870,21 +868,16 @@ hipError_t rt_launch_assemble(const float4* gathered, uint32_t max_rows, uint32_
 hipError_t rt_launch_intersect(const float4* grp, const float4* sph, uint32_t ngroups,
                                uint32_t scene_fast, const float* rays, uint32_t n, int* out_i,
                                float* out_t, const float4* bnd, const uint32_t* perm,
-                               uint32_t nclusters, const uint4* mfA, uint32_t mf_nblk,
-                               float mf_qs, float mf_abs, hipStream_t stream) {
+                               uint32_t nclusters, const MfScene* mf, hipStream_t stream) {
     const uint32_t T = RT_BLOCK_THREADS;
 #ifdef RT_MFMA_FILTER
-    if (mfA && !bnd) {
-        hipLaunchKernelGGL(rt_intersect_mfma_kernel, dim3((n + T - 1) / T), dim3(T), 0, stream, mfA,
-                           mf_nblk, mf_qs, mf_abs, grp, sph, ngroups, scene_fast, rays, n, out_i,
-                           out_t);
+    if (mf && mf->A && !bnd) {
+        hipLaunchKernelGGL(rt_intersect_mfma_kernel, dim3((n + T - 1) / T), dim3(T), 0, stream, *mf,
+                           grp, sph, ngroups, scene_fast, rays, n, out_i, out_t);
         return hipGetLastError();
     }
 #else
-    (void)mfA;
-    (void)mf_nblk;
-    (void)mf_qs;
-    (void)mf_abs;
+    (void)mf;
 #endif
     if (bnd)
         hipLaunchKernelGGL(rt_intersect_cull_kernel, dim3((n + T - 1) / T), dim3(T), 0, stream, grp,

@@ -107,8 +107,8 @@ def dominance(sp, rays, chunk=4000):
 
 
 def tangent_pair():
-    """Two unit spheres touching at (1, 0, 0), the later one (index 1) first in
-    Morton order: rays through the contact point tie exactly."""
+    """Two unit spheres touching at (1, 0, 0), the later one (index 1) first in the
+    culled order: rays through the contact point tie exactly."""
     mats = scene.MaterialCache()
     mats.insert("a", scene.RayTraceMaterial((0.5, 0.5, 0.5, 1), scene.Reflectance.Lambertian, 1, 0))
     sp = [scene.Sphere((2, 0, 0), 1, 0), scene.Sphere((0, 0, 0), 1, 0)]

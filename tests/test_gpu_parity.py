@@ -959,3 +959,34 @@ def test_registered_host_output_two_in_flight(renderer, S):
     for f in range(4):
         ref, _ = renderer.render(cam, W, H, S, D, frame0=f * S)  # pageable: staged + copied
         check_exact(got[f], ref)
+
+
+@pytest.mark.parametrize("which", ["rtiow", "reference", "spheres2k"])
+def test_block_culled_walk_identical(renderer, which):
+    """The matrix-core walk skips, per half-wave, the 32-sphere blocks whose
+    bounding sphere no ray of the half passes near (MfScene::B; proof in
+    rt_dev_intersect.h "Block bounds"). Frames and segment counts are
+    bit-identical with every block walked (knob mf_cull=0) and equal the
+    oracle's; spheres2k has 63 blocks, two chunks of bound tiles."""
+    import torch
+    if which == "spheres2k":
+        sc = scene.ten_thousand_scene()
+        sp, mt = arrays(sc)
+        sp = np.ascontiguousarray(sp[:2000])
+    else:
+        sp, mt = arrays(scene.rtiow_final_scene() if which == "rtiow" else scene.reference_scene())
+    cam = default_camera_block()
+    renderer.set_scene(sp, mt)
+    W, H, S, D, F = 64, 36, 8, 8, 2
+    outs = []
+    for cull in (0, 1):
+        renderer.tune("mf_cull", str(cull))
+        out = torch.full((F, H, W, 4), -3.0, dtype=torch.float32, device="cuda")
+        renderer.render_frames_device(cam, F, out.data_ptr(), W, H, S, D, frame0=3, flags=NO_REUSE)
+        st = renderer.wait()
+        outs.append((out.cpu().numpy(), st["segments"]))
+    renderer.tune(None)
+    check_exact(outs[1][0], outs[0][0])
+    assert outs[1][1] == outs[0][1]
+    ref, segs = O.render(cam, sp, mt, W, H, S, D, frame0=3 + (F - 1) * S)
+    check_exact(outs[1][0][F - 1], ref)

@@ -62,10 +62,19 @@ def sphere_rows(sp, sq):
     c = sp["center"].astype(F).astype(D)
     r2 = (sp["radius"] * sp["radius"]).astype(F).astype(D)  # the stored s.w = RN(r*r)
     assert np.all(np.abs(c) <= 2.0 ** 12)  # mf_ok
+    S = r2 - (1.0 - M - MU) * (c ** 2).sum(1)
+    assert np.all(np.abs(S) <= 2.0 ** 15)  # mf_ok
+    return rows_of(c, S, sq)
 
+
+def rows_of(c, S, sq):
+    """A rows (f32 values of the f16 parts, K = 32) of centres c (n, 3) and
+    constants S' (n,); an infinite S' is its hi part alone (build_mfma)."""
     def hl(x):
         hi = x.astype(H16)
-        return hi, (x - hi.astype(D)).astype(H16)
+        with np.errstate(invalid="ignore"):
+            lo = np.where(np.isinf(x), 0.0, x - hi.astype(D)).astype(H16)
+        return hi, lo
 
     his, los = [], []
     for a in range(3):
@@ -76,10 +85,8 @@ def sphere_rows(sp, sq):
         hi, lo = hl(c[:, a] * c[:, b] * 2.0 ** -sq)
         his.append(hi)
         los.append(lo)
-    S = r2 - (1.0 - M - MU) * (c ** 2).sum(1)
-    assert np.all(np.abs(S) <= 2.0 ** 15)  # mf_ok
     shi, slo = hl(S)
-    n = len(sp)
+    n = len(c)
     one = np.ones(n, H16)
     # K group 0: hi y0..y7, lo y0..y7; group 1: hi y0..y7, hi y8, hi y8, lo y8,
     # 1, 1, S' hi, S' lo, 0 (build_mfma's words w0..w15)
@@ -102,15 +109,16 @@ def ray_constants(rays):
     return o, e, k1, oo, two * o
 
 
-def ray_columns(rays, sq, abs_margin):
+def ray_columns(rays, sq, abs_margin, mub=0.0):
     """The ray column (n, 32) and threshold T0 (n,), as the kernel builds them:
-    the negated features, -1, -1 against S', T0's hi, lo against 1, 1."""
+    the negated features, -1, -1 against S', T0's hi, lo against 1, 1 (mub:
+    the block-bound tile's extra margin muB in T0_B)."""
     o, e, k1, oo, o2 = ray_constants(rays)
     sc = F(2.0 ** sq)
     with np.errstate(invalid="ignore", over="ignore"):
         feats = [fma32(F(2.0) * k1, e[:, a], o2[:, a]) for a in range(3)]
         feats += [((F(2.0) * e[:, a] if a != b else e[:, a]) * e[:, b]) * sc for a, b in QUAD]
-        T0 = (fma32(-k1, k1, F(1.0 - M - MU) * oo) - F(abs_margin)).astype(F)
+        T0 = (fma32(-k1, k1, F(1.0 - M - MU - mub) * oo) - F(abs_margin)).astype(F)
     his, los = [], []
     for x in feats:
         hi, lo = split(-x)
@@ -252,3 +260,68 @@ def test_scale_is_the_whole_scenes():
     assert scene_rows("rtiow")[1] == qscale(SCENES["rtiow"]())
     full = SCENES["spheres10k"]()
     assert scene_rows("spheres10k")[1] == qscale(full)
+
+
+MUB = 2.0 ** -7  # rt_dev_intersect.h RT_MF_MUB
+
+
+def round_up_f32(v):
+    f = np.float32(v)
+    return float(np.nextafter(f, np.float32(np.inf))) if float(f) < v else float(f)
+
+
+def block_bounds(sp, perm, nblk):
+    """rt_api.cpp build_mfma's block bounds: per 32 walk positions the box
+    centre C (f32) of the members, L = max(|c - C| (1 + 2^-40) + r (1 +
+    2^-18)), R^2 = (1 + 2^-3) L^2 (1 + 2^-40) + 2^-60 and S'_B = R^2 - (1 - m -
+    mu' - muB)|C|^2 rounded up (+inf beyond 2^15, -inf for an empty block)."""
+    c_all = sp["center"].astype(F).astype(D)
+    r2_all = (sp["radius"] * sp["radius"]).astype(F).astype(D)
+    kB = 1.0 - M - MU - MUB
+    C = np.zeros((nblk, 3))
+    S = np.full(nblk, -np.inf)
+    for b in range(nblk):
+        idx = perm[32 * b:32 * b + 32]
+        idx = idx[idx >= 0]
+        if len(idx) == 0:
+            continue
+        c = c_all[idx]
+        C[b] = ((c.min(0) + c.max(0)) * 0.5).astype(F).astype(D)
+        Lm = np.max(np.linalg.norm(c - C[b], axis=1) * (1 + 2.0 ** -40) + np.sqrt(r2_all[idx]) * (1 + 2.0 ** -18))
+        R2 = (1 + 2.0 ** -3) * Lm * Lm * (1 + 2.0 ** -40) + 2.0 ** -60
+        SB = round_up_f32((R2 - kB * (C[b] ** 2).sum()) * (1 + 2.0 ** -40) + 2.0 ** -60)
+        S[b] = SB if abs(SB) <= 2.0 ** 15 else np.inf
+    return C, S
+
+
+@pytest.mark.parametrize("name", sorted(SCENES))
+def test_block_bounds_are_conservative(name):
+    """The walk skips a 32-sphere block for a half-wave when no ray of the
+    half has V_B < 0 on the block's bound row (rt_dev_intersect.h "Block
+    bounds"): every exact hit of a member sphere must have V_B < 0, in every
+    summation order, on the adversarial ray sets (rays in the walk's domain:
+    mfma_wave_ok and |d|^2 in [2^-100, 2^100])."""
+    from bevy_raytrace_amd import abi
+    full = SCENES[name]()
+    sq = qscale(full)
+    perm = abi.cull_layout(full)[0]
+    nblk = (len(perm) - 8) // 32  # whole clusters (+ one pad group)
+    C, S = block_bounds(full, perm, nblk)
+    A = rows_of(C, S, sq)
+    sp = full[:SUBSET.get(name, len(full))]
+    rays = _rays(sp, "blk" + name, 6_000 if len(sp) < 1000 else 2_000)
+    d = rays[:, 3:].astype(F)
+    dd = (d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2]
+    rays = rays[(dd >= 2.0 ** -100) & (dd <= 2.0 ** 100)]
+    Bc, _ = ray_columns(rays, sq, 2.0 ** (sq - 20), MUB)
+    hits = exact_hits(sp, rays)  # (rays, spheres of the subset)
+    pos = np.full(len(full), -1)
+    pos[perm[perm >= 0]] = np.nonzero(perm >= 0)[0]
+    blk = pos[:len(sp)] // 32  # block of each checked sphere
+    assert hits.sum() > 500
+    for order in ORDERS:
+        with np.errstate(invalid="ignore", over="ignore"):
+            passed = mfma_sum(A, Bc, order) < 0  # (rays, blocks)
+        lost = hits & ~passed[:, blk]
+        assert not lost.any(), (f"{order}: {int(lost.sum())} exact hits in skipped blocks, e.g. "
+                                f"{np.argwhere(lost)[0].tolist()}")

@@ -8,6 +8,7 @@ set -uo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$1
 shift
+mkdir -p "$R/$O"
 cd /tmp && export TMPDIR=/tmp
 FPL=${FPL:-2}
 CMD="python3 $R/bench.py --steps $FPL --warmup 0 --frames-per-launch $FPL --no-cpu-baseline --reuse-steps 0 --cull-steps 0 $*"
