@@ -1047,6 +1047,7 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
         for (uint32_t t = 0; t < 2; ++t) {
             if (t) __builtin_amdgcn_sched_barrier(0);
             if ((((t ? m1 : m0) >> (b & 31u)) & 1u) == 0u) continue;  // no ray of the half near the block
+            PROF_ADD(10, 1);  // tiles walked
 #if defined(RT_SENS_MFMA) || defined(RT_SENS_VALU)
             f16x H = __builtin_amdgcn_mfma_f32_32x32x16_f16(
 #else

@@ -9,6 +9,7 @@ ENV_TO_KNOB = {
     "RT_TAIL_SPLIT": "tail_split", "RT_TAIL": "tail", "RT_PREFETCH": "prefetch",
     "RT_PRIO": "prio_mode", "RT_PRIO_SHIFT": "prio_shift", "RT_WG_PER_CU": "wg_per_cu",
     "RT_WIDE_MAX": "wide_max", "RT_FAST_EXACT": "fast_exact", "RT_BLOCK_REGION": "block_region",
+    "RT_MF_CULL": "mf_cull", "RT_DIRECT_OUT": "direct_out",
 }
 
 

@@ -102,10 +102,16 @@ def passes(C, R, rays):
     oc = C - o
     tc = np.einsum("ij,ij->i", oc, dn)
     d2 = np.einsum("ij,ij->i", oc, oc) - np.maximum(tc, 0) ** 2
+    if MARGIN:  # the bound row's margins: R^2 (1 + 2^-3) + muB (|o|^2 + |C|^2)
+        R2 = R * R * (1 + 2.0 ** -3) + 2.0 ** -7 * (np.einsum("ij,ij->i", o, o) + C @ C)
+        R = np.sqrt(R2)
     inside = np.einsum("ij,ij->i", oc, oc) <= R * R
+    if LINE:  # the filter's test: the infinite line, either direction
+        return (np.einsum("ij,ij->i", oc, oc) - tc ** 2) <= R * R * (1 + 1e-6)
     return inside | ((tc >= 0) & (d2 <= R * R * (1 + 1e-6)))
 
 
+allsegs = [np.concatenate(paths[q]) for q in range(n)]
 orders = {"list": np.arange(len(sph)), "morton": morton_order(sph[:, :3].astype(np.float64))}
 # the big spheres (r > 0.5) in blocks of their own at the front, rest Morton
 big = np.nonzero(np.abs(sph[:, 3]) > 0.5)[0]
@@ -138,17 +144,31 @@ def kd_order(idx, c):
 orders["big_block+kd"] = np.concatenate([big, -np.ones((-len(big)) % 32, np.int64),
                                          np.array(kd_order(small, sph[:, :3].astype(np.float64)))])
 trials = 4000
+MIX = int(os.environ.get("MIX", "0"))
+MARGIN = os.environ.get("MARGIN", "0") == "1"
+WEIGHT = os.environ.get("WEIGHT", "1") == "1"  # pairs weighted by their iterations
+LINE = os.environ.get("LINE", "0") == "1"  # line test (what the bound tile computes)
 for name, order in orders.items():
     bnd = bounds(order)
     skip = np.zeros(len(bnd))
     skip_seg1 = np.zeros(len(bnd))
+    # a half-wave spends iterations in proportion to its pixels' path
+    # lengths: draw pairs weighted by their mean segments per path
+    seg_w = np.array([np.mean([len(paths[q][k]) + len(paths[q + pairs][k]) for k in range(nsamp)])
+                      for q in range(pairs)])
+    seg_w = seg_w / seg_w.sum()
     for t in range(trials):
-        p = rng.integers(0, pairs)
-        lanes = [p] * 20 + [p + pairs] * 12
+        p = rng.choice(pairs, p=seg_w) if WEIGHT else rng.integers(0, pairs)
+        if MIX:  # lanes from MIX random pixels (the queue's chunk mixing)
+            lanes = list(rng.integers(0, 2 * pairs, MIX).repeat(32 // MIX))
+        else:
+            lanes = [p] * 20 + [p + pairs] * 12
         rays = []
         for q in lanes:
-            path = paths[q][rng.integers(0, nsamp)]
-            rays.append(path[rng.integers(0, len(path))])
+            # a lane's state at a random iteration: uniform over ALL segments
+            # of the pixel's paths (long paths hold the lane longer)
+            allseg = allsegs[q]
+            rays.append(allseg[rng.integers(0, len(allseg))])
         rays = np.array(rays)
         for b, (C, R) in enumerate(bnd):
             if not passes(C, R, rays).any():
