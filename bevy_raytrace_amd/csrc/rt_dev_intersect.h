@@ -974,7 +974,7 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
         const h8v C01 = as_h8(c0), C11 = as_h8(c1);
         for (uint32_t k = 0; k < nchunk; ++k) {
             // the next chunk's fragments load while this chunk's tiles run
-            const uint4* pb = mf.B + (size_t)(k + 1u < nchunk ? k + 1u : k) * 128u;
+            const uint4* pb = mf.B + (size_t)RT_IDX(k + 1u < nchunk ? k + 1u : k, nchunk, RT_SITE_MF_BOUND) * 128u;
             const uint4 nq0 = pb[lane], nq1 = pb[64u + lane];
             h8v F0, F1;
             __builtin_memcpy(&F0, &bq0, 16);
@@ -1119,7 +1119,7 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
     // bytes): 1.5 KB per block instead of 2 (rt_api.cpp build_mfma).
     const uint32_t off1 = lane < 32u ? lane : lane + 32u;
     auto load = [&](uint32_t p, uint4& x0, uint4& x1) {
-        const uint4* pa = mfA + (size_t)p * RT_MF_BLK;
+        const uint4* pa = mfA + (size_t)RT_IDX(p, nblk, RT_SITE_MFA) * RT_MF_BLK;
         x0 = pa[lane];
         x1 = pa[off1];
     };

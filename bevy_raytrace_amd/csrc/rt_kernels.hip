@@ -99,6 +99,7 @@ enum RtSite : uint32_t {
     RT_SITE_PERM = 18,       // culled list: perm[idx]
     RT_SITE_MFA = 19,        // matrix-core walk: A-fragment block
     RT_SITE_DEAD_QUEUE = 20, // matrix-core walk: a lane without a ray queued a candidate
+    RT_SITE_MF_BOUND = 21,   // matrix-core walk: block-bound chunk
 };
 #ifdef RT_CHECK_BOUNDS
 __device__ unsigned int g_rt_check[4];  // violations, first (site, index, bound)

@@ -12,12 +12,14 @@ from collections import defaultdict
 
 d = sys.argv[1]
 rows = defaultdict(list)
+wall = defaultdict(list)
 for f in sorted(glob.glob(os.path.join(d, "ab_*_[0-9].json"))):
     kind = re.match(r"ab_(.+)_\d+\.json$", os.path.basename(f)).group(1)
     j = json.load(open(f))
     r = j["roofline"]
     cyc = r["kernel_ms_per_launch"] * r["clock_ghz_run"]
     rows[kind].append(cyc)
+    wall[kind].append(r["kernel_ms_per_launch"])
     print(f"{os.path.basename(f):28s} {j['value']:10.1f} Mrays/s {j['ms_per_step']:8.3f} ms/step "
           f"{r['kernel_ms_per_launch']:9.3f} ms {r['clock_ghz_run']:.4f} GHz {cyc:8.2f} Mcyc "
           f"frac {r['frac']}")
@@ -27,4 +29,6 @@ if rows.get("base"):
         if k == "base":
             continue
         n = sum(v) / len(v)
-        print(f"mean Mcyc per launch: base {b:.2f}, {k} {n:.2f} ({(n / b - 1) * 100:+.2f} %)")
+        bw, nw = sum(wall["base"]) / len(wall["base"]), sum(wall[k]) / len(wall[k])
+        print(f"mean Mcyc per launch: base {b:.2f}, {k} {n:.2f} ({(n / b - 1) * 100:+.2f} %); "
+              f"ms {bw:.2f} vs {nw:.2f} ({(nw / bw - 1) * 100:+.2f} %)")
