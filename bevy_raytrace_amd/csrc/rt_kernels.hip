@@ -141,6 +141,17 @@ __device__ unsigned long long g_chunk_clk[RT_CHUNK_TRACE_MAX];  // shader clock 
 __device__ unsigned long long g_wave_trace[RT_TRACE_MAX_WAVES * 4];
 #endif
 
+#ifdef RT_RAY_DUMP
+// Diagnostic build only (-DRT_RAY_DUMP): every lane's ray (o, pixel; d,
+// bounce) of waves 0..RT_RAY_DUMP_WAVES-1 at their loop iteration
+// RT_RAY_DUMP_ITER, read back with rt_debug_ray_dump() (tools/ray_dump.py).
+#define RT_RAY_DUMP_WAVES 1024
+#ifndef RT_RAY_DUMP_ITER
+#define RT_RAY_DUMP_ITER 5000
+#endif
+__device__ float4 g_ray_dump[RT_RAY_DUMP_WAVES * 64 * 2];
+#endif
+
 #ifndef RT_PARAMS_HOLD
 // The launch parameters re-read from the kernarg segment where they are used
 // (scalar loads) instead of being held in SGPRs across the whole loop: the
@@ -376,6 +387,22 @@ __device__ __forceinline__ void render_body(
 #endif
         PROF_MARK(0);
         PROF_ADD(4, 1);
+#ifdef RT_PROFILE
+        {   // diagnostic: distinct pixels per half-wave (c[6]) and lanes at bounce 0 (c[14])
+            uint64_t rest = rt_ballot(has_item);
+            uint32_t distinct = 0;
+            while (rest) {
+                const uint32_t l0 = (uint32_t)__builtin_ctzll(rest);
+                const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)st.pix, (int)l0);
+                const uint64_t half = l0 < 32u ? 0x00000000FFFFFFFFull : 0xFFFFFFFF00000000ull;
+                const uint64_t same = rt_ballot(has_item && st.pix == p0) & half;
+                rest &= ~same;
+                ++distinct;
+            }
+            PROF_ADD(6, distinct);
+            PROF_ADD(14, (unsigned long long)__popcll(rt_ballot(has_item && st.bounce == 0)));
+        }
+#endif
         PROF_ADD(9, (unsigned long long)__popcll(rt_ballot(has_item)));
 
         // ---- opt-in camera sampling: a lane at bounce 0 holds a fresh sample
@@ -386,6 +413,16 @@ __device__ __forceinline__ void render_body(
             sampled_primary_ray(P, st.pix - y * P.width, y, idx, st.o, st.d);
         }
 
+#ifdef RT_RAY_DUMP
+        if (iter == RT_RAY_DUMP_ITER) {
+            const uint32_t wid = blockIdx.x * (RT_BLOCK_THREADS / 64) + threadIdx.x / 64;
+            if (wid < RT_RAY_DUMP_WAVES) {
+                const uint32_t k = (wid * 64u + lane) * 2u;
+                g_ray_dump[k] = make_float4(st.o.x, st.o.y, st.o.z, __uint_as_float(has_item ? st.pix : 0xFFFFFFFFu));
+                g_ray_dump[k + 1] = make_float4(st.d.x, st.d.y, st.d.z, __uint_as_float(st.bounce));
+            }
+        }
+#endif
         // ---- intersect (intersect.wgsl:145-163): every lane with an item holds
         // a ray that needs tracing here.
         int hi = -1;
@@ -894,6 +931,15 @@ int rt_debug_wave_trace(unsigned long long* out, uint32_t max_waves) {
     if (max_waves > RT_TRACE_MAX_WAVES) max_waves = RT_TRACE_MAX_WAVES;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_trace),
                                (size_t)max_waves * 4 * sizeof(unsigned long long)) == hipSuccess
+               ? (int)max_waves : -1;
+}
+#endif
+
+#ifdef RT_RAY_DUMP
+int rt_debug_ray_dump(float* out, uint32_t max_waves) {
+    if (max_waves > RT_RAY_DUMP_WAVES) max_waves = RT_RAY_DUMP_WAVES;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ray_dump), (size_t)max_waves * 64 * 2 * sizeof(float4)) ==
+                   hipSuccess
                ? (int)max_waves : -1;
 }
 #endif

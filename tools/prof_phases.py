@@ -46,5 +46,6 @@ for case in cases:
           f" | cand-groups/iter {c[5] / it:.2f} drain-max/iter {c[6] / it:.2f} "
           f"exact wave-max {c[13] / it:.2f} full {c[14] / it:.2f} flushes/iter {c[11] / it:.3f} "
           f"groups(VALU)/tiles(MFMA) per iter {c[10] / it:.2f} exact lane-mean {c[15] / max(c[9], 1):.2f} "
-          f"c14/lane {c[14] / max(c[9], 1):.2f}",
+          f"c14/lane {c[14] / max(c[9], 1):.2f} | MFMA runs: distinct pixels per half {c[6] / it / 2:.2f}, "
+          f"bounce-0 lanes share {c[14] / max(c[9], 1):.2f}",
           flush=True)
