@@ -557,8 +557,13 @@ static void cull_layout(const float4* sph, const float* S, const float2* rm, uin
         split(b + cut, e);
     };
     split(0, kd.size());
+    // the large spheres padded to a whole 32-sphere block, so that the k-d
+    // subtrees of 32 that follow are exactly the matrix-core walk's blocks
+    // (padded to a group only, the blocks straddled subtrees: RTIOW bound
+    // radii 4.3-11.4 instead of 3.5-4.8)
     std::vector<uint32_t> order = big;
-    while (order.size() % RT_GROUP) order.push_back(0xFFFFFFFFu);
+    if (!big.empty())
+        while (order.size() % 32) order.push_back(0xFFFFFFFFu);
     for (uint32_t i : kd) order.push_back(i);
     while (order.size() % RT_GROUP) order.push_back(0xFFFFFFFFu);
     L.ngroups = (uint32_t)(order.size() / RT_GROUP);
