@@ -820,15 +820,19 @@ static int build_mfma(rt_ctx* ctx) {
     }
     // block bounds (rt_dev_intersect.h "Block bounds"): per chunk of 32
     // blocks, rows = the blocks' bounding spheres in the sphere rows' layout
-    const uint32_t nchunk = (nblk + 31) / 32;
+    // two bounds per block, one per half (16 spheres; a block is walked for a
+    // half-wave when either passes): bound row r of chunk k = half r & 1 of
+    // block 16 k + (r >> 1), so one chunk of 32 rows covers 16 blocks
+    const uint32_t nchunk = (nblk + 15) / 16;
     std::vector<uint16_t> hb((size_t)nchunk * 128 * 8);
     const double kB = 1.0 - 0x1p-16 - 0x1p-16 - 0x1p-7;  // 1 - m - mu' - muB
     for (uint32_t r = 0; r < nchunk * 32; ++r) {
         const uint32_t k = r / 32, j = r & 31;
+        const uint32_t p0 = 16 * r;  // the half-block's first walk position
         double lo3[3] = {INFINITY, INFINITY, INFINITY}, hi3[3] = {-INFINITY, -INFINITY, -INFINITY};
         bool any = false;
-        if (r < nblk)
-            for (uint32_t p = 32 * r; p < 32 * r + 32; ++p) {
+        if (r < 2 * nblk)
+            for (uint32_t p = p0; p < p0 + 16; ++p) {
                 if (L.perm[p] == 0xFFFFFFFFu) continue;
                 any = true;
                 const float4 q = msph[p];
@@ -842,7 +846,7 @@ static int build_mfma(rt_ctx* ctx) {
         if (any) {
             for (int a = 0; a < 3; ++a) C[a] = (double)(float)((lo3[a] + hi3[a]) * 0.5);
             double Lm = 0.0;
-            for (uint32_t p = 32 * r; p < 32 * r + 32; ++p) {
+            for (uint32_t p = p0; p < p0 + 16; ++p) {
                 if (L.perm[p] == 0xFFFFFFFFu) continue;
                 const float4 q = msph[p];
                 const double dx = q.x - C[0], dy = q.y - C[1], dz = q.z - C[2];

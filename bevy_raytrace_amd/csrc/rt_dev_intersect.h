@@ -675,7 +675,8 @@ typedef float f16x __attribute__((ext_vector_type(16)));
 // tests/test_mfma_filter.py restates this arithmetic and checks it.
 //
 // Block bounds (mf.B). The list is walked in the culled list's spatial order
-// (rt_api.cpp build_mfma), and each 32-sphere block has a bounding sphere (C,
+// (rt_api.cpp build_mfma), and each 16-sphere half of a 32-sphere block has a
+// bounding sphere (a block is walked when either half's passes) (C,
 // L = max_i (|C - c_i| + r_i (1 + 2^-18)), R^2 = (1 + 2^-3) L^2 + 2^-60) whose
 // bound row is a sphere row with S'_B = R^2 - (1 - m - mu' - muB)|C|^2 (rounded
 // up; muB = 2^-7), tested against the ray column with T0_B = (1 - m - mu' -
@@ -959,9 +960,11 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
     // the filter's with the bound margin muB in its threshold (T0_B; proof in
     // the header above). A wave with a live ray outside |d|^2 in [2^-100,
     // 2^100] (the proof's domain) walks every block.
-    const uint32_t nchunk = (nblk + 31u) >> 5;
-    uint32_t mv0 = 0xFFFFFFFFu, mv1 = 0xFFFFFFFFu;  // lane k: chunk k's masks, halves 0 / 1
+    const uint32_t nchunk = (nblk + 31u) >> 5;   // of the walk: 32 blocks
+    const uint32_t nbchunk = (nblk + 15u) >> 4;  // of the bounds: 16 blocks, 2 bounds each
+    uint32_t mv0 = 0xFFFFFFFFu, mv1 = 0xFFFFFFFFu;  // lane k: walk chunk k's masks, halves 0 / 1
     if (mf.B != nullptr && rt_ballot(live && !(dd >= 0x1p-100f && dd <= 0x1p100f)) == 0) {
+        mv0 = mv1 = 0u;
         const float TB =
             live ? __builtin_fmaf(-k1, k1, (1.0f - m_ - RT_MF_MU - RT_MF_MUB) * oo) - mf_abs : INFINITY;
         uint32_t h8b = pk(-f[8], TB);  // (hi x8, T0_B hi)
@@ -972,9 +975,9 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
         const uint32_t c0[4] = {b0[1][0], r13[0], r14[0], b0[1][3]};
         const uint32_t c1[4] = {b1[1][0], r13[1], r14[1], b1[1][3]};
         const h8v C01 = as_h8(c0), C11 = as_h8(c1);
-        for (uint32_t k = 0; k < nchunk; ++k) {
+        for (uint32_t k = 0; k < nbchunk; ++k) {
             // the next chunk's fragments load while this chunk's tiles run
-            const uint4* pb = mf.B + (size_t)RT_IDX(k + 1u < nchunk ? k + 1u : k, nchunk, RT_SITE_MF_BOUND) * 128u;
+            const uint4* pb = mf.B + (size_t)RT_IDX(k + 1u < nbchunk ? k + 1u : k, nbchunk, RT_SITE_MF_BOUND) * 128u;
             const uint4 nq0 = pb[lane], nq1 = pb[64u + lane];
             h8v F0, F1;
             __builtin_memcpy(&F0, &bq0, 16);
@@ -992,9 +995,21 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
                 const uint64_t bm = rt_ballot(g < 0);
                 mk2[t] = (uint32_t)bm | (uint32_t)(bm >> 32);
             }
-            if (lane == k) {
-                mv0 = mk2[0];
-                mv1 = mk2[1];
+            // bound rows 2i, 2i + 1 are block 16 k + i's halves: its bit is
+            // their OR, the 16 block bits compressed from the even positions
+            auto fold = [](uint32_t m) {
+                m = (m | (m >> 1)) & 0x55555555u;
+                m = (m | (m >> 1)) & 0x33333333u;
+                m = (m | (m >> 2)) & 0x0F0F0F0Fu;
+                m = (m | (m >> 4)) & 0x00FF00FFu;
+                m = (m | (m >> 8)) & 0x0000FFFFu;
+                return m;
+            };
+            const uint32_t sh = (k & 1u) * 16u;
+            const uint32_t f0 = fold(mk2[0]) << sh, f1 = fold(mk2[1]) << sh;
+            if (lane == (k >> 1)) {
+                mv0 |= f0;
+                mv1 |= f1;
             }
         }
     }

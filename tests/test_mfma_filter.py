@@ -270,18 +270,19 @@ def round_up_f32(v):
     return float(np.nextafter(f, np.float32(np.inf))) if float(f) < v else float(f)
 
 
-def block_bounds(sp, perm, nblk):
-    """rt_api.cpp build_mfma's block bounds: per 32 walk positions the box
-    centre C (f32) of the members, L = max(|c - C| (1 + 2^-40) + r (1 +
-    2^-18)), R^2 = (1 + 2^-3) L^2 (1 + 2^-40) + 2^-60 and S'_B = R^2 - (1 - m -
-    mu' - muB)|C|^2 rounded up (+inf beyond 2^15, -inf for an empty block)."""
+def block_bounds(sp, perm, nblk, size=16):
+    """rt_api.cpp build_mfma's bounds: per `size` walk positions (half a
+    32-sphere block) the box centre C (f32) of the members, L = max(|c - C|
+    (1 + 2^-40) + r (1 + 2^-18)), R^2 = (1 + 2^-3) L^2 (1 + 2^-40) + 2^-60 and
+    S'_B = R^2 - (1 - m - mu' - muB)|C|^2 rounded up (+inf beyond 2^15, -inf
+    for an empty one); nblk counts bounds."""
     c_all = sp["center"].astype(F).astype(D)
     r2_all = (sp["radius"] * sp["radius"]).astype(F).astype(D)
     kB = 1.0 - M - MU - MUB
     C = np.zeros((nblk, 3))
     S = np.full(nblk, -np.inf)
     for b in range(nblk):
-        idx = perm[32 * b:32 * b + 32]
+        idx = perm[size * b:size * b + size]
         idx = idx[idx >= 0]
         if len(idx) == 0:
             continue
@@ -297,7 +298,7 @@ def block_bounds(sp, perm, nblk):
 @pytest.mark.parametrize("name", sorted(SCENES))
 def test_block_bounds_are_conservative(name):
     """The walk skips a 32-sphere block for a half-wave when no ray of the
-    half has V_B < 0 on the block's bound row (rt_dev_intersect.h "Block
+    half has V_B < 0 on either of the block's two half-block bound rows (rt_dev_intersect.h "Block
     bounds"): every exact hit of a member sphere must have V_B < 0, in every
     summation order, on the adversarial ray sets (rays in the walk's domain:
     mfma_wave_ok and |d|^2 in [2^-100, 2^100])."""
@@ -305,7 +306,7 @@ def test_block_bounds_are_conservative(name):
     full = SCENES[name]()
     sq = qscale(full)
     perm = abi.cull_layout(full)[0]
-    nblk = (len(perm) - 8) // 32  # whole clusters (+ one pad group)
+    nblk = (len(perm) - 8) // 16  # half-block bounds over whole clusters (+ one pad group)
     C, S = block_bounds(full, perm, nblk)
     A = rows_of(C, S, sq)
     sp = full[:SUBSET.get(name, len(full))]
@@ -317,7 +318,7 @@ def test_block_bounds_are_conservative(name):
     hits = exact_hits(sp, rays)  # (rays, spheres of the subset)
     pos = np.full(len(full), -1)
     pos[perm[perm >= 0]] = np.nonzero(perm >= 0)[0]
-    blk = pos[:len(sp)] // 32  # block of each checked sphere
+    blk = pos[:len(sp)] // 16  # the half-block bound of each checked sphere
     assert hits.sum() > 500
     for order in ORDERS:
         with np.errstate(invalid="ignore", over="ignore"):
