@@ -823,8 +823,14 @@ static int build_mfma(rt_ctx* ctx) {
     // two bounds per block, one per half (16 spheres; a block is walked for a
     // half-wave when either passes): bound row r of chunk k = half r & 1 of
     // block 16 k + (r >> 1), so one chunk of 32 rows covers 16 blocks
+    // A bound row has K 31 = 1, against the ray column's -RN_f16(2^-7 |o|^2)
+    // (the margin muB|o|^2 of T0_B; sphere rows have 0 there). Each chunk
+    // also holds the bounds' forward rows (rt_dev_intersect.h "Forward
+    // bounds"; v_mfma_f32_32x32x8_f16 B fragments, 8 bytes per lane at uint2
+    // 256 + lane): C hi x3, 1 | L' (rounded up), 0 x3 against the ray's dn
+    // hi x3, c0 hi | 1, 0 x3.
     const uint32_t nchunk = (nblk + 15) / 16;
-    std::vector<uint16_t> hb((size_t)nchunk * 128 * 8);
+    std::vector<uint16_t> hb((size_t)nchunk * RT_MF_BCHUNK * 8);
     const double kB = 1.0 - 0x1p-16 - 0x1p-16 - 0x1p-7;  // 1 - m - mu' - muB
     for (uint32_t r = 0; r < nchunk * 32; ++r) {
         const uint32_t k = r / 32, j = r & 31;
@@ -843,6 +849,7 @@ static int build_mfma(rt_ctx* ctx) {
                 }
             }
         double C[3] = {0.0, 0.0, 0.0}, SB = -INFINITY;  // empty: never passes
+        double Lf = 0.0;  // the forward row's L' (empty: 0, never reached)
         if (any) {
             for (int a = 0; a < 3; ++a) C[a] = (double)(float)((lo3[a] + hi3[a]) * 0.5);
             double Lm = 0.0;
@@ -857,13 +864,29 @@ static int build_mfma(rt_ctx* ctx) {
             const double CC = C[0] * C[0] + C[1] * C[1] + C[2] * C[2];
             SB = (double)round_up_f32((R2 - kB * CC) * (1.0 + 0x1p-40) + 0x1p-60);
             if (!(std::fabs(SB) <= 0x1p15)) SB = INFINITY;  // out of the split's range: always passes
+            // L' = (1 + 2^-3) L + 2^-7 |C|_1 + 2^-14, rounded up; +inf (the
+            // forward row always passes) with the line row's or beyond f16
+            const double C1 = std::fabs(C[0]) + std::fabs(C[1]) + std::fabs(C[2]);
+            Lf = (1.0 + 0x1p-3) * Lm + 0x1p-7 * C1 + 0x1p-14;
+            if (std::isinf(SB) || !(Lf <= 0x1p15)) Lf = INFINITY;
         }
         uint16_t row[32];
         make_row(C, SB, row);
-        uint16_t* blk = &hb[(size_t)k * 128 * 8];
+        row[31] = f16_bits(1.0);  // against the ray's -RN_f16(muB |o|^2)
+        uint16_t* blk = &hb[(size_t)k * RT_MF_BCHUNK * 8];
         for (int hh = 0; hh < 2; ++hh)
             for (int half = 0; half < 2; ++half)  // B0: K 0..15, B1: K 16..31
                 std::memcpy(&blk[((size_t)half * 64 + 32 * hh + j) * 8], &row[16 * half + 8 * hh], 16);
+        uint16_t fw[8] = {};
+        for (int a = 0; a < 3; ++a) fw[a] = f16_bits(C[a]);
+        fw[3] = f16_bits(1.0);  // against the ray's c0
+        fw[4] = f16_bits(Lf);   // against the ray's 1; rounded up below
+        {
+            _Float16 hv;
+            std::memcpy(&hv, &fw[4], 2);
+            if ((double)hv < Lf) ++fw[4];  // the next f16 up (Lf > 0)
+        }
+        for (int hh = 0; hh < 2; ++hh) std::memcpy(&blk[(size_t)128 * 8 + (32 * hh + j) * 4], &fw[4 * hh], 8);
     }
     int rc = ensure(ctx, &ctx->d_mfA, &ctx->mfA_cap, h.size() * sizeof(uint16_t));
     if (!rc) rc = ensure(ctx, &ctx->d_mfB, &ctx->mfB_cap, hb.size() * sizeof(uint16_t));

@@ -679,8 +679,10 @@ typedef float f16x __attribute__((ext_vector_type(16)));
 // bounding sphere (a block is walked when either half's passes) (C,
 // L = max_i (|C - c_i| + r_i (1 + 2^-18)), R^2 = (1 + 2^-3) L^2 + 2^-60) whose
 // bound row is a sphere row with S'_B = R^2 - (1 - m - mu' - muB)|C|^2 (rounded
-// up; muB = 2^-7), tested against the ray column with T0_B = (1 - m - mu' -
-// muB)|o|^2 - k1^2 - abs'. A half-wave skips a block whose bound no ray of
+// up; muB = 2^-7) and K 31 = 1, tested against the walk's own ray column,
+// whose K 31 holds -RN_f16(muB |o|^2) (0 in sphere rows): T0_B = T0 -
+// RN_f16(muB |o|^2) = (1 - m - mu' - muB')|o|^2 - k1^2 - abs' with muB' within
+// 2^-11 muB of muB (the slack below is 2^-8 wide). A half-wave skips a block whose bound no ray of
 // the half passes (V_B >= 0 in every lane). Why a skipped block holds no hit:
 // a member sphere i the exact test hits is a candidate of the packed VALU
 // filter (its proof, ray_filter_consts), so by the culled list's bound proof
@@ -696,6 +698,22 @@ typedef float f16x __attribute__((ext_vector_type(16)));
 // for every live lane, else the wave walks every block. Bound rows of blocks
 // with an out-of-range bound always pass (S'_B hi = +inf), of empty blocks
 // never (-inf).
+//
+// Forward bounds. A bound is also skipped for a ray when it lies wholly behind
+// the ray's origin. Any hit of a member sphere i (root >= EPSILON > 0) has
+// half_b < 0 or |o - c_i|^2 < r_i^2 (1 + 2^-20) in f32 (else exact_core's
+// certain-miss shortcut holds), so in exact arithmetic dn.(c_i - o) >=
+// -r_i (1 + 2^-20) - 2^-20 (|o| + |c_i|), and dn.(C - o) >= -L - 2^-20 (|o| +
+// |C| + L). The forward row (rt_api.cpp build_mfma; one
+// v_mfma_f32_32x32x8_f16 per half) computes U = dn_hi.C_hi + c0_hi + L'_hi,
+// c0 = fma(2^-7, |o|_1, -k1) (k1 = dn.o), L' = (1 + 2^-3) L + 2^-7 |C|_1 +
+// 2^-14 rounded UP to f16 (+inf, always passing, where the line row does or
+// beyond 2^15). The f16 parts cost <= 2^-9.9 |C|_1 (dn_hi C_hi) and
+// 2^-10.8 |o|_1 (c0_hi), v_rsq and the f32 sums <= 2^-20 (|C|_1 + |o|_1 + L'),
+// all inside the 2^-3 L + 2^-7 (|C|_1 + |o|_1) + 2^-14 slack: a hit's bound
+// has U > 0, and the tile passes a (ray, bound) pair iff V_B < 0 and U >= +0
+// (tile_or_fwd; tests/test_mfma_filter.py test_forward_bounds_are_conservative
+// checks it numerically in five summation orders).
 #define RT_MF_MU 0x1p-16f
 #define RT_MF_MUB 0x1p-7f  // the block-bound tile's extra margin (see "Block bounds")
 #ifndef RT_MF_CAP
@@ -818,6 +836,23 @@ __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, ui
 __device__ __forceinline__ uint32_t or3_dual(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0xFE);
 }
+// The bound tile's pass flag with the forward rows: the OR over the lane's 16
+// (ray, bound) pairs of V & ~U -- the sign bit set iff some pair has V < 0
+// (the line passes near) and U >= +0 (the bound is not behind the origin):
+// 16 v_bitop3_b32 ((a & ~b) | c, function 0xBA; dual-issued) in four chains,
+// then one 3-input OR and an OR.
+__device__ __forceinline__ uint32_t tile_or_fwd(const f16x& V, const f16x& U) {
+    uint32_t acc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        acc[q] = __builtin_amdgcn_bitop3_b32(__float_as_uint(V[4 * q]), __float_as_uint(U[4 * q]), 0u, 0xBA);
+#pragma unroll
+        for (int i = 1; i < 4; ++i)
+            acc[q] = __builtin_amdgcn_bitop3_b32(__float_as_uint(V[4 * q + i]), __float_as_uint(U[4 * q + i]),
+                                                 acc[q], 0xBA);
+    }
+    return or3_dual(acc[0], acc[1], acc[2]) | acc[3];
+}
 __device__ __forceinline__ void tile_or(const f16x& H, int* gq, int& g) {
     uint32_t v[16];
 #pragma unroll
@@ -851,6 +886,7 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
     // load stays unconditional, so hipcc's vmcnt waits count exactly)
     const uint4* pb0 = mf.B != nullptr ? mf.B : mfA;
     uint4 bq0 = pb0[__lane_id()], bq1 = pb0[64u + __lane_id()];
+    uint2 bq2 = reinterpret_cast<const uint2*>(pb0)[(mf.B != nullptr ? 256u : 0u) + __lane_id()];
     const float dd = dot(d, d);
     const float l = sqrt_x(dd);
     const float a = l * l;  // sqr(length(r.dir)), intersect.wgsl:98
@@ -925,7 +961,9 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
         w[12] = pk(x8, l8);
         w[13] = h8t;
         w[14] = pk(tl, -1.0f);
-        w[15] = pk(-1.0f, 0.0f);
+        // K 31: -RN_f16(muB |o|^2) against a bound row's 1 (T0_B's margin,
+        // "Block bounds") and a sphere row's 0
+        w[15] = pk(-1.0f, -(RT_MF_MUB * oo));
     }
     // B fragments of K group g (K 16g..16g+15), half t: lane l holds column
     // l & 31, k = 16g + 8 (l >> 5) .. + 8. v_permlane32_swap(lo, hi) swaps lo's
@@ -955,44 +993,58 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
     // passes near. The bound tile is the TRANSPOSED product -- the rays'
     // fragments as the A operand (rows), the chunk's 32 block bounds as B
     // (columns; their fragments have the sphere rows' layout, which is B's) --
-    // so lane l holds bound l & 31 against 16 of the half's rays and one OR
-    // tree + one ballot give the half's 32-bit block mask. The ray column is
-    // the filter's with the bound margin muB in its threshold (T0_B; proof in
-    // the header above). A wave with a live ray outside |d|^2 in [2^-100,
-    // 2^100] (the proof's domain) walks every block.
+    // so lane l holds bound l & 31 against 16 of the half's rays, and the
+    // AND-NOT / OR tree of the line tile V_B and the forward tile U + one
+    // ballot give the half's 32-bit bound mask. The ray column is the walk's
+    // own (a bound row's K 31 = 1 picks up its -muB |o|^2: T0_B; "Block
+    // bounds" and "Forward bounds" in the header above). A wave with a live
+    // ray outside |d|^2 in [2^-100, 2^100] (the proof's domain) walks every
+    // block.
     const uint32_t nchunk = (nblk + 31u) >> 5;   // of the walk: 32 blocks
     const uint32_t nbchunk = (nblk + 15u) >> 4;  // of the bounds: 16 blocks, 2 bounds each
     uint32_t mv0 = 0xFFFFFFFFu, mv1 = 0xFFFFFFFFu;  // lane k: walk chunk k's masks, halves 0 / 1
     if (mf.B != nullptr && rt_ballot(live && !(dd >= 0x1p-100f && dd <= 0x1p100f)) == 0) {
         mv0 = mv1 = 0u;
-        const float TB =
-            live ? __builtin_fmaf(-k1, k1, (1.0f - m_ - RT_MF_MU - RT_MF_MUB) * oo) - mf_abs : INFINITY;
-        uint32_t h8b = pk(-f[8], TB);  // (hi x8, T0_B hi)
-        asm volatile("" : "+v"(h8b));
-        const float tlb = live ? TB - half_f32(h8b, 1) : 0.0f;
-        const auto r13 = __builtin_amdgcn_permlane32_swap(w[9], h8b, false, false);
-        const auto r14 = __builtin_amdgcn_permlane32_swap(w[10], pk(tlb, -1.0f), false, false);
-        const uint32_t c0[4] = {b0[1][0], r13[0], r14[0], b0[1][3]};
-        const uint32_t c1[4] = {b1[1][0], r13[1], r14[1], b1[1][3]};
-        const h8v C01 = as_h8(c0), C11 = as_h8(c1);
+        // the forward column (rt_api.cpp build_mfma; "Forward bounds"), K 0..7
+        // of v_mfma_f32_32x32x8_f16: dn = -e hi x3, c0 = fma(2^-7, |o|_1, -k1)
+        // hi | 1, 0 x3 -- lanes 32..63 of a half's fragment hold the constant
+        // K 4..7
+        typedef _Float16 h4v __attribute__((ext_vector_type(4)));
+        h4v G0, G1;
+        {
+            const float c0 = __builtin_fmaf(0x1p-7f, fabsf(o.x) + fabsf(o.y) + fabsf(o.z), -k1);
+            const uint32_t u0 = pk(-ex, -ey), u1 = pk(-ez, c0);
+            const uint32_t k4 = pk(1.0f, 0.0f), k6 = 0u;
+            const auto r0 = __builtin_amdgcn_permlane32_swap(u0, k4, false, false);
+            const auto r1 = __builtin_amdgcn_permlane32_swap(u1, k6, false, false);
+            const uint2 g0 = make_uint2(r0[0], r1[0]), g1 = make_uint2(r0[1], r1[1]);
+            __builtin_memcpy(&G0, &g0, 8);
+            __builtin_memcpy(&G1, &g1, 8);
+        }
         for (uint32_t k = 0; k < nbchunk; ++k) {
-            // the next chunk's fragments load while this chunk's tiles run
-            const uint4* pb = mf.B + (size_t)RT_IDX(k + 1u < nbchunk ? k + 1u : k, nbchunk, RT_SITE_MF_BOUND) * 128u;
-            const uint4 nq0 = pb[lane], nq1 = pb[64u + lane];
+            // chunk 0's fragments were loaded first; a later chunk's load here
+            // (no prefetch: its registers would spill, and up to 512 spheres
+            // have one chunk)
+            if (k != 0u) {
+                const uint4* pb = mf.B + (size_t)RT_IDX(k, nbchunk, RT_SITE_MF_BOUND) * RT_MF_BCHUNK;
+                bq0 = pb[lane];
+                bq1 = pb[64u + lane];
+                bq2 = reinterpret_cast<const uint2*>(pb)[256u + lane];
+            }
             h8v F0, F1;
+            h4v F2;
             __builtin_memcpy(&F0, &bq0, 16);
             __builtin_memcpy(&F1, &bq1, 16);
-            bq0 = nq0;
-            bq1 = nq1;
+            __builtin_memcpy(&F2, &bq2, 8);
             uint32_t mk2[2];
 #pragma unroll
             for (uint32_t t = 0; t < 2; ++t) {
                 const f16x V = __builtin_amdgcn_mfma_f32_32x32x16_f16(
-                    t ? C11 : C01, F1, __builtin_amdgcn_mfma_f32_32x32x16_f16(t ? B10 : B00, F0, zero, 0, 0, 0),
+                    t ? B11 : B01, F1, __builtin_amdgcn_mfma_f32_32x32x16_f16(t ? B10 : B00, F0, zero, 0, 0, 0),
                     0, 0, 0);
-                int gq[4], g;
-                tile_or(V, gq, g);
-                const uint64_t bm = rt_ballot(g < 0);
+                const f16x U = __builtin_amdgcn_mfma_f32_32x32x8f16(t ? G1 : G0, F2, zero, 0, 0, 0);
+                const uint32_t acc = tile_or_fwd(V, U);
+                const uint64_t bm = rt_ballot((int)acc < 0);
                 mk2[t] = (uint32_t)bm | (uint32_t)(bm >> 32);
             }
             // bound rows 2i, 2i + 1 are block 16 k + i's halves: its bit is

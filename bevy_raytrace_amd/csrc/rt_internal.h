@@ -30,6 +30,7 @@
 // uint4 entries of one 32-sphere block of matrix-core A fragments: A0 for 64
 // lanes + A1 for lanes 32..63 (lanes 0..31 of A1 equal their A0; build_mfma)
 #define RT_MF_BLK 96u
+#define RT_MF_BCHUNK 160u  // uint4 entries per bound chunk: line rows K 0..31, forward rows K 0..7
 #define RT_GROUP 8            // spheres per filter group (SoA, 128 B)
 #ifndef RT_SLOT_BUF_CAP
 #define RT_SLOT_BUF_CAP 32    // slot-store buffer entries per wave (rt_kernels.hip)

@@ -67,7 +67,7 @@ def sphere_rows(sp, sq):
     return rows_of(c, S, sq)
 
 
-def rows_of(c, S, sq):
+def rows_of(c, S, sq, bound=False):
     """A rows (f32 values of the f16 parts, K = 32) of centres c (n, 3) and
     constants S' (n,); an infinite S' is its hi part alone (build_mfma)."""
     def hl(x):
@@ -91,7 +91,7 @@ def rows_of(c, S, sq):
     # K group 0: hi y0..y7, lo y0..y7; group 1: hi y0..y7, hi y8, hi y8, lo y8,
     # 1, 1, S' hi, S' lo, 0 (build_mfma's words w0..w15)
     cols = his[:8] + los[:8] + his[:8] + [his[8], his[8], los[8], one, one, shi, slo,
-                                          np.zeros(n, H16)]
+                                          one if bound else np.zeros(n, H16)]
     return np.stack(cols, 1).astype(F)
 
 
@@ -109,16 +109,18 @@ def ray_constants(rays):
     return o, e, k1, oo, two * o
 
 
-def ray_columns(rays, sq, abs_margin, mub=0.0):
+def ray_columns(rays, sq, abs_margin):
     """The ray column (n, 32) and threshold T0 (n,), as the kernel builds them:
-    the negated features, -1, -1 against S', T0's hi, lo against 1, 1 (mub:
-    the block-bound tile's extra margin muB in T0_B)."""
+    the negated features, -1, -1 against S', T0's hi, lo against 1, 1, and
+    K 31 = -RN_f16(muB |o|^2) (against 0 in a sphere row, 1 in a block-bound
+    row: T0_B's margin)."""
     o, e, k1, oo, o2 = ray_constants(rays)
     sc = F(2.0 ** sq)
     with np.errstate(invalid="ignore", over="ignore"):
         feats = [fma32(F(2.0) * k1, e[:, a], o2[:, a]) for a in range(3)]
         feats += [((F(2.0) * e[:, a] if a != b else e[:, a]) * e[:, b]) * sc for a, b in QUAD]
-        T0 = (fma32(-k1, k1, F(1.0 - M - MU - mub) * oo) - F(abs_margin)).astype(F)
+        T0 = (fma32(-k1, k1, F(1.0 - M - MU) * oo) - F(abs_margin)).astype(F)
+        k31 = (-(F(MUB) * oo)).astype(H16).astype(F)
     his, los = [], []
     for x in feats:
         hi, lo = split(-x)
@@ -129,7 +131,7 @@ def ray_columns(rays, sq, abs_margin, mub=0.0):
         thi, tlo = split(T0)
     # the kernel's words w0..w15: hi x0..x7 twice, lo x0..x7, (hi x8, lo x8),
     # (hi x8, T0 hi), (T0 lo, -1), (-1, 0)
-    cols = his[:8] + his[:8] + los[:8] + [his[8], los[8], his[8], thi, tlo, m1, m1, z]
+    cols = his[:8] + his[:8] + los[:8] + [his[8], los[8], his[8], thi, tlo, m1, m1, k31]
     return np.stack(cols, 1), T0
 
 
@@ -270,7 +272,7 @@ def round_up_f32(v):
     return float(np.nextafter(f, np.float32(np.inf))) if float(f) < v else float(f)
 
 
-def block_bounds(sp, perm, nblk, size=16):
+def block_bounds(sp, perm, nblk, size=16, return_forward=False):
     """rt_api.cpp build_mfma's bounds: per `size` walk positions (half a
     32-sphere block) the box centre C (f32) of the members, L = max(|c - C|
     (1 + 2^-40) + r (1 + 2^-18)), R^2 = (1 + 2^-3) L^2 (1 + 2^-40) + 2^-60 and
@@ -281,6 +283,7 @@ def block_bounds(sp, perm, nblk, size=16):
     kB = 1.0 - M - MU - MUB
     C = np.zeros((nblk, 3))
     S = np.full(nblk, -np.inf)
+    Lf = np.zeros(nblk)  # the forward rows' L' (0 for an empty bound)
     for b in range(nblk):
         idx = perm[size * b:size * b + size]
         idx = idx[idx >= 0]
@@ -292,7 +295,44 @@ def block_bounds(sp, perm, nblk, size=16):
         R2 = (1 + 2.0 ** -3) * Lm * Lm * (1 + 2.0 ** -40) + 2.0 ** -60
         SB = round_up_f32((R2 - kB * (C[b] ** 2).sum()) * (1 + 2.0 ** -40) + 2.0 ** -60)
         S[b] = SB if abs(SB) <= 2.0 ** 15 else np.inf
+        lf = (1 + 2.0 ** -3) * Lm + 2.0 ** -7 * np.abs(C[b]).sum() + 2.0 ** -14
+        if np.isinf(S[b]) or not lf <= 2.0 ** 15:
+            Lf[b] = np.inf
+        else:  # rounded up to f16
+            h = np.float16(lf)
+            Lf[b] = float(np.nextafter(h, np.float16(np.inf))) if float(h) < lf else float(h)
+    if return_forward:
+        return C, S, Lf
     return C, S
+
+
+def forward_rows(C, Lf):
+    """rt_api.cpp build_mfma's forward rows (K 0..7 of v_mfma_f32_32x32x8_f16,
+    zero-padded to 32): C hi x3, 1, L' (f16, rounded up)."""
+    n = len(C)
+    cols = [np.zeros(n)] * 32
+    for a in range(3):
+        cols[a] = C[:, a].astype(H16).astype(D)
+    cols[3] = np.ones(n)
+    cols[4] = Lf.astype(H16).astype(D)
+    assert np.all(cols[4] >= Lf)
+    return np.stack(cols, 1).astype(F)
+
+
+def forward_columns(rays):
+    """The kernel's forward column (intersect_world_mfma): dn = -e hi x3, c0 =
+    fma(2^-7, |o|_1, -k1) hi, 1 (zero-padded to 32)."""
+    o, e, k1, _, _ = ray_constants(rays)
+    with np.errstate(invalid="ignore", over="ignore"):
+        o1 = ((np.abs(o[:, 0]) + np.abs(o[:, 1])).astype(F) + np.abs(o[:, 2])).astype(F)
+        c0 = fma32(F(2.0 ** -7), o1, -k1)
+    n = len(rays)
+    cols = [np.zeros(n, F)] * 32
+    for a in range(3):
+        cols[a] = split(-e[:, a])[0]
+    cols[3] = split(c0)[0]
+    cols[4] = np.ones(n, F)
+    return np.stack(cols, 1)
 
 
 @pytest.mark.parametrize("name", sorted(SCENES))
@@ -308,13 +348,13 @@ def test_block_bounds_are_conservative(name):
     perm = abi.cull_layout(full)[0]
     nblk = (len(perm) - 8) // 16  # half-block bounds over whole clusters (+ one pad group)
     C, S = block_bounds(full, perm, nblk)
-    A = rows_of(C, S, sq)
+    A = rows_of(C, S, sq, bound=True)
     sp = full[:SUBSET.get(name, len(full))]
     rays = _rays(sp, "blk" + name, 6_000 if len(sp) < 1000 else 2_000)
     d = rays[:, 3:].astype(F)
     dd = (d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2]
     rays = rays[(dd >= 2.0 ** -100) & (dd <= 2.0 ** 100)]
-    Bc, _ = ray_columns(rays, sq, 2.0 ** (sq - 20), MUB)
+    Bc, _ = ray_columns(rays, sq, 2.0 ** (sq - 20))
     hits = exact_hits(sp, rays)  # (rays, spheres of the subset)
     pos = np.full(len(full), -1)
     pos[perm[perm >= 0]] = np.nonzero(perm >= 0)[0]
@@ -326,3 +366,43 @@ def test_block_bounds_are_conservative(name):
         lost = hits & ~passed[:, blk]
         assert not lost.any(), (f"{order}: {int(lost.sum())} exact hits in skipped blocks, e.g. "
                                 f"{np.argwhere(lost)[0].tolist()}")
+
+
+@pytest.mark.parametrize("name", sorted(SCENES))
+def test_forward_bounds_are_conservative(name):
+    """The bound tile passes a (ray, half-block bound) pair only when its line
+    row passes (V_B < 0) AND its forward row does (U >= +0: the bound is not
+    wholly behind the ray's origin, rt_dev_intersect.h "Forward bounds"): every
+    exact hit of a member sphere must pass both, in every summation order."""
+    from bevy_raytrace_amd import abi
+    full = SCENES[name]()
+    sq = qscale(full)
+    perm = abi.cull_layout(full)[0]
+    nblk = (len(perm) - 8) // 16
+    C, S, Lf = block_bounds(full, perm, nblk, return_forward=True)
+    A = rows_of(C, S, sq, bound=True)
+    Af = forward_rows(C, Lf)
+    sp = full[:SUBSET.get(name, len(full))]
+    rays = _rays(sp, "fwd" + name, 6_000 if len(sp) < 1000 else 2_000)
+    d = rays[:, 3:].astype(F)
+    dd = (d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2]
+    rays = rays[(dd >= 2.0 ** -100) & (dd <= 2.0 ** 100)]
+    Bc, _ = ray_columns(rays, sq, 2.0 ** (sq - 20))
+    Uc = forward_columns(rays)
+    hits = exact_hits(sp, rays)
+    pos = np.full(len(full), -1)
+    pos[perm[perm >= 0]] = np.nonzero(perm >= 0)[0]
+    blk = pos[:len(sp)] // 16
+    assert hits.sum() > 500
+    cut = 0
+    for order in ORDERS:
+        with np.errstate(invalid="ignore", over="ignore"):
+            line = mfma_sum(A, Bc, order) < 0
+            U = mfma_sum(Af, Uc, order)
+        assert not np.isnan(U).any()
+        passed = line & ~np.signbit(U)
+        cut = max(cut, int((line & ~passed).sum()))
+        lost = hits & ~passed[:, blk]
+        assert not lost.any(), (f"{order}: {int(lost.sum())} exact hits in skipped bounds, e.g. "
+                                f"{np.argwhere(lost)[0].tolist()}")
+    assert cut > 0  # the forward rows do cut pairs the line rows pass
