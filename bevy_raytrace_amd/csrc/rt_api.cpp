@@ -860,7 +860,8 @@ static int build_mfma(rt_ctx* ctx) {
                 Lm = std::max(Lm, std::sqrt(dx * dx + dy * dy + dz * dz) * (1.0 + 0x1p-40) +
                                       std::sqrt((double)q.w) * (1.0 + 0x1p-18));
             }
-            const double R2 = (1.0 + 0x1p-3) * Lm * Lm * (1.0 + 0x1p-40) + 0x1p-60;
+            // (1 + 2^-4), not the culled list's (1 + 2^-3): rt_dev_intersect.h "Block bounds"
+            const double R2 = (1.0 + 0x1p-4) * Lm * Lm * (1.0 + 0x1p-40) + 0x1p-60;
             const double CC = C[0] * C[0] + C[1] * C[1] + C[2] * C[2];
             SB = (double)round_up_f32((R2 - kB * CC) * (1.0 + 0x1p-40) + 0x1p-60);
             if (!(std::fabs(SB) <= 0x1p15)) SB = INFINITY;  // out of the split's range: always passes

@@ -677,27 +677,32 @@ typedef float f16x __attribute__((ext_vector_type(16)));
 // Block bounds (mf.B). The list is walked in the culled list's spatial order
 // (rt_api.cpp build_mfma), and each 16-sphere half of a 32-sphere block has a
 // bounding sphere (a block is walked when either half's passes) (C,
-// L = max_i (|C - c_i| + r_i (1 + 2^-18)), R^2 = (1 + 2^-3) L^2 + 2^-60) whose
+// L = max_i (|C - c_i| + r_i (1 + 2^-18)), R^2 = (1 + 2^-4) L^2 + 2^-60) whose
 // bound row is a sphere row with S'_B = R^2 - (1 - m - mu' - muB)|C|^2 (rounded
 // up; muB = 2^-7) and K 31 = 1, tested against the walk's own ray column,
 // whose K 31 holds -RN_f16(muB |o|^2) (0 in sphere rows): T0_B = T0 -
 // RN_f16(muB |o|^2) = (1 - m - mu' - muB')|o|^2 - k1^2 - abs' with muB' within
-// 2^-11 muB of muB (the slack below is 2^-8 wide). A half-wave skips a block whose bound no ray of
-// the half passes (V_B >= 0 in every lane). Why a skipped block holds no hit:
-// a member sphere i the exact test hits is a candidate of the packed VALU
-// filter (its proof, ray_filter_consts), so by the culled list's bound proof
-// (rt_api.cpp, above cull_layout; it holds for any member set) the line's
-// distance from C has dist_C^2 <= (1 + 2^-4 + 2^-8) L^2 + 2^-8 (|o|^2 + |C|^2).
+// 2^-11 muB of muB. A half-wave skips a block whose bounds no ray of the half
+// passes (V_B >= 0 in every lane). Why a skipped block holds no hit: a member
+// sphere i the exact test hits is a candidate of the packed VALU filter (its
+// proof, ray_filter_consts), so by the first steps of the culled list's bound
+// proof (rt_api.cpp, above cull_layout) dist_i <= r_i (1 + 2^-18) +
+// sqrt(delta_i), delta_i = 2^-15 (|o - c_i|^2 + |o|^2 + |c_i|^2) <= 2^-15
+// (6 (|o|^2 + |C|^2) + 4 L^2), and dist_C <= L + sqrt(delta_i); with 2ab <=
+// a^2/32 + 32 b^2 (the culled list uses 1/16, 16):
+//   dist_C^2 <= (1 + 2^-5) L^2 + 33 delta_i
+//            <= (1 + 2^-5 + 2^-7.95) L^2 + 2^-7.37 (|o|^2 + |C|^2).
 // The bound row's exact value is F_B = hb~_C^2 + R^2 - (1 - m)|o - C|^2 +
-// (mu' + muB)(|o|^2 + |C|^2) + abs' >= R^2 - dist_C^2 + (mu' + muB - 2^-18)
-// (|o|^2 + |C|^2) >= (2^-4 - 2^-8) L^2 + 2^-60 + (mu' + 2^-7 - 2^-8 - 2^-18)
-// (|o|^2 + |C|^2), which exceeds the tile's rounding (<= 2^-16.02 (|o|^2 +
-// |C|^2) + 2^-20.4 |S'_B|, the analysis above; |C_i| <= 2^12 as the members',
-// |S'_B| <= 2^15 or the bound row always passes): V_B = T0_B - H0_B < 0. The
-// proof's domain: |o_i| <= 2^12 (mfma_wave_ok) and |d|^2 in [2^-100, 2^100]
-// for every live lane, else the wave walks every block. Bound rows of blocks
-// with an out-of-range bound always pass (S'_B hi = +inf), of empty blocks
-// never (-inf).
+// (mu' + muB')(|o|^2 + |C|^2) + abs' >= R^2 - dist_C^2 + (mu' + muB' - 2^-18)
+// (|o|^2 + |C|^2) >= (2^-5 - 2^-7.95) L^2 + 2^-60 + (2^-7 (1 - 2^-11) -
+// 2^-7.37 - 2^-18)(|o|^2 + |C|^2) (the last factor > 2^-9.3), which exceeds
+// the tile's rounding (<= 2^-16.02 (|o|^2 + |C|^2) + 2^-20.4 |S'_B|, |S'_B| <=
+// R^2 + |C|^2, the analysis above; |C_i| <= 2^12 as the members', |S'_B| <=
+// 2^15 or the bound row always passes): V_B = T0_B - H0_B < 0. The proof's
+// domain: |o_i| <= 2^12 (mfma_wave_ok) and |d|^2 in [2^-100, 2^100] for every
+// live lane, else the wave walks every block. Bound rows of blocks with an
+// out-of-range bound always pass (S'_B hi = +inf), of empty blocks never
+// (-inf).
 //
 // Forward bounds. A bound is also skipped for a ray when it lies wholly behind
 // the ray's origin. Any hit of a member sphere i (root >= EPSILON > 0) has

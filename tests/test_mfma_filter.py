@@ -275,7 +275,7 @@ def round_up_f32(v):
 def block_bounds(sp, perm, nblk, size=16, return_forward=False):
     """rt_api.cpp build_mfma's bounds: per `size` walk positions (half a
     32-sphere block) the box centre C (f32) of the members, L = max(|c - C|
-    (1 + 2^-40) + r (1 + 2^-18)), R^2 = (1 + 2^-3) L^2 (1 + 2^-40) + 2^-60 and
+    (1 + 2^-40) + r (1 + 2^-18)), R^2 = (1 + 2^-4) L^2 (1 + 2^-40) + 2^-60 and
     S'_B = R^2 - (1 - m - mu' - muB)|C|^2 rounded up (+inf beyond 2^15, -inf
     for an empty one); nblk counts bounds."""
     c_all = sp["center"].astype(F).astype(D)
@@ -292,7 +292,7 @@ def block_bounds(sp, perm, nblk, size=16, return_forward=False):
         c = c_all[idx]
         C[b] = ((c.min(0) + c.max(0)) * 0.5).astype(F).astype(D)
         Lm = np.max(np.linalg.norm(c - C[b], axis=1) * (1 + 2.0 ** -40) + np.sqrt(r2_all[idx]) * (1 + 2.0 ** -18))
-        R2 = (1 + 2.0 ** -3) * Lm * Lm * (1 + 2.0 ** -40) + 2.0 ** -60
+        R2 = (1 + 2.0 ** -4) * Lm * Lm * (1 + 2.0 ** -40) + 2.0 ** -60
         SB = round_up_f32((R2 - kB * (C[b] ** 2).sum()) * (1 + 2.0 ** -40) + 2.0 ** -60)
         S[b] = SB if abs(SB) <= 2.0 ** 15 else np.inf
         lf = (1 + 2.0 ** -3) * Lm + 2.0 ** -7 * np.abs(C[b]).sum() + 2.0 ** -14
