@@ -831,7 +831,7 @@ static int build_mfma(rt_ctx* ctx) {
     // hi x3, c0 hi | 1, 0 x3.
     const uint32_t nchunk = (nblk + 15) / 16;
     std::vector<uint16_t> hb((size_t)nchunk * RT_MF_BCHUNK * 8);
-    const double kB = 1.0 - 0x1p-16 - 0x1p-16 - 0x1p-7;  // 1 - m - mu' - muB
+    const double kB = 1.0 - 0x1p-16 - 0x1p-16 - 0x1p-8;  // 1 - m - mu' - muB (RT_MF_MUB)
     for (uint32_t r = 0; r < nchunk * 32; ++r) {
         const uint32_t k = r / 32, j = r & 31;
         const uint32_t p0 = 16 * r;  // the half-block's first walk position

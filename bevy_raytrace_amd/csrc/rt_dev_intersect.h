@@ -679,23 +679,25 @@ typedef float f16x __attribute__((ext_vector_type(16)));
 // bounding sphere (a block is walked when either half's passes) (C,
 // L = max_i (|C - c_i| + r_i (1 + 2^-18)), R^2 = (1 + 2^-4) L^2 + 2^-60) whose
 // bound row is a sphere row with S'_B = R^2 - (1 - m - mu' - muB)|C|^2 (rounded
-// up; muB = 2^-7) and K 31 = 1, tested against the walk's own ray column,
+// up; muB = 2^-8) and K 31 = 1, tested against the walk's own ray column,
 // whose K 31 holds -RN_f16(muB |o|^2) (0 in sphere rows): T0_B = T0 -
 // RN_f16(muB |o|^2) = (1 - m - mu' - muB')|o|^2 - k1^2 - abs' with muB' within
 // 2^-11 muB of muB. A half-wave skips a block whose bounds no ray of the half
 // passes (V_B >= 0 in every lane). Why a skipped block holds no hit: a member
 // sphere i the exact test hits is a candidate of the packed VALU filter (its
-// proof, ray_filter_consts), so by the first steps of the culled list's bound
-// proof (rt_api.cpp, above cull_layout) dist_i <= r_i (1 + 2^-18) +
-// sqrt(delta_i), delta_i = 2^-15 (|o - c_i|^2 + |o|^2 + |c_i|^2) <= 2^-15
-// (6 (|o|^2 + |C|^2) + 4 L^2), and dist_C <= L + sqrt(delta_i); with 2ab <=
-// a^2/32 + 32 b^2 (the culled list uses 1/16, 16):
+// proof, ray_filter_consts), so by the first step of the culled list's bound
+// proof (rt_api.cpp, above cull_layout) dist_i^2 <= r_i^2 (1 + 2^-17) +
+// (m + 2^-19)|o - c_i|^2 + (mu + 2^-17)(|o|^2 + |c_i|^2) <= r_i^2 (1 + 2^-17) +
+// delta_i with delta_i = 2^-14.3 (|o|^2 + |c_i|^2) (|o - c_i|^2 <= 2|o|^2 +
+// 2|c_i|^2) <= 2^-14.3 |o|^2 + 2^-13.3 (|C|^2 + L^2) (|c_i|^2 <= 2|C|^2 +
+// 2L^2); dist_i <= r_i (1 + 2^-18) + sqrt(delta_i), and the line distance is
+// 1-Lipschitz: dist_C <= L + sqrt(delta_i). With 2ab <= a^2/32 + 32 b^2:
 //   dist_C^2 <= (1 + 2^-5) L^2 + 33 delta_i
-//            <= (1 + 2^-5 + 2^-7.95) L^2 + 2^-7.37 (|o|^2 + |C|^2).
+//            <= (1 + 2^-5 + 2^-8.26) L^2 + 2^-8.26 (|o|^2 + |C|^2).
 // The bound row's exact value is F_B = hb~_C^2 + R^2 - (1 - m)|o - C|^2 +
 // (mu' + muB')(|o|^2 + |C|^2) + abs' >= R^2 - dist_C^2 + (mu' + muB' - 2^-18)
-// (|o|^2 + |C|^2) >= (2^-5 - 2^-7.95) L^2 + 2^-60 + (2^-7 (1 - 2^-11) -
-// 2^-7.37 - 2^-18)(|o|^2 + |C|^2) (the last factor > 2^-9.3), which exceeds
+// (|o|^2 + |C|^2) >= (2^-5 - 2^-8.26) L^2 + 2^-60 + (2^-8 (1 - 2^-11) -
+// 2^-8.26 - 2^-18)(|o|^2 + |C|^2) (the last factor > 2^-10.7), which exceeds
 // the tile's rounding (<= 2^-16.02 (|o|^2 + |C|^2) + 2^-20.4 |S'_B|, |S'_B| <=
 // R^2 + |C|^2, the analysis above; |C_i| <= 2^12 as the members', |S'_B| <=
 // 2^15 or the bound row always passes): V_B = T0_B - H0_B < 0. The proof's
@@ -720,7 +722,7 @@ typedef float f16x __attribute__((ext_vector_type(16)));
 // (tile_or_fwd; tests/test_mfma_filter.py test_forward_bounds_are_conservative
 // checks it numerically in five summation orders).
 #define RT_MF_MU 0x1p-16f
-#define RT_MF_MUB 0x1p-7f  // the block-bound tile's extra margin (see "Block bounds")
+#define RT_MF_MUB 0x1p-8f  // the block-bound tile's extra margin (see "Block bounds")
 #ifndef RT_MF_CAP
 #define RT_MF_CAP 12  // queue entries per lane and half (LDS)
 #endif
