@@ -193,6 +193,12 @@ def load(path=None):
     if hasattr(lib, "rt_debug_counters"):  # internal diagnostic symbol
         lib.rt_debug_counters.restype = ctypes.c_int
         lib.rt_debug_counters.argtypes = [_VP, ctypes.POINTER(ctypes.c_uint64)]
+    if hasattr(lib, "rt_debug_counters32"):  # internal diagnostic symbol (RT_PROFILE builds)
+        lib.rt_debug_counters32.restype = ctypes.c_int
+        lib.rt_debug_counters32.argtypes = [_VP, ctypes.POINTER(ctypes.c_uint64)]
+    if hasattr(lib, "rt_debug_intersect_tiles"):  # internal (tests/test_gpu_intersect.py)
+        lib.rt_debug_intersect_tiles.restype = ctypes.c_int
+        lib.rt_debug_intersect_tiles.argtypes = [_VP, ctypes.POINTER(ctypes.c_uint64)]
     if hasattr(lib, "rt_debug_tune"):  # internal A/B knobs (tests, tools/)
         lib.rt_debug_tune.restype = ctypes.c_int
         lib.rt_debug_tune.argtypes = [_VP, ctypes.c_char_p, ctypes.c_char_p]

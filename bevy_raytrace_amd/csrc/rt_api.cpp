@@ -131,6 +131,9 @@ struct rt_ctx {
     float4* d_bnd_c = nullptr;
     uint32_t* d_perm_c = nullptr;
     size_t grp_c_cap = 0, sph_c_cap = 0, shd_c_cap = 0, bnd_c_cap = 0, perm_c_cap = 0;
+    // (radius, material bits) in the culled order, kept so that a material
+    // update rebuilds only d_shd_c (the geometry does not move)
+    std::vector<float2> h_rm_c;
     // matrix-core filter (RT_MFMA_FILTER builds, build_mfma): f16 A fragments
     bool mf_ok = false;
     bool mf_dirty = false;          // rt_update_spheres: fragments rebuilt by mfma_ready
@@ -152,7 +155,10 @@ struct rt_ctx {
     uint32_t head = 0;      // oldest pending slot
     uint32_t npending = 0;  // frames enqueued and not yet waited for
     hipStream_t stream = nullptr;  // = fr[0].stream: scene uploads, intersect, progressive
-    unsigned long long dbg[16] = {};  // diagnostic counters of the last waited frame
+    unsigned long long dbg[RT_DBG_COUNTERS] = {};  // diagnostic counters of the last waited frame
+    // the last rt_intersect's matrix-core walk: (block, half) tiles walked,
+    // and tiles without block bounds (rt_debug_intersect_tiles)
+    unsigned long long isect_tiles[2] = {};
 
     struct HostReg {
         void* ptr;
@@ -505,10 +511,12 @@ static float round_up_f32(double v) {
     return f;
 }
 
-// sph: (cx, cy, cz, r*r) f32 records, S: their filter constants, rm: (radius,
-// material bits), all in the original order, n records.
-static void cull_layout(const float4* sph, const float* S, const float2* rm, uint32_t n,
-                        CullLayout& L) {
+// The spatial order of the list, shared by the culled list (cull_layout) and
+// the matrix-core walk (build_mfma): original indices, 0xFFFFFFFF for a pad
+// position; its length is a multiple of RT_GROUP. sph: (cx, cy, cz, r*r) f32
+// records and S their filter constants, in the original order, n records.
+// O(N log^2 N): a stable sort per k-d level.
+static std::vector<uint32_t> spatial_order(const float4* sph, const float* S, uint32_t n) {
     auto finite_rec = [&](uint32_t i) {
         const float4 q = sph[i];
         return std::isfinite(q.x) && std::isfinite(q.y) && std::isfinite(q.z) && std::isfinite(q.w) &&
@@ -566,6 +574,27 @@ static void cull_layout(const float4* sph, const float* S, const float2* rm, uin
         while (order.size() % 32) order.push_back(0xFFFFFFFFu);
     for (uint32_t i : kd) order.push_back(i);
     while (order.size() % RT_GROUP) order.push_back(0xFFFFFFFFu);
+    return order;
+}
+
+// Walk positions of spatial_order's list for n spheres, at most: the large
+// spheres padded to a whole 32-sphere block (<= 31 pads), the rest to a group
+// (<= 7) -- the matrix-core buffers are sized for it, so rebuilding them after
+// rt_update_spheres (which can move spheres between the large and the rest)
+// never reallocates.
+static uint32_t spatial_order_max(uint32_t n) { return n + 31u + RT_GROUP - 1u; }
+
+// The culled list: spatial_order's list in groups, clusters of 8 groups and
+// supers of 8 clusters with their bounds. rm: (radius, material bits) in the
+// original order.
+static void cull_layout(const float4* sph, const float* S, const float2* rm, uint32_t n,
+                        CullLayout& L) {
+    auto finite_rec = [&](uint32_t i) {
+        const float4 q = sph[i];
+        return std::isfinite(q.x) && std::isfinite(q.y) && std::isfinite(q.z) && std::isfinite(q.w) &&
+               std::isfinite(S[i]);
+    };
+    const std::vector<uint32_t> order = spatial_order(sph, S, n);
     L.ngroups = (uint32_t)(order.size() / RT_GROUP);
     L.nclusters = (L.ngroups + 7) / 8;
     const uint32_t slots = L.nclusters * 8;  // groups the walk may visit
@@ -651,6 +680,14 @@ static void cull_layout(const float4* sph, const float* S, const float2* rm, uin
     }
 }
 
+// The culled list's shading records from h_rm_c and the current materials.
+static int upload_shd_c(rt_ctx* ctx) {
+    std::vector<float4> rec(2 * ctx->h_rm_c.size());
+    shade_records(ctx->h_rm_c.data(), ctx->h_rm_c.size(), ctx->h_mats, rec.data());
+    HIP_TRY(ctx, hipMemcpy(ctx->d_shd_c, rec.data(), sizeof(float4) * rec.size(), hipMemcpyHostToDevice));
+    return RT_OK;
+}
+
 // Rebuild and upload the culled list from the host mirrors (set_scene / update).
 static int build_cull(rt_ctx* ctx) {
     CullLayout L;
@@ -663,11 +700,10 @@ static int build_cull(rt_ctx* ctx) {
     if (rc) return rc;
     HIP_TRY(ctx, hipMemcpy(ctx->d_grp_c, L.grp.data(), sizeof(float4) * L.nrec, hipMemcpyHostToDevice));
     HIP_TRY(ctx, hipMemcpy(ctx->d_sph_c, L.sph.data(), sizeof(float4) * L.nrec, hipMemcpyHostToDevice));
+    ctx->h_rm_c = L.rm;
     {
-        std::vector<float4> rec(2 * (size_t)L.nrec);
-        shade_records(L.rm.data(), L.nrec, ctx->h_mats, rec.data());
-        HIP_TRY(ctx, hipMemcpy(ctx->d_shd_c, rec.data(), sizeof(float4) * rec.size(),
-                               hipMemcpyHostToDevice));
+        int rc2 = upload_shd_c(ctx);
+        if (rc2) return rc2;
     }
     if (!L.bnd.empty())
         HIP_TRY(ctx, hipMemcpy(ctx->d_bnd_c, L.bnd.data(), sizeof(float4) * L.bnd.size(),
@@ -763,15 +799,19 @@ static int build_mfma(rt_ctx* ctx) {
     }
     int sq = 0;
     while (qmax * std::ldexp(1.0, -sq) > 0x1p14) ++sq;  // <= 10 for |c| <= 2^12
-    // the walk's order: the culled list's (large spheres first in groups of
-    // their own, the rest in k-d order), walked in 32-sphere blocks
-    CullLayout L;
-    cull_layout(ctx->h_sph.data(), ctx->h_S.data(), ctx->h_rm.data(), n, L);
-    const uint32_t nblk = (L.ngroups * RT_GROUP + 31) / 32;
+    // the walk's order: the culled list's (large spheres first, padded to a
+    // whole block, the rest in k-d order), walked in 32-sphere blocks; only
+    // the order is computed (no groups or bounds of the culled list)
+    const std::vector<uint32_t> order = spatial_order(ctx->h_sph.data(), ctx->h_S.data(), n);
+    const uint32_t nblk = (uint32_t)((order.size() + 31) / 32);
     // queue entries hold a 14-bit group index (rt_dev_intersect.h mf_spread):
     // larger lists use the VALU filter
     if (nblk > 2048u) return RT_OK;
-    const uint32_t npos = nblk * 32;  // <= L.nrec (whole clusters + a pad group)
+    const uint32_t npos = nblk * 32;
+    auto perm_at = [&](uint32_t p) { return p < order.size() ? order[p] : 0xFFFFFFFFu; };
+    // buffers sized for the largest order n spheres can have: a rebuild after
+    // rt_update_spheres never reallocates (a reserved render allocates nothing)
+    const uint32_t nblk_max = (spatial_order_max(n) + 31) / 32;
     static const int QA[6] = {0, 1, 2, 0, 0, 1}, QB[6] = {0, 1, 2, 1, 2, 2};
     // the row of a sphere or bound (c, S'): K 0..31 (f16 bits); pad: S' = -inf
     auto make_row = [&](const double c[3], double S, uint16_t row[32]) {
@@ -796,7 +836,7 @@ static int build_mfma(rt_ctx* ctx) {
     for (uint32_t p = 0; p < npos; ++p) {
         const uint32_t b = p / 32, l0 = p & 31;
         uint16_t row[32];
-        const uint32_t i = L.perm[p];
+        const uint32_t i = perm_at(p);
         if (i != 0xFFFFFFFFu) {
             const float4 q = ctx->h_sph[i];
             msph[p] = q;
@@ -839,7 +879,7 @@ static int build_mfma(rt_ctx* ctx) {
         bool any = false;
         if (r < 2 * nblk)
             for (uint32_t p = p0; p < p0 + 16; ++p) {
-                if (L.perm[p] == 0xFFFFFFFFu) continue;
+                if (perm_at(p) == 0xFFFFFFFFu) continue;
                 any = true;
                 const float4 q = msph[p];
                 const double c[3] = {q.x, q.y, q.z};
@@ -854,7 +894,7 @@ static int build_mfma(rt_ctx* ctx) {
             for (int a = 0; a < 3; ++a) C[a] = (double)(float)((lo3[a] + hi3[a]) * 0.5);
             double Lm = 0.0;
             for (uint32_t p = p0; p < p0 + 16; ++p) {
-                if (L.perm[p] == 0xFFFFFFFFu) continue;
+                if (perm_at(p) == 0xFFFFFFFFu) continue;
                 const float4 q = msph[p];
                 const double dx = q.x - C[0], dy = q.y - C[1], dz = q.z - C[2];
                 Lm = std::max(Lm, std::sqrt(dx * dx + dy * dy + dz * dz) * (1.0 + 0x1p-40) +
@@ -889,10 +929,11 @@ static int build_mfma(rt_ctx* ctx) {
         }
         for (int hh = 0; hh < 2; ++hh) std::memcpy(&blk[(size_t)128 * 8 + (32 * hh + j) * 4], &fw[4 * hh], 8);
     }
-    int rc = ensure(ctx, &ctx->d_mfA, &ctx->mfA_cap, h.size() * sizeof(uint16_t));
-    if (!rc) rc = ensure(ctx, &ctx->d_mfB, &ctx->mfB_cap, hb.size() * sizeof(uint16_t));
-    if (!rc) rc = ensure(ctx, &ctx->d_mf_sph, &ctx->mf_sph_cap, msph.size() * sizeof(float4));
-    if (!rc) rc = ensure(ctx, &ctx->d_mf_perm, &ctx->mf_perm_cap, mperm.size() * sizeof(uint32_t));
+    const size_t nchunk_max = (nblk_max + 15) / 16;
+    int rc = ensure(ctx, &ctx->d_mfA, &ctx->mfA_cap, (size_t)nblk_max * RT_MF_BLK * 16);
+    if (!rc) rc = ensure(ctx, &ctx->d_mfB, &ctx->mfB_cap, nchunk_max * RT_MF_BCHUNK * 16);
+    if (!rc) rc = ensure(ctx, &ctx->d_mf_sph, &ctx->mf_sph_cap, (size_t)nblk_max * 32 * sizeof(float4));
+    if (!rc) rc = ensure(ctx, &ctx->d_mf_perm, &ctx->mf_perm_cap, (size_t)nblk_max * 32 * sizeof(uint32_t));
     if (rc) return rc;
     HIP_TRY(ctx, hipMemcpy(ctx->d_mfA, h.data(), h.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
     HIP_TRY(ctx, hipMemcpy(ctx->d_mfB, hb.data(), hb.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
@@ -1061,11 +1102,18 @@ int rt_update_materials(rt_ctx* ctx, uint32_t first, const rt_material* material
     rc = quiesce(ctx);
     if (rc) return rc;
     // every sphere's shading record carries its material: all are rebuilt
-    // (O(N) on the host, 32 B per sphere), the culled order's at the next
-    // culled call
+    // (O(N) on the host, 32 B per sphere), in the original order and -- when
+    // the culled list exists -- in its order (its geometry, permutation and
+    // bounds do not change)
     rc = upload_shd(ctx, 0, ctx->h_rm.size());
     if (rc) return rc;
-    ctx->cull_dirty = true;
+    if (!ctx->cull_dirty) {
+        rc = upload_shd_c(ctx);
+        if (rc) {
+            ctx->cull_dirty = true;  // rebuilt whole at the next culled call
+            return rc;
+        }
+    }
     return RT_OK;
 }
 
@@ -1474,7 +1522,7 @@ static int finish(rt_ctx* ctx, Frame& f, rt_stats* st) {
         int rc = check_bounds(ctx, "render");
         if (rc) return rc;
     }
-    for (int i = 0; i < 16; ++i) ctx->dbg[i] = f.h_segs[2 + i];
+    for (int i = 0; i < RT_DBG_COUNTERS; ++i) ctx->dbg[i] = f.h_segs[2 + i];
     if (!st) return RT_OK;
     std::memset(st, 0, sizeof(*st));
     double kms = 0.0;
@@ -1748,6 +1796,7 @@ int rt_intersect_ex(rt_ctx* ctx, const float* rays, uint32_t n, uint32_t flags, 
     if (n == 0) return RT_OK;
     if (!rays || !hit_index || !hit_t)
         return fail(ctx, RT_ERR_INVALID_ARG, "rt_intersect: NULL array");
+    ctx->isect_tiles[0] = ctx->isect_tiles[1] = 0;
     int rc = no_pending(ctx, "rt_intersect");
     if (rc) return rc;
     const bool cull = (flags & RT_FLAG_CULL) != 0;
@@ -1755,9 +1804,12 @@ int rt_intersect_ex(rt_ctx* ctx, const float* rays, uint32_t n, uint32_t flags, 
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     void* buf = nullptr;
     const size_t rb = sizeof(float) * 6 * (size_t)n, ob = sizeof(int32_t) * (size_t)n;
-    HIP_TRY(ctx, hipMalloc(&buf, rb + 2 * ob));
+    const size_t cb = (rb + 2 * ob + 15) & ~(size_t)15;  // the tile counters after the outputs
+    HIP_TRY(ctx, hipMalloc(&buf, cb + 2 * sizeof(unsigned long long)));
     char* b = (char*)buf;
+    unsigned long long* tiles = (unsigned long long*)(b + cb);
     hipError_t e = hipMemcpyAsync(b, rays, rb, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(tiles, 0, 2 * sizeof(unsigned long long), ctx->stream);
     // the brute-force walk takes the render's filter: the matrix-core tiles
     // when the scene fits them (unless RT_FLAG_VALU_FILTER)
     MfScene mf = {};
@@ -1771,12 +1823,15 @@ int rt_intersect_ex(rt_ctx* ctx, const float* rays, uint32_t n, uint32_t flags, 
                                 ctx->scene_fast && ctx->tune.fast_exact ? 1u : 0u,
                                 (const float*)b, n, (int*)(b + rb), (float*)(b + rb + ob),
                                 cull ? ctx->d_bnd_c : nullptr, cull ? ctx->d_perm_c : nullptr,
-                                cull ? ctx->nclusters_c : 0u, &mf, ctx->stream);
+                                cull ? ctx->nclusters_c : 0u, &mf, tiles, ctx->stream);
     }
     if (e == hipSuccess)
         e = hipMemcpyAsync(hit_index, b + rb, ob, hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess)
         e = hipMemcpyAsync(hit_t, b + rb + ob, ob, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(ctx->isect_tiles, tiles, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                           ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     hipFree(buf);
     if (e != hipSuccess)
@@ -1808,11 +1863,30 @@ int rt_debug_cull_layout(const rt_sphere* spheres, uint32_t n, uint32_t* counts,
     return 0;
 }
 
-// Internal (not in include/rt_hip.h): the 16 diagnostic counters of the last
-// waited call; all zero unless the library was built with -DRT_PROFILE.
+// Internal (not in include/rt_hip.h): the first 16 diagnostic counters of the
+// last waited call; all zero unless the library was built with -DRT_PROFILE.
 int rt_debug_counters(const rt_ctx* ctx, uint64_t* out16) {
     if (!ctx || !out16) return RT_ERR_INVALID_ARG;
     for (int i = 0; i < 16; ++i) out16[i] = ctx->dbg[i];
+    return RT_OK;
+}
+
+// Internal: all RT_DBG_COUNTERS (32) diagnostic counters of the last waited
+// call (RT_PROFILE builds; rt_dev_intersect.h "Prof" lists them).
+int rt_debug_counters32(const rt_ctx* ctx, uint64_t* out32) {
+    if (!ctx || !out32) return RT_ERR_INVALID_ARG;
+    for (int i = 0; i < RT_DBG_COUNTERS; ++i) out32[i] = ctx->dbg[i];
+    return RT_OK;
+}
+
+// Internal (tests/test_gpu_intersect.py): the last rt_intersect's matrix-core
+// walk, out2 = (block-half tiles walked, tiles a walk without block bounds
+// visits) summed over its waves; (0, 0) when it took the VALU walk or the
+// culled list. Product build: the batch-query kernel counts, the render does not.
+int rt_debug_intersect_tiles(const rt_ctx* ctx, uint64_t* out2) {
+    if (!ctx || !out2) return RT_ERR_INVALID_ARG;
+    out2[0] = ctx->isect_tiles[0];
+    out2[1] = ctx->isect_tiles[1];
     return RT_OK;
 }
 

@@ -10,8 +10,10 @@ namespace {
 // and wave-level event counts, summed into a debug buffer. Never compiled into
 // the product library.
 #ifdef RT_PROFILE
+// c[0..3], c[7], c[12], c[16..19]: phase clocks (rt_kernels.hip PROF_MARK
+// sites); the rest event counts (tools/prof_phases.py names them all).
 struct Prof {
-    unsigned long long c[16];
+    unsigned long long c[RT_DBG_COUNTERS];
     unsigned long long last;
 };
 #define PROF_DECL Prof prof_ = {};
@@ -518,13 +520,13 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
     }
     PROF_MARK(1);
 #ifdef RT_PROFILE
-    PROF_ADD(6, wave_max_u32(cnt));
+    PROF_ADD(24, wave_max_u32(cnt));  // VALU walk: queue depth (wave max)
 #ifdef RT_PROF_NESTED  // c[14]: the nested drain's wave iterations, sum_k max_lanes popcount(m_k)
     {
         const uint32_t kmax = wave_max_u32(cnt);
         for (uint32_t k = 0; k < kmax; ++k) {
             const uint32_t pc = k < cnt ? (uint32_t)__popc(cq[k * 64 + lane] & 0xFFu) : 0u;
-            PROF_ADD(14, wave_max_u32(pc));
+            PROF_ADD(25, wave_max_u32(pc));
         }
     }
 #endif
@@ -539,10 +541,10 @@ __device__ __forceinline__ int intersect_world(const float4* __restrict__ grp,
     {
         uint32_t sum1 = ecnt[1];
         for (int off = 32; off > 0; off >>= 1) sum1 += __shfl_xor(sum1, off);
-        PROF_ADD(14, sum1);
+        PROF_ADD(25, sum1);
     }
 #else
-    PROF_ADD(14, wave_max_u32(ecnt[1]));
+    PROF_ADD(25, wave_max_u32(ecnt[1]));
 #endif
     {
         uint32_t sum0 = ecnt[0];
@@ -764,9 +766,9 @@ __device__ __forceinline__ bool mfma_wave_ok(v3 o, bool live) {
 }
 
 #ifdef RT_PROFILE
-#define MF_ECNT , uint32_t& ecnt_
+#define MF_ECNT , uint32_t* ecnt_
 #define MF_ECNT_PASS , ecnt_
-#define MF_ECNT_INC ++ecnt_
+#define MF_ECNT_INC
 #else
 #define MF_ECNT
 #define MF_ECNT_PASS
@@ -789,7 +791,7 @@ __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, ui
     const uint32_t na = t ? c1[0] : c0[0], nb = t ? c1[1] : c0[1];
     const uint32_t* q = cq + t * (RT_MF_CAP * 64u);
 #ifdef RT_PROFILE
-    uint32_t ecnt[2] = {0, 0};  // (exact-test counts are not reported for this path)
+    uint32_t* const ecnt = ecnt_;  // [0] exact tests, [1] past the certain-miss shortcut (this lane)
 #endif
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // One loop over the lane's (entry, bit) pairs of both columns, in any
@@ -871,7 +873,11 @@ __device__ __forceinline__ void tile_or(const f16x& H, int* gq, int& g) {
 
 // Called by the whole wave (the MFMA operands span all 64 lanes): lanes
 // without a ray (live false) trace a dummy ray whose threshold is +inf.
-// mf_qs = 2^sq, mf_abs = abs' (build_mfma).
+// mf_qs = 2^sq, mf_abs = abs' (build_mfma). COUNT (the batch query,
+// rt_intersect_mfma_kernel; never the render): tile_cnt[0] += the (block,
+// half) tiles the wave walks, tile_cnt[1] += the 2 nblk it would walk without
+// block bounds (rt_debug_intersect_tiles).
+template <bool COUNT = false>
 __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
                                                     uint32_t scene_fast, v3 o, v3 d, bool live,
                                                     uint64_t live_mask, float& t_out,
@@ -879,7 +885,7 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
 #ifdef RT_PROFILE
                                                     , Prof& prof_
 #endif
-                                                    ) {
+                                                    , unsigned long long* tile_cnt = nullptr) {
     const uint4* __restrict__ mfA = mf.A;
     const uint32_t nblk = mf.nblk;
     const float mf_qs = mf.qs, mf_abs = mf.abs;
@@ -889,11 +895,17 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
         d = mk(0.0f, 0.0f, 1.0f);
     }
     // chunk 0's block-bound fragments, loaded first so that the ray features
-    // cover their latency (from the A fragments when there are no bounds: the
-    // load stays unconditional, so hipcc's vmcnt waits count exactly)
-    const uint4* pb0 = mf.B != nullptr ? mf.B : mfA;
-    uint4 bq0 = pb0[__lane_id()], bq1 = pb0[64u + __lane_id()];
-    uint2 bq2 = reinterpret_cast<const uint2*>(pb0)[(mf.B != nullptr ? 256u : 0u) + __lane_id()];
+    // cover their latency (from block 0's A fragments when there are no
+    // bounds, entries [0, 64) of its RT_MF_BLK: the load stays unconditional,
+    // so hipcc's vmcnt waits count exactly, and in range)
+    const bool has_b = mf.B != nullptr;
+    const uint4* pb0 = has_b ? mf.B : mfA;
+    const uint32_t pb0_n = has_b ? RT_MF_BCHUNK : RT_MF_BLK;  // uint4 entries of chunk / block 0
+    (void)pb0_n;  // (read by the checked build's RT_IDX only)
+    uint4 bq0 = pb0[RT_IDX(__lane_id(), pb0_n, RT_SITE_MF_BOUND)];
+    uint4 bq1 = pb0[RT_IDX((has_b ? 64u : 0u) + __lane_id(), pb0_n, RT_SITE_MF_BOUND)];
+    uint2 bq2 = reinterpret_cast<const uint2*>(pb0)[RT_IDX((has_b ? 256u : 0u) + __lane_id(), 2u * pb0_n,
+                                                           RT_SITE_MF_BOUND)];
     const float dd = dot(d, d);
     const float l = sqrt_x(dd);
     const float a = l * l;  // sqr(length(r.dir)), intersect.wgsl:98
@@ -1010,7 +1022,7 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
     const uint32_t nchunk = (nblk + 31u) >> 5;   // of the walk: 32 blocks
     const uint32_t nbchunk = (nblk + 15u) >> 4;  // of the bounds: 16 blocks, 2 bounds each
     uint32_t mv0 = 0xFFFFFFFFu, mv1 = 0xFFFFFFFFu;  // lane k: walk chunk k's masks, halves 0 / 1
-    if (mf.B != nullptr && rt_ballot(live && !(dd >= 0x1p-100f && dd <= 0x1p100f)) == 0) {
+    if (has_b && rt_ballot(live && !(dd >= 0x1p-100f && dd <= 0x1p100f)) == 0) {
         mv0 = mv1 = 0u;
         // the forward column (rt_api.cpp build_mfma; "Forward bounds"), K 0..7
         // of v_mfma_f32_32x32x8_f16: dn = -e hi x3, c0 = fma(2^-7, |o|_1, -k1)
@@ -1071,7 +1083,9 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
                 mv1 |= f1;
             }
         }
+        PROF_ADD(17, nbchunk);  // bound chunks: 2 halves x (2 MFMA 32x32x16 + 1 MFMA 32x32x8)
     }
+    PROF_MARK(16);  // ray column + bound tiles
 
     float best_t = VERY_FAR;
     int best_i = -1;
@@ -1087,7 +1101,9 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
     asm volatile("" : "+v"(zeroB));
 #endif
 #ifdef RT_PROFILE
-    uint32_t ecnt_ = 0;  // this lane's exact tests (c[13]: wave max, c[15]: lane sum)
+    // this lane's exact tests (c[13]: wave max, c[15]: lane sum) and those
+    // past the certain-miss shortcut (c[21]: lane sum)
+    uint32_t ecnt_[2] = {0, 0};
 #endif
     // wave-uniform upper bounds of every lane's queue length per half (SGPRs):
     // one per group some lane queued from since the last drain
@@ -1151,6 +1167,7 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
                 for (uint32_t q = 0; q < 4; ++q) {
                     if (rt_ballot(gq[q] < 0) == 0) continue;  // no lane has one in this group
                     ++(t ? ub1 : ub0);
+                    PROF_ADD(23, 1);  // group appends (wave-level)
                     const uint32_t m = mf_flags(H[4 * q], H[4 * q + 1], H[4 * q + 2], H[4 * q + 3]);
                     // Branch-free append: every lane writes its next slot
                     // (< RT_MF_CAP: the check above) and keeps it only with a
@@ -1197,11 +1214,14 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
         x0 = pa[lane];
         x1 = pa[off1];
     };
+    uint32_t walked = 0;  // COUNT: tiles walked by the wave
     for (uint32_t k = 0; k < nchunk; ++k) {
         const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)mv0, (int)k);
         const uint32_t m1 = (uint32_t)__builtin_amdgcn_readlane((int)mv1, (int)k);
         const uint32_t rem = nblk - 32u * k;
-        uint32_t todo = (m0 | m1) & (rem >= 32u ? 0xFFFFFFFFu : ((1u << rem) - 1u));
+        const uint32_t valid = rem >= 32u ? 0xFFFFFFFFu : ((1u << rem) - 1u);
+        if (COUNT) walked += (uint32_t)(__popc(m0 & valid) + __popc(m1 & valid));
+        uint32_t todo = (m0 | m1) & valid;
         if (todo == 0u) continue;
         // the next block to walk (the last one again when none is left: its
         // fragments reload from L1, and every load stays unconditional, so
@@ -1228,6 +1248,10 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
             if (!more2) break;
         }
     }
+    if (COUNT && __lane_id() == 0) {
+        atomicAdd(tile_cnt, (unsigned long long)walked);
+        atomicAdd(tile_cnt + 1, 2ull * nblk);
+    }
     PROF_MARK(1);
     const uint32_t cnt0 = qcount(qp0, q0), cnt1 = qcount(qp1, q1);
     if (fast)
@@ -1239,8 +1263,11 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
     PROF_MARK(2);
 #ifdef RT_PROFILE
     {
-        PROF_ADD(13, wave_max_u32(ecnt_));
-        uint32_t sum0 = ecnt_;
+        PROF_ADD(13, wave_max_u32(ecnt_[0]));
+        uint32_t sum1 = ecnt_[1];
+        for (int off = 32; off > 0; off >>= 1) sum1 += __shfl_xor(sum1, off);
+        PROF_ADD(21, sum1);
+        uint32_t sum0 = ecnt_[0];
         for (int off = 32; off > 0; off >>= 1) sum0 += __shfl_xor(sum0, off);
         PROF_ADD(15, sum0);
     }

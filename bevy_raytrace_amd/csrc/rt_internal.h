@@ -14,13 +14,14 @@
 #define RT_WAVE_CHUNK_TAIL 16 // ... in the last 2 x 64 x waves items of the queue
 #endif
 // Counter block at the start of the ctx's counter buffer (u32 words):
-// [0,4) two u64 segment counters, [4,36) 16 u64 diagnostic counters
-// (RT_PROFILE builds), [36,40) two u64 clock sums (the render waves'
-// s_memtime and s_memrealtime deltas: rt_stats.clock_ghz), [40, ...) one u32
+// [0,4) two u64 segment counters, [4,68) 32 u64 diagnostic counters
+// (RT_PROFILE builds), [68,72) two u64 clock sums (the render waves'
+// s_memtime and s_memrealtime deltas: rt_stats.clock_ghz), [72, ...) one u32
 // work counter per pass.
-#define RT_CNT_CLOCK_OFFSET 36
-#define RT_CNT_WORK_OFFSET 40
-#define RT_CNT_U64 20  // u64 counters copied back per call (segments, diagnostics, clocks)
+#define RT_DBG_COUNTERS 32
+#define RT_CNT_CLOCK_OFFSET (4 + 2 * RT_DBG_COUNTERS)
+#define RT_CNT_WORK_OFFSET (RT_CNT_CLOCK_OFFSET + 4)
+#define RT_CNT_U64 (2 + RT_DBG_COUNTERS + 2)  // u64 counters copied back per call (segments, diagnostics, clocks)
 #define RT_TAIL_ITEM 0x80000000u  // PathState::item flag: a tail item (per-sample slots)
 // PathState::item / slot-buffer entry flag: the item covers every sample of
 // its (frame, pixel) and writes the output pixel itself (KParams::dout); the
@@ -198,7 +199,7 @@ hipError_t rt_launch_assemble(const float4* gathered, uint32_t max_rows, uint32_
 hipError_t rt_launch_intersect(const float4* grp, const float4* sph, uint32_t ngroups,
                                uint32_t scene_fast, const float* rays, uint32_t n, int* out_i, float* out_t,
                                const float4* bnd, const uint32_t* perm, uint32_t nclusters,
-                               const MfScene* mf, hipStream_t stream);
+                               const MfScene* mf, unsigned long long* tile_cnt, hipStream_t stream);
 hipError_t rt_render_occupancy(int* blocks_per_cu, int* blocks_per_cu_cull);
 hipError_t rt_launch_primary(const KParams* P, float4* pd, hipStream_t stream);
 #ifdef RT_CHECK_BOUNDS

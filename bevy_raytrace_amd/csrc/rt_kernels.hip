@@ -429,9 +429,11 @@ __device__ __forceinline__ void render_body(
         float t = VERY_FAR;
         const uint64_t live = rt_ballot(has_item);
         if ((uint32_t)__popcll(live) <= P.wide_max) {  // nearly empty wave: sphere-parallel
+            PROF_ADD(20, 1);
             intersect_wide<CULL>(sph, P.nspheres, P.scene_fast, live, st.o, st.d, hi, t, P.perm);
 #ifdef RT_MFMA_FILTER
         } else if (!CULL && P.mf.A && mfma_wave_ok(st.o, has_item)) {  // the whole wave
+            PROF_ADD(18, 1);
             const int h2 = intersect_world_mfma(P.mf, P.scene_fast, st.o, st.d,
                                                 has_item, live, t, cqm
 #ifdef RT_PROFILE
@@ -442,6 +444,7 @@ __device__ __forceinline__ void render_body(
             else t = VERY_FAR;
 #endif
         } else if (has_item) {
+            PROF_ADD(19, 1);
             hi = intersect_world<CULL>(grp, sph, P.ngroups, P.scene_fast, st.o, st.d, t, cq,
 #ifdef RT_PROFILE
                                        prof_,
@@ -465,6 +468,7 @@ __device__ __forceinline__ void render_body(
         for (;;) {
             const uint64_t sh = rt_ballot(shading);
             if (sh == 0) break;
+            PROF_ADD(22, 1);  // shading rounds (wave-level)
             segs = __builtin_amdgcn_readfirstlane(segs + (uint32_t)__popcll(sh));
             if (shading) {
                 const bool done = shade(P, st, hi, t, sph, shd);
@@ -567,7 +571,7 @@ __device__ __forceinline__ void render_body(
     PROF_MARK(7);
     prof_.c[8] = __builtin_amdgcn_s_memtime() - t_begin;
     if (lane == 0)
-        for (int i = 0; i < 16; ++i) atomicAdd(dbg + i, prof_.c[i]);
+        for (int i = 0; i < RT_DBG_COUNTERS; ++i) atomicAdd(dbg + i, prof_.c[i]);
 #endif
 #ifdef RT_WAVE_TRACE
     {
@@ -685,10 +689,13 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_cull_kernel(
 // takes it for every wave whose rays fit the split's range): the whole wave
 // runs the tiles, lanes past n trace a dummy ray that never has a candidate; a
 // wave with a ray outside the range takes the VALU filter, as in the render.
+// tile_cnt: the matrix-core walk's (tiles walked, tiles without block bounds)
+// summed over its waves (rt_debug_intersect_tiles); a VALU-walk wave adds none.
 __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_mfma_kernel(
     const MfScene mf, const float4* __restrict__ grp,
     const float4* __restrict__ sph, uint32_t ngroups, uint32_t scene_fast,
-    const float* __restrict__ rays, uint32_t n, int* __restrict__ out_i, float* __restrict__ out_t) {
+    const float* __restrict__ rays, uint32_t n, int* __restrict__ out_i, float* __restrict__ out_t,
+    unsigned long long* __restrict__ tile_cnt) {
     __shared__ uint32_t s_cq[RT_BLOCK_THREADS * RT_CQ_CAP];
     __shared__ __attribute__((aligned(8))) uint32_t s_cqm[(RT_BLOCK_THREADS / 64) * RT_MF_QW];
     const uint32_t wave = threadIdx.x / 64u;
@@ -711,12 +718,12 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_mfma_kernel(
 #else
     if (mfma_wave_ok(o, live)) {
 #endif
-        hi = intersect_world_mfma(mf, scene_fast, o, d, live, lm, t,
-                                  s_cqm + wave * RT_MF_QW
+        hi = intersect_world_mfma<true>(mf, scene_fast, o, d, live, lm, t,
+                                        s_cqm + wave * RT_MF_QW
 #ifdef RT_PROFILE
-                                  , prof_
+                                        , prof_
 #endif
-                                  );
+                                        , tile_cnt);
     } else if (live) {
         hi = intersect_world<false>(grp, sph, ngroups, scene_fast, o, d, t,
                                     s_cq + wave * (64u * RT_CQ_CAP),
@@ -906,16 +913,18 @@ hipError_t rt_launch_assemble(const float4* gathered, uint32_t max_rows, uint32_
 hipError_t rt_launch_intersect(const float4* grp, const float4* sph, uint32_t ngroups,
                                uint32_t scene_fast, const float* rays, uint32_t n, int* out_i,
                                float* out_t, const float4* bnd, const uint32_t* perm,
-                               uint32_t nclusters, const MfScene* mf, hipStream_t stream) {
+                               uint32_t nclusters, const MfScene* mf, unsigned long long* tile_cnt,
+                               hipStream_t stream) {
     const uint32_t T = RT_BLOCK_THREADS;
 #ifdef RT_MFMA_FILTER
     if (mf && mf->A && !bnd) {
         hipLaunchKernelGGL(rt_intersect_mfma_kernel, dim3((n + T - 1) / T), dim3(T), 0, stream, *mf,
-                           grp, sph, ngroups, scene_fast, rays, n, out_i, out_t);
+                           grp, sph, ngroups, scene_fast, rays, n, out_i, out_t, tile_cnt);
         return hipGetLastError();
     }
 #else
     (void)mf;
+    (void)tile_cnt;
 #endif
     if (bnd)
         hipLaunchKernelGGL(rt_intersect_cull_kernel, dim3((n + T - 1) / T), dim3(T), 0, stream, grp,

@@ -212,10 +212,23 @@ class Renderer:
         return int(self.lib.rt_debug_alloc_count(self.ctx))
 
     def debug_counters(self):
-        """Diagnostic counters of the last call (non-zero only for -DRT_PROFILE builds)."""
-        out = (ctypes.c_uint64 * 16)()
-        self.lib.rt_debug_counters(self.ctx, out)
+        """Diagnostic counters of the last call (non-zero only for -DRT_PROFILE
+        builds): 32 when the library has rt_debug_counters32, else 16."""
+        if hasattr(self.lib, "rt_debug_counters32"):
+            out = (ctypes.c_uint64 * 32)()
+            self.lib.rt_debug_counters32(self.ctx, out)
+        else:
+            out = (ctypes.c_uint64 * 16)()
+            self.lib.rt_debug_counters(self.ctx, out)
         return list(out)
+
+    def intersect_tiles(self):
+        """The last intersect()'s matrix-core walk: (block-half tiles walked,
+        tiles without block bounds), summed over its waves; (0, 0) when it
+        took the VALU walk or the culled list (internal diagnostic)."""
+        out = (ctypes.c_uint64 * 2)()
+        check(self.lib, self.ctx, self.lib.rt_debug_intersect_tiles(self.ctx, out))
+        return int(out[0]), int(out[1])
 
     def assemble_shard_frames(self, gathered_ptr: int, max_rows, frames, image_ptr: int, width,
                               height, row_block, shard_count, stream=None):

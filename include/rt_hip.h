@@ -230,11 +230,13 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n,
  * Replace records [first, first+count) of the current scene; counts N and M
  * are unchanged. Only the touched sphere records and 8-sphere groups are
  * re-packed and uploaded. The matrix-core filter's f16 sphere rows (their
- * scale 2^-sq depends on every centre: O(N) on the host, 64 B per sphere
- * uploaded) are rebuilt once, at the next call that walks them (a caller that
- * renders only the culled list never pays for them); the culled list
- * (RT_FLAG_CULL), which depends on every sphere, likewise at the next culled
- * call. */
+ * scale 2^-sq and their k-d spatial order depend on every centre: O(N log^2 N)
+ * on the host for the order, 64 B per sphere uploaded; buffers sized for the
+ * worst-case order, so the rebuild never allocates) are rebuilt once, at the
+ * next call that walks them (a caller that renders only the culled list never
+ * pays for them); the culled list (RT_FLAG_CULL), which depends on every
+ * sphere, likewise at the next culled call. rt_update_materials rebuilds the
+ * shading records only (both orders, O(N), 32 B per sphere): no geometry. */
 int rt_update_spheres(rt_ctx* ctx, uint32_t first, const rt_sphere* spheres, uint32_t count);
 int rt_update_materials(rt_ctx* ctx, uint32_t first, const rt_material* materials,
                         uint32_t count);

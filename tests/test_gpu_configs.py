@@ -116,7 +116,10 @@ def test_config4_8k_segments_exact(renderer):
 
 def test_config5_10k_full_frame(renderer):
     """The whole 1080p frame with 10,000 spheres (list streamed, not staged):
-    sampled rows bit-exact; the culled list gives the same frame and count."""
+    sampled rows bit-exact; the packed VALU filter over every sphere
+    (RT_FLAG_VALU_FILTER: no block bounds, nothing skipped) and the culled
+    list give the same frame and count as the default matrix-core walk with
+    its block bounds (20 bound chunks)."""
     wl, sp, mt = _scene("spheres10k1080")
     W, H, S, D = wl.width, wl.height, wl.spp, wl.max_depth
     assert len(sp) == 10_000 and (W, H, S, D) == (1920, 1080, 128, 16)
@@ -130,6 +133,10 @@ def test_config5_10k_full_frame(renderer):
     culled, sc = renderer.render(cam, W, H, S, D, flags=NO_REUSE | CULL)
     check_exact(culled, img)
     assert sc["segments"] == st["segments"]
+    del culled
+    valu, sv = renderer.render(cam, W, H, S, D, flags=NO_REUSE | abi.RT_FLAG_VALU_FILTER)
+    check_exact(valu, img)
+    assert sv["segments"] == st["segments"]
 
 
 def test_config5_10k_segments_exact(renderer):

@@ -192,3 +192,74 @@ def test_largest_matrix_core_list(renderer, n):
     bad = np.nonzero((gi != ci) | (gt.view(np.uint32) != ct.view(np.uint32)))[0]
     assert bad.size == 0, f"{bad.size} rays differ, e.g. {bad[:5].tolist()}"
     assert (ci >= n - 4096).sum() > 600 and (ci >= 0).mean() > 0.5
+
+
+def _box_scene(n, lo, hi, rmin, rmax, seed):
+    from bevy_raytrace_amd.abi import SPHERE_DTYPE
+    rng = np.random.default_rng(seed)
+    sp = np.zeros(n, dtype=SPHERE_DTYPE)
+    sp["center"] = rng.uniform(lo, hi, (n, 3)).astype(np.float32)
+    sp["radius"] = rng.uniform(rmin, rmax, n).astype(np.float32)
+    return sp
+
+
+COHERENT = {  # name -> (spheres, half-waves of rays)
+    # the headline's list: 16 blocks, one bound chunk
+    "rtiow": lambda: (scene.rtiow_final_scene().objects_gpu(), 4096),
+    # 2,000 spheres at |c| ~ 140..176: sphere rows near the f16 split's
+    # range (|S'| <= 2^15, rt_api.cpp build_mfma), 63 blocks, 4 bound chunks
+    "cluster_at_range_edge": lambda: (_box_scene(2000, (95, -5, 95), (125, 25, 125), 0.1, 0.8, 11), 2048),
+    # 2,000 spheres in a 80-unit box: 4 bound chunks
+    "random2k": lambda: (_box_scene(2000, (-40, 0, -40), (40, 20, 40), 0.2, 1.0, 12), 2048),
+    # config 5's list: 313 blocks, 20 bound chunks
+    "spheres10k": lambda: (scene.ten_thousand_scene().objects_gpu(), 1024),
+}
+
+
+@pytest.mark.parametrize("name", sorted(COHERENT))
+def test_block_bounds_at_their_decision_boundary(renderer, name):
+    """Block-bound culling on the GPU where it decides (rt_dev_intersect.h
+    "Block bounds" / "Forward bounds"): every 32-ray half-wave is coherent and
+    aimed at ONE 16-sphere half-block -- rays tangent to the member whose far
+    side sets the bound's radius (so their lines pass at the bound's own
+    radius), the same ray replicated 32 times, fans from one origin grazing a
+    member at r (1 +- 1e-8..1e-4), and origins at |o|^2 just below 2^15, the
+    largest the matrix-core walk takes (tests/raygen.py coherent_halves).
+    Such halves skip most blocks: the walk must skip > 30 % of the tiles a
+    walk without bounds visits (rt_debug_intersect_tiles) while index and t
+    stay bit-exact against the oracle; the same rays through every block
+    (knob mf_cull=0) and through the unculled packed VALU filter
+    (RT_FLAG_VALU_FILTER) give the same bits."""
+    from bevy_raytrace_amd import abi
+    from bevy_raytrace_amd.abi import MATERIAL_DTYPE
+    from raygen import coherent_halves
+    sp, halves = COHERENT[name]()
+    perm = abi.cull_layout(sp)[0]
+    rays = coherent_halves(sp, perm, halves, seed=zlib.crc32(name.encode()) % 1000)
+    mt = np.zeros(int(sp["material"].max()) + 1, dtype=MATERIAL_DTYPE)
+    renderer.set_scene(sp, mt)
+    ci, ct = O.intersect_batch(sp, rays)
+    assert (ci >= 0).mean() > 0.2
+
+    def exact(gi, gt, what):
+        bad = np.nonzero((gi != ci) | (gt.view(np.uint32) != ct.view(np.uint32)))[0]
+        assert bad.size == 0, (f"{what}: {bad.size} rays differ, e.g. {bad[:5].tolist()}: gpu "
+                               f"{gi[bad[:5]]} {gt[bad[:5]]} cpu {ci[bad[:5]]} {ct[bad[:5]]}")
+
+    gi, gt = renderer.intersect(rays)
+    walked, total = renderer.intersect_tiles()
+    exact(gi, gt, "block-bound walk")
+    # every wave took the matrix-core walk (|o|^2 <= 2^15, |c| in range): 2
+    # halves x nblk tiles each without bounds -- and skipped
+    nblk = (int(np.nonzero(perm >= 0)[0].max()) + 1 + 31) // 32
+    assert total == 2 * nblk * (-(-len(rays) // 64)), (total, nblk)
+    assert walked <= 0.7 * total, (walked, total)
+    renderer.tune(mf_cull=0)
+    ai, at = renderer.intersect(rays)
+    w_all, t_all = renderer.intersect_tiles()
+    exact(ai, at, "every block (mf_cull=0)")
+    assert w_all == t_all == total
+    renderer.tune(None)
+    vi, vt = renderer.intersect(rays, flags=RT_FLAG_VALU_FILTER)
+    exact(vi, vt, "unculled VALU filter")
+    assert renderer.intersect_tiles() == (0, 0)

@@ -779,16 +779,22 @@ def test_coincident_spheres_queue_flushes(renderer, flags):
 
 
 def test_cull_full_1080p64_identical(renderer):
-    """RT_FLAG_CULL at the headline size: the culled walk's frame and segment
-    counts equal the brute-force walk's, bit for bit (its speed is bench.py's
-    `culled` line, not a test: a shared or throttled box says nothing there)."""
+    """The headline frame through three walks, bit for bit with equal segment
+    counts: the default matrix-core walk with block bounds, the packed VALU
+    filter over EVERY sphere (RT_FLAG_VALU_FILTER: no bounds, no skipping --
+    the unculled reference for the other two) and the culled list
+    (RT_FLAG_CULL). (Speeds are bench.py's, not a test's: a shared or
+    throttled box says nothing there.)"""
+    from bevy_raytrace_amd.abi import RT_FLAG_VALU_FILTER
     sp, mt = arrays(scene.rtiow_final_scene())
     cam = default_camera_block()
     renderer.set_scene(sp, mt)
     b, sb = renderer.render(cam, 1920, 1080, 64, 16, flags=NO_REUSE)
+    v, sv = renderer.render(cam, 1920, 1080, 64, 16, flags=NO_REUSE | RT_FLAG_VALU_FILTER)
+    check_exact(b, v)
     c, sc = renderer.render(cam, 1920, 1080, 64, 16, flags=NO_REUSE | CULL)
-    check_exact(c, b)
-    assert sc["segments"] == sb["segments"] == sc["traced_segments"]
+    check_exact(c, v)
+    assert sc["segments"] == sb["segments"] == sv["segments"] == sc["traced_segments"]
 
 
 @pytest.mark.parametrize("K,k", [(3, 1), (8, 7)])
