@@ -20,10 +20,15 @@ per second, every segment traced (primary-hit reuse off for the headline;
 its frame time is reported separately as `primary_reuse`).
 
 Roofline: SIMD issue, the resource the kernel executes on:
-the render kernel's issue cycles per launch (rocprofv3 PMC record in
-profiles/pmc_traffic.json: 4 per VALU instruction, 2 per 32-bit integer one,
-8 per MFMA) over that launch's duration (HIP events on the stream the kernel
-runs on), against 1024 SIMDs x the profiled clock. The metric's fp32 roofline
+the render kernel's issue cycles per launch, MEASURED from the rocprofv3 PMC
+record of the workload (profiles/pmc_traffic.json, tools/pmc_summary.py):
+4 x (SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2) -- the quad-cycles the VALU
+issue port was held, gfx950's dual-issued pairs counted once -- + 4 x
+SQ_INSTS_MFMA (an MFMA holds the issue 8 cycles), scaled to this run's launch
+(per frame, and per pixel at N > 1), over that launch's duration (HIP events
+on the stream the kernel runs on), against 1024 SIMDs x this run's own shader
+clock (rt_stats.clock_ghz, measured inside the timed launches); the line's
+`formula` and `peak_formula` fields say the same. The metric's fp32 roofline
 (the reference's 18 x N_spheres fp32 flops per segment over 157.3 TF) is kept
 as `fp32_algorithm_ratio`: the kernel runs the brute-force walk's filter as
 f16 MFMA tiles and the exact fp32 test only on candidates, so that ratio
@@ -115,11 +120,40 @@ def load_pmc(workload_key):
 
 def load_traffic(e, frames_per_launch):
     """HBM bytes per render launch from the PMC record, scaled per frame to
-    this run's average launch (block sums and tail samples are per frame)."""
+    this run's average launch (block sums and tail samples are per frame);
+    at N > 1 `frames_per_launch` carries the rank's pixel share too."""
     try:
         return int(e["hbm_bytes_per_launch"] / e["frames_per_launch"] * frames_per_launch)
     except (TypeError, KeyError, ZeroDivisionError):
         return None
+
+
+def load_executed(workload_key):
+    """What the render kernel executes per frame of this workload
+    (profiles/executed.json, tools/executed.py + tools/executed_summary.py:
+    the RT_PROFILE build's counters of one bench-shaped launch)."""
+    path = os.path.join(ROOT, "profiles", "executed.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(workload_key)
+    except (OSError, ValueError):
+        return None
+
+
+def executed_report(ex, frames_per_launch):
+    """The executed-work block of the roofline for one launch of this run
+    (per-frame counts x frames x pixel share): tiles, MFMA flops, exact
+    tests, shading, and the issue shares per phase."""
+    if not ex:
+        return None
+    pf = ex.get("per_frame", {})
+    out = {k: (round(v * frames_per_launch) if isinstance(v, (int, float)) else v)
+           for k, v in pf.items()}
+    for k in ("per_segment", "issue_model", "phase_wave_time_share", "useful_issue_fraction",
+              "source", "note"):
+        if k in ex:
+            out[k] = ex[k]
+    return out
 
 
 def valu_report(e):
@@ -430,6 +464,8 @@ def main():
     packed = (torch.empty((FPL, len(rows), W, 4), dtype=torch.float32, device="cuda")
               if gather_path and len(rows) != max_rows else None)
 
+    gather_events = []  # (start, end) CUDA events around each launch's gather + assembly
+
     def launch(first, nf, flags):
         """Enqueue frames [first, first + nf): render, then (N > 1) one RCCL
         gather of the nf shard slabs to rank 0 and the device re-assembly --
@@ -447,6 +483,8 @@ def main():
             # rank k's nf frames land as slab k of a (world, nf, max_rows, W)
             # view, the layout rt_assemble_shard_frames reads: one assembly
             # launch for the launch's frames
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record(stream)
             g = (gathered.view(-1)[:world * nf * max_rows * W * 4].view(world, nf, max_rows, W, 4)
                  if rank == 0 else None)
             if args.dist_backend == "nccl":
@@ -461,6 +499,9 @@ def main():
             if rank == 0:
                 r.assemble_shard_frames(g.data_ptr(), max_rows, nf, image.data_ptr(), W, H, B,
                                         world, stream=stream.cuda_stream)
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record(stream)
+            gather_events.append((ev0, ev1))
 
     def run(nsteps, flags):
         """nsteps frames in launches of <= FPL frames (near-equal sizes), two
@@ -508,7 +549,9 @@ def main():
             dt = float(t.item())
         return dt, stats, sizes
 
+    gather_events.clear()
     dt, stats, sizes = timed(args.steps, NO_REUSE)
+    gather_ms = sum(a.elapsed_time(b) for a, b in gather_events) if gather_events else 0.0
     # the timed headline run's first frame of its last launch, kept for the
     # parity check below before the reuse / cull runs overwrite the buffer
     head_idx = args.steps - sizes[-1]
@@ -528,13 +571,30 @@ def main():
         dist.all_reduce(tot)
     segs_all, traced_all = float(tot[0].item()), float(tot[1].item())
     per_rank = None
-    if dist_on:  # load balance of the row tiling: each rank's render-kernel time
-        mine = torch.tensor([float(sum(kms)), float(segs_local)], dtype=torch.float64,
-                            device=red_dev)
+    if dist_on:
+        # per rank, over the timed steps: the render kernels (load balance of
+        # the row tiling), the rest of the library calls (the pixel table and
+        # the collect -- on the IPC path the collect's system-scope writes of
+        # the rank's rows into rank 0's image, over xGMI), and on the gather
+        # path the RCCL gather + re-assembly (CUDA events on the bench stream)
+        call_ms = float(sum(s["total_ms"] for s in stats))
+        mine = torch.tensor([float(sum(kms)), float(segs_local), call_ms, gather_ms, dt * 1e3],
+                            dtype=torch.float64, device=red_dev)
         parts = [torch.empty_like(mine) for _ in range(world)]
         dist.all_gather(parts, mine)
-        per_rank = {"kernel_ms": [round(float(p[0].item()), 3) for p in parts],
-                    "segments": [int(p[1].item()) for p in parts]}
+        per_rank = {"path": ("ipc" if use_ipc else
+                             "rccl" if args.dist_backend == "nccl" else "gloo"),
+                    "kernel_ms": [round(float(p[0].item()), 3) for p in parts],
+                    "render_ms": [round(float(p[0].item()), 3) for p in parts],
+                    "transfer_ms": [round(float(p[2].item() - p[0].item()) if use_ipc
+                                          else float(p[3].item()), 3) for p in parts],
+                    "call_ms": [round(float(p[2].item()), 3) for p in parts],
+                    "wall_ms": [round(float(p[4].item()), 3) for p in parts],
+                    "segments": [int(p[1].item()) for p in parts],
+                    "note": ("render_ms: the rank's render kernels; transfer_ms: ipc -- its library "
+                             "calls beyond the render (pixel table + collect writing its rows into "
+                             "rank 0's image), rccl/gloo -- the gather + re-assembly; wall_ms: the "
+                             "timed region on that rank before the max")}
 
     reuse = None
     if args.reuse_steps > 0:
@@ -586,15 +646,22 @@ def main():
     flops_total = traced_local * FLOPS_PER_SPHERE_TEST * nsph
     achieved = flops_total / (kernel_ms_total * 1e-3) / 1e12
     pmc = load_pmc(wl.key)
-    traffic = load_traffic(pmc, args.steps / max(1, len(sizes)))
+    # the PMC and executed-work records are of whole frames on one GPU: a
+    # rank of N renders its rows' share of every frame
+    px_share = len(rows) / H
+    fpl_eff = args.steps / max(1, len(sizes)) * px_share
+    traffic = load_traffic(pmc, fpl_eff)
     kms_launch = kernel_ms_total / launches
     # the shader clock the timed launches ran at (rt_stats.clock_ghz: the
     # render waves' s_memtime ticks over their 100 MHz ticks), launch-time weighted
     clock_run = (sum(s["kernel_ms"] * s["clock_ghz"] for s in stats) / kernel_ms_total
                  if kernel_ms_total > 0 else 0.0)
 
-    roofline = simd_issue_roofline(pmc, args.steps / max(1, len(sizes)), kms_launch, clock_run)
+    roofline = simd_issue_roofline(pmc, fpl_eff, kms_launch, clock_run)
+    if px_share < 1.0:
+        roofline["record_scaled_by_pixel_share"] = round(px_share, 6)
     roofline.update({
+        "executed": executed_report(load_executed(wl.key), fpl_eff),
         "traffic": traffic,
         # HBM GB/s of the render kernel: PMC bytes per launch / this run's
         # HIP-event launch time (peak ~8,000 GB/s: not the bound)

@@ -94,6 +94,13 @@ struct Tuning {
     // the matrix-core walk skips the 32-sphere blocks whose bound no ray of
     // the half-wave passes (MfScene::B); off: every block (same bits)
     bool mf_cull = true;
+    // lists of 2..32 bound chunks test the chunk-level bounds first
+    // (MfScene::top); off: every chunk's block bounds (same bits)
+    bool mf_top = true;
+    // RT_FLAG_IMAGE_OUT: a system-scope release per collect wave after its
+    // write-through stores (off: the stores drained by s_waitcnt vmcnt(0)
+    // only -- A/B)
+    bool dsys_release = true;
 };
 
 struct rt_ctx {
@@ -138,6 +145,7 @@ struct rt_ctx {
     bool mf_ok = false;
     bool mf_dirty = false;          // rt_update_spheres: fragments rebuilt by mfma_ready
     uint32_t mf_nblk = 0;
+    bool mf_top = false;  // a chunk-level bound chunk follows the block bounds (build_mfma)
     float mf_qs = 1.0f;   // 2^sq: the ray side's scale of the quadratic features
     float mf_abs = 0.0f;  // absolute margin of the threshold, 2^(sq - 20)
     uint4* d_mfA = nullptr;
@@ -250,7 +258,7 @@ static bool tune_set(Tuning& t, const char* name, const char* v) {
     } else if (!strcmp(name, "tail_split")) {
         t.tail_split = x != 0;
     } else if (!strcmp(name, "item_order")) {
-        if (x < 0 || x > 3) return false;
+        if (x < 0 || x > 7) return false;
         t.item_order = (uint32_t)x;
     } else if (!strcmp(name, "block_region")) {
         if (x < 0) return false;
@@ -273,6 +281,10 @@ static bool tune_set(Tuning& t, const char* name, const char* v) {
         t.direct_out = x != 0;
     } else if (!strcmp(name, "mf_cull")) {
         t.mf_cull = x != 0;
+    } else if (!strcmp(name, "mf_top")) {
+        t.mf_top = x != 0;
+    } else if (!strcmp(name, "dsys_release")) {
+        t.dsys_release = x != 0;
     } else if (!strcmp(name, "chk_shrink")) {
         if (x != 0 && x != 4 && x != 5 && x != 7 && x != 16) return false;
         t.chk_shrink = (uint32_t)x;
@@ -870,30 +882,35 @@ static int build_mfma(rt_ctx* ctx) {
     // 256 + lane): C hi x3, 1 | L' (rounded up), 0 x3 against the ray's dn
     // hi x3, c0 hi | 1, 0 x3.
     const uint32_t nchunk = (nblk + 15) / 16;
-    std::vector<uint16_t> hb((size_t)nchunk * RT_MF_BCHUNK * 8);
+    // chunk-level bounds (lists of 2..32 bound chunks, 513..16,384 walk
+    // positions): one more chunk after the others, row j = the bound of
+    // chunk j's 512 walk positions, tested first, so a half-wave only tests
+    // the block bounds of the chunks it passes near (rt_dev_intersect.h "Chunk
+    // bounds"; 10,000 spheres: 20 chunks)
+    const bool top = nchunk >= 2 && nchunk <= 32;
+    std::vector<uint16_t> hb((size_t)(nchunk + (top ? 1 : 0)) * RT_MF_BCHUNK * 8);
     const double kB = 1.0 - 0x1p-16 - 0x1p-16 - 0x1p-8;  // 1 - m - mu' - muB (RT_MF_MUB)
-    for (uint32_t r = 0; r < nchunk * 32; ++r) {
-        const uint32_t k = r / 32, j = r & 31;
-        const uint32_t p0 = 16 * r;  // the half-block's first walk position
+    // the bound of walk positions [p0, p1) as row j of bound chunk blk (line
+    // row K 0..31 and forward row K 0..7); no member: never passes
+    auto bound_row = [&](uint32_t p0, uint32_t p1, uint16_t* blk, uint32_t j) {
         double lo3[3] = {INFINITY, INFINITY, INFINITY}, hi3[3] = {-INFINITY, -INFINITY, -INFINITY};
         bool any = false;
-        if (r < 2 * nblk)
-            for (uint32_t p = p0; p < p0 + 16; ++p) {
-                if (perm_at(p) == 0xFFFFFFFFu) continue;
-                any = true;
-                const float4 q = msph[p];
-                const double c[3] = {q.x, q.y, q.z};
-                for (int a = 0; a < 3; ++a) {
-                    lo3[a] = std::min(lo3[a], c[a]);
-                    hi3[a] = std::max(hi3[a], c[a]);
-                }
+        for (uint32_t p = p0; p < p1; ++p) {
+            if (perm_at(p) == 0xFFFFFFFFu) continue;
+            any = true;
+            const float4 q = msph[p];
+            const double c[3] = {q.x, q.y, q.z};
+            for (int a = 0; a < 3; ++a) {
+                lo3[a] = std::min(lo3[a], c[a]);
+                hi3[a] = std::max(hi3[a], c[a]);
             }
+        }
         double C[3] = {0.0, 0.0, 0.0}, SB = -INFINITY;  // empty: never passes
         double Lf = 0.0;  // the forward row's L' (empty: 0, never reached)
         if (any) {
             for (int a = 0; a < 3; ++a) C[a] = (double)(float)((lo3[a] + hi3[a]) * 0.5);
             double Lm = 0.0;
-            for (uint32_t p = p0; p < p0 + 16; ++p) {
+            for (uint32_t p = p0; p < p1; ++p) {
                 if (perm_at(p) == 0xFFFFFFFFu) continue;
                 const float4 q = msph[p];
                 const double dx = q.x - C[0], dy = q.y - C[1], dz = q.z - C[2];
@@ -914,7 +931,6 @@ static int build_mfma(rt_ctx* ctx) {
         uint16_t row[32];
         make_row(C, SB, row);
         row[31] = f16_bits(1.0);  // against the ray's -RN_f16(muB |o|^2)
-        uint16_t* blk = &hb[(size_t)k * RT_MF_BCHUNK * 8];
         for (int hh = 0; hh < 2; ++hh)
             for (int half = 0; half < 2; ++half)  // B0: K 0..15, B1: K 16..31
                 std::memcpy(&blk[((size_t)half * 64 + 32 * hh + j) * 8], &row[16 * half + 8 * hh], 16);
@@ -928,8 +944,18 @@ static int build_mfma(rt_ctx* ctx) {
             if ((double)hv < Lf) ++fw[4];  // the next f16 up (Lf > 0)
         }
         for (int hh = 0; hh < 2; ++hh) std::memcpy(&blk[(size_t)128 * 8 + (32 * hh + j) * 4], &fw[4 * hh], 8);
+    };
+    for (uint32_t r = 0; r < nchunk * 32; ++r) {
+        const uint32_t k = r / 32, j = r & 31;
+        const uint32_t p0 = 16 * r;  // the half-block's first walk position
+        bound_row(p0, r < 2 * nblk ? p0 + 16 : p0, &hb[(size_t)k * RT_MF_BCHUNK * 8], j);
     }
-    const size_t nchunk_max = (nblk_max + 15) / 16;
+    if (top)
+        for (uint32_t j = 0; j < 32; ++j) {
+            const uint32_t p0 = 512 * j, p1 = j < nchunk ? std::min(p0 + 512, npos) : p0;
+            bound_row(p0, p1, &hb[(size_t)nchunk * RT_MF_BCHUNK * 8], j);
+        }
+    const size_t nchunk_max = (nblk_max + 15) / 16 + 1;  // + the chunk-level bounds
     int rc = ensure(ctx, &ctx->d_mfA, &ctx->mfA_cap, (size_t)nblk_max * RT_MF_BLK * 16);
     if (!rc) rc = ensure(ctx, &ctx->d_mfB, &ctx->mfB_cap, nchunk_max * RT_MF_BCHUNK * 16);
     if (!rc) rc = ensure(ctx, &ctx->d_mf_sph, &ctx->mf_sph_cap, (size_t)nblk_max * 32 * sizeof(float4));
@@ -941,6 +967,7 @@ static int build_mfma(rt_ctx* ctx) {
     HIP_TRY(ctx, hipMemcpy(ctx->d_mf_perm, mperm.data(), mperm.size() * sizeof(uint32_t),
                            hipMemcpyHostToDevice));
     ctx->mf_nblk = nblk;
+    ctx->mf_top = top;
     ctx->mf_qs = (float)std::ldexp(1.0, sq);
     ctx->mf_abs = (float)std::ldexp(1.0, sq - 20);
     ctx->mf_ok = true;
@@ -1015,6 +1042,7 @@ static MfScene mf_scene(const rt_ctx* ctx) {
     mf.sph = ctx->d_mf_sph;
     mf.perm = ctx->d_mf_perm;
     mf.nblk = ctx->mf_nblk;
+    mf.top = ctx->mf_top && ctx->tune.mf_top ? 1u : 0u;
     mf.qs = ctx->mf_qs;
     mf.abs = ctx->mf_abs;
     return mf;
@@ -1332,6 +1360,7 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     // 1-spp frame written into a registered host buffer by the render kernel
     // took 2.8 ms of kernel instead of 0.77, profiles/r04/direct/)
     K_.dsys = (p.flags & RT_FLAG_IMAGE_OUT) ? 1u : 0u;
+    K_.dsys_release = tn.dsys_release ? 1u : 0u;
     const bool direct = tn.direct_out && prog_mode == 0 && !passes.empty() && !K_.dsys &&
                         passes[0].block_begin == 0 && passes[0].nblocks == blocks_total &&
                         (K == 1 || (p.flags & RT_FLAG_IMAGE_OUT));
@@ -1435,7 +1464,8 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         K_.ti1 = (uint32_t)((g1 - g0 + 3) / 4 * npix);
         K_.ti2 = K_.ti1 + (uint32_t)((g2 - g1 + 1) / 2 * npix);
         K_.tail_items = K_.ti2 + (uint32_t)((g_end - g2) * npix);
-        K_.item_order = tn.item_order;
+        // grouped order (bit 2) needs whole groups of 8 pixels; else pixel-major
+        K_.item_order = (tn.item_order & 4u) && npix % 8u != 0 ? (tn.item_order & 3u) | 3u : tn.item_order;
         K_.div_nreg = make_fastdiv(K_.qmain > K_.qpix ? K_.qmain - K_.qpix : 1u);
         K_.div_nfpix = make_fastdiv(npix && K_.main_pix ? K_.main_pix / npix : 1u);
         K_.div_ng4 = make_fastdiv(g1 > g0 ? (uint32_t)((g1 - g0 + 3) / 4) : 1u);

@@ -10,8 +10,9 @@ namespace {
 // and wave-level event counts, summed into a debug buffer. Never compiled into
 // the product library.
 #ifdef RT_PROFILE
-// c[0..3], c[7], c[12], c[16..19]: phase clocks (rt_kernels.hip PROF_MARK
-// sites); the rest event counts (tools/prof_phases.py names them all).
+// c[0..3], c[7], c[12], c[16]: phase clocks (rt_kernels.hip PROF_MARK
+// sites), c[26] the diagnostic reductions' own time; the rest event counts
+// (tools/executed.py names them all).
 struct Prof {
     unsigned long long c[RT_DBG_COUNTERS];
     unsigned long long last;
@@ -753,6 +754,14 @@ __device__ __forceinline__ uint32_t mf_flags(float v0, float v1, float v2, float
     return lo | hi;
 }
 
+// The lane id (0..63) as a value the compiler cannot hoist or keep in a
+// register across loops: an address built from it is recomputed at its use.
+__device__ __forceinline__ uint32_t opaque_lane() {
+    uint32_t l = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    asm volatile("" : "+v"(l));
+    return l;
+}
+
 __device__ __forceinline__ uint32_t bperm(uint32_t src_lane, uint32_t v) {
     return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
 }
@@ -774,9 +783,19 @@ __device__ __forceinline__ bool mfma_wave_ok(v3 o, bool live) {
 #define MF_ECNT_PASS
 #define MF_ECNT_INC
 #endif
-template <bool FAST>
+// SP: the drain's record array, global (const float4*) or the workgroup's
+// LDS copy (lds_cfloat4*, RT_MF_SPH_LDS builds).
+typedef __attribute__((address_space(3))) const float4 lds_cfloat4;
+__device__ __forceinline__ float4 rec_load(const float4* __restrict__ p, uint32_t i) { return p[i]; }
+__device__ __forceinline__ float4 rec_load(lds_cfloat4* p, uint32_t i) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) const f4v lds_f4v;
+    const f4v v = ((lds_f4v*)p)[i];  // one ds_read_b128
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+template <bool FAST, typename SP>
 __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, uint32_t cnt1,
-                                           const float4* __restrict__ sph, uint32_t nsph,
+                                           SP sph, uint32_t nsph,
                                            const uint32_t* __restrict__ perm, v3 o,
                                            v3 d, float a,
                                            float ya, float& best_t, int& best_i MF_ECNT) {
@@ -820,7 +839,7 @@ __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, ui
         MF_ECNT_INC;
         // the walk's order is spatial: an exact tie goes to the lower
         // ORIGINAL index (perm, read on ties only)
-        exact_body<FAST, true>(sph[RT_IDX(base + b, nsph, RT_SITE_MF_SPH)], (int)(base + b), o,
+        exact_body<FAST, true>(rec_load(sph, RT_IDX(base + b, nsph, RT_SITE_MF_SPH)), (int)(base + b), o,
                                d, a, ya, best_t, best_i, perm EXACT_PASS);
     }
 }
@@ -877,7 +896,10 @@ __device__ __forceinline__ void tile_or(const f16x& H, int* gq, int& g) {
 // rt_intersect_mfma_kernel; never the render): tile_cnt[0] += the (block,
 // half) tiles the wave walks, tile_cnt[1] += the 2 nblk it would walk without
 // block bounds (rt_debug_intersect_tiles).
-template <bool COUNT = false>
+// SPH_LDS (RT_MF_SPH_LDS builds): the drain's exact tests read the records
+// from the workgroup's LDS copy sph_lds (render_body copies mf.sph there when
+// it fits) instead of global memory.
+template <bool COUNT = false, bool SPH_LDS = false>
 __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
                                                     uint32_t scene_fast, v3 o, v3 d, bool live,
                                                     uint64_t live_mask, float& t_out,
@@ -885,11 +907,13 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
 #ifdef RT_PROFILE
                                                     , Prof& prof_
 #endif
-                                                    , unsigned long long* tile_cnt = nullptr) {
+                                                    , unsigned long long* tile_cnt = nullptr,
+                                                    lds_cfloat4* sph_lds = nullptr) {
     const uint4* __restrict__ mfA = mf.A;
     const uint32_t nblk = mf.nblk;
     const float mf_qs = mf.qs, mf_abs = mf.abs;
     const float4* __restrict__ sph = mf.sph;
+    (void)sph_lds;
     if (!live) {
         o = mk(0.0f, 0.0f, 0.0f);
         d = mk(0.0f, 0.0f, 1.0f);
@@ -898,14 +922,25 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
     // cover their latency (from block 0's A fragments when there are no
     // bounds, entries [0, 64) of its RT_MF_BLK: the load stays unconditional,
     // so hipcc's vmcnt waits count exactly, and in range)
+    // The lane offsets come from an opaque lane id at each use (opaque_lane):
+    // hoisted, hipcc kept them as three 64-bit per-lane offsets live across
+    // the whole kernel, and spilled them to scratch around the bound tiles.
+    // With chunk-level bounds (mf.top) the first bound chunk tested is the
+    // chunk-level one, after the ceil(nblk / 16) block-bound chunks.
     const bool has_b = mf.B != nullptr;
-    const uint4* pb0 = has_b ? mf.B : mfA;
+    const uint32_t nbchunk = (nblk + 15u) >> 4;  // block-bound chunks: 16 blocks, 2 bounds each
+    const uint4* pb0 = has_b ? mf.B + (mf.top ? (size_t)nbchunk * RT_MF_BCHUNK : 0) : mfA;
     const uint32_t pb0_n = has_b ? RT_MF_BCHUNK : RT_MF_BLK;  // uint4 entries of chunk / block 0
     (void)pb0_n;  // (read by the checked build's RT_IDX only)
-    uint4 bq0 = pb0[RT_IDX(__lane_id(), pb0_n, RT_SITE_MF_BOUND)];
-    uint4 bq1 = pb0[RT_IDX((has_b ? 64u : 0u) + __lane_id(), pb0_n, RT_SITE_MF_BOUND)];
-    uint2 bq2 = reinterpret_cast<const uint2*>(pb0)[RT_IDX((has_b ? 256u : 0u) + __lane_id(), 2u * pb0_n,
-                                                           RT_SITE_MF_BOUND)];
+    uint4 bq0, bq1;
+    uint2 bq2;
+    {
+        const uint32_t l = opaque_lane();
+        bq0 = pb0[RT_IDX(l, pb0_n, RT_SITE_MF_BOUND)];
+        bq1 = pb0[RT_IDX((has_b ? 64u : 0u) + l, pb0_n, RT_SITE_MF_BOUND)];
+        bq2 = reinterpret_cast<const uint2*>(pb0)[RT_IDX((has_b ? 256u : 0u) + l, 2u * pb0_n,
+                                                         RT_SITE_MF_BOUND)];
+    }
     const float dd = dot(d, d);
     const float l = sqrt_x(dd);
     const float a = l * l;  // sqr(length(r.dir)), intersect.wgsl:98
@@ -1019,8 +1054,16 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
     // bounds" and "Forward bounds" in the header above). A wave with a live
     // ray outside |d|^2 in [2^-100, 2^100] (the proof's domain) walks every
     // block.
+    //
+    // Chunk bounds (mf.top: 2..32 bound chunks, e.g. 10,000 spheres in 20):
+    // row j of the chunk-level chunk is the bound of bound chunk j's 512 walk
+    // positions, built like a block bound (C, L over its members, R^2 =
+    // (1 + 2^-4) L^2, muB, forward row), so the "Block bounds" / "Forward
+    // bounds" proofs hold for it unchanged: a ray with an exact hit in chunk
+    // j passes row j. Its tile (the same three MFMAs per half) runs first; a
+    // half that no ray of passes chunk j gets no block of chunk j, and a chunk
+    // neither half passes is not tested at all.
     const uint32_t nchunk = (nblk + 31u) >> 5;   // of the walk: 32 blocks
-    const uint32_t nbchunk = (nblk + 15u) >> 4;  // of the bounds: 16 blocks, 2 bounds each
     uint32_t mv0 = 0xFFFFFFFFu, mv1 = 0xFFFFFFFFu;  // lane k: walk chunk k's masks, halves 0 / 1
     if (has_b && rt_ballot(live && !(dd >= 0x1p-100f && dd <= 0x1p100f)) == 0) {
         mv0 = mv1 = 0u;
@@ -1040,22 +1083,14 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
             __builtin_memcpy(&G0, &g0, 8);
             __builtin_memcpy(&G1, &g1, 8);
         }
-        for (uint32_t k = 0; k < nbchunk; ++k) {
-            // chunk 0's fragments were loaded first; a later chunk's load here
-            // (no prefetch: its registers would spill, and up to 512 spheres
-            // have one chunk)
-            if (k != 0u) {
-                const uint4* pb = mf.B + (size_t)RT_IDX(k, nbchunk, RT_SITE_MF_BOUND) * RT_MF_BCHUNK;
-                bq0 = pb[lane];
-                bq1 = pb[64u + lane];
-                bq2 = reinterpret_cast<const uint2*>(pb)[256u + lane];
-            }
+        // one bound chunk's tiles: per half the 32-bit mask of its rows some
+        // ray of the half passes
+        auto bound_tiles = [&](uint32_t* mk2) {
             h8v F0, F1;
             h4v F2;
             __builtin_memcpy(&F0, &bq0, 16);
             __builtin_memcpy(&F1, &bq1, 16);
             __builtin_memcpy(&F2, &bq2, 8);
-            uint32_t mk2[2];
 #pragma unroll
             for (uint32_t t = 0; t < 2; ++t) {
                 const f16x V = __builtin_amdgcn_mfma_f32_32x32x16_f16(
@@ -1065,6 +1100,36 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
                 const uint32_t acc = tile_or_fwd(V, U);
                 const uint64_t bm = rt_ballot((int)acc < 0);
                 mk2[t] = (uint32_t)bm | (uint32_t)(bm >> 32);
+            }
+        };
+        const bool top = mf.top != 0u;
+        uint32_t top2[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};  // chunks some ray of each half passes near
+        if (top) {
+            bound_tiles(top2);  // the preloaded chunk-level fragments
+            PROF_ADD(27, 1);    // chunk-level bound tiles (2 halves x 3 MFMAs)
+        }
+        for (uint32_t k = 0; k < nbchunk; ++k) {
+            // (with chunk bounds, at most 32 chunks: k < 32)
+            if (top && (((top2[0] | top2[1]) >> (k & 31u)) & 1u) == 0u) continue;
+            // chunk 0's fragments were loaded first (without chunk bounds); a
+            // later chunk's load here (no prefetch: its registers would spill,
+            // and up to 512 spheres have one chunk)
+            if (k != 0u || top) {
+                // the chunk's base an opaque SGPR pair: the loads take the
+                // scalar-base form with a 32-bit lane offset, not three
+                // per-lane 64-bit pointers stepped through the loop
+                const uint4* pb = mf.B + (size_t)RT_IDX(k, nbchunk, RT_SITE_MF_BOUND) * RT_MF_BCHUNK;
+                asm volatile("" : "+s"(pb));
+                const uint32_t l = opaque_lane();
+                bq0 = pb[l];
+                bq1 = pb[64u + l];
+                bq2 = reinterpret_cast<const uint2*>(pb)[256u + l];
+            }
+            uint32_t mk2[2];
+            bound_tiles(mk2);
+            if (top) {  // a half that passes no ray near the chunk gets none of its blocks
+                mk2[0] = ((top2[0] >> k) & 1u) ? mk2[0] : 0u;
+                mk2[1] = ((top2[1] >> k) & 1u) ? mk2[1] : 0u;
             }
             // bound rows 2i, 2i + 1 are block 16 k + i's halves: its bit is
             // their OR, the 16 block bits compressed from the even positions
@@ -1082,8 +1147,8 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
                 mv0 |= f0;
                 mv1 |= f1;
             }
+            PROF_ADD(17, 1);  // bound chunks: 2 halves x (2 MFMA 32x32x16 + 1 MFMA 32x32x8)
         }
-        PROF_ADD(17, nbchunk);  // bound chunks: 2 halves x (2 MFMA 32x32x16 + 1 MFMA 32x32x8)
     }
     PROF_MARK(16);  // ray column + bound tiles
 
@@ -1108,22 +1173,37 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
     // wave-uniform upper bounds of every lane's queue length per half (SGPRs):
     // one per group some lane queued from since the last drain
     uint32_t ub0 = 0, ub1 = 0;
+    // the exact tests of the queued candidates (the records from global
+    // memory, or from the workgroup's LDS copy: SPH_LDS)
+    auto drain = [&](uint32_t cnt0, uint32_t cnt1) {
+        if constexpr (SPH_LDS) {
+            if (__builtin_expect(fast, 1))
+                mfma_drain<true>(cq, cnt0, cnt1, sph_lds, nblk * 32u, mf.perm, o, d, a, ya, best_t,
+                                 best_i MF_ECNT_PASS);
+            else
+                mfma_drain<false>(cq, cnt0, cnt1, sph_lds, nblk * 32u, mf.perm, o, d, a, ya, best_t,
+                                  best_i MF_ECNT_PASS);
+        } else {
+            if (__builtin_expect(fast, 1))  // (the IEEE drain is placed out of the way)
+                mfma_drain<true>(cq, cnt0, cnt1, sph, nblk * 32u, mf.perm, o, d, a, ya, best_t,
+                                 best_i MF_ECNT_PASS);
+            else
+                mfma_drain<false>(cq, cnt0, cnt1, sph, nblk * 32u, mf.perm, o, d, a, ya, best_t,
+                                  best_i MF_ECNT_PASS);
+        }
+    };
     // one 32-sphere block: both ray halves against A fragments x0 (K 0..15),
     // x1 (K 16..31)
     auto block = [&](uint32_t b, const uint4 x0, const uint4 x1, uint32_t m0, uint32_t m1) {
         // a block adds at most 4 entries to each half's queue: make room first,
         // while no tile result is live (the lanes' own counts are compared
         // only when the scalar bound says the queue may be full)
-        if (max(ub0, ub1) + 4u > RT_MF_CAP &&
-            rt_ballot(max(qcount(qp0, q0), qcount(qp1, q1)) + 4u > RT_MF_CAP) != 0) {
+        if (__builtin_expect(max(ub0, ub1) + 4u > RT_MF_CAP &&
+                             rt_ballot(max(qcount(qp0, q0), qcount(qp1, q1)) + 4u > RT_MF_CAP) != 0,
+                             0)) {  // (rare: kept out of the walk's hot blocks)
             const uint32_t cnt0 = qcount(qp0, q0), cnt1 = qcount(qp1, q1);
             PROF_ADD(11, 1);  // queue flushes
-            if (fast)
-                mfma_drain<true>(cq, cnt0, cnt1, sph, nblk * 32u, mf.perm, o, d, a, ya, best_t,
-                                 best_i MF_ECNT_PASS);
-            else
-                mfma_drain<false>(cq, cnt0, cnt1, sph, nblk * 32u, mf.perm, o, d, a, ya, best_t,
-                                  best_i MF_ECNT_PASS);
+            drain(cnt0, cnt1);
             qp0 = q0;
             qp1 = q1;
             ub0 = ub1 = 0;
@@ -1253,16 +1333,12 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
         atomicAdd(tile_cnt + 1, 2ull * nblk);
     }
     PROF_MARK(1);
-    const uint32_t cnt0 = qcount(qp0, q0), cnt1 = qcount(qp1, q1);
-    if (fast)
-        mfma_drain<true>(cq, cnt0, cnt1, sph, nblk * 32u, mf.perm, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
-    else
-        mfma_drain<false>(cq, cnt0, cnt1, sph, nblk * 32u, mf.perm, o, d, a, ya, best_t, best_i MF_ECNT_PASS);
+    drain(qcount(qp0, q0), qcount(qp1, q1));
     // the walk position of the winner -> its original index
     if (best_i >= 0) best_i = (int)mf.perm[RT_IDX((uint32_t)best_i, nblk * 32u, RT_SITE_PERM)];
     PROF_MARK(2);
 #ifdef RT_PROFILE
-    {
+    {   // (diagnostic reductions: their time goes to c[26])
         PROF_ADD(13, wave_max_u32(ecnt_[0]));
         uint32_t sum1 = ecnt_[1];
         for (int off = 32; off > 0; off >>= 1) sum1 += __shfl_xor(sum1, off);
@@ -1270,6 +1346,7 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
         uint32_t sum0 = ecnt_[0];
         for (int off = 32; off > 0; off >>= 1) sum0 += __shfl_xor(sum0, off);
         PROF_ADD(15, sum0);
+        PROF_MARK(26);
     }
 #endif
     t_out = best_t;

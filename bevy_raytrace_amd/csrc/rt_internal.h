@@ -33,6 +33,9 @@
 #define RT_MF_BLK 96u
 #define RT_MF_BCHUNK 160u  // uint4 entries per bound chunk: line rows K 0..31, forward rows K 0..7
 #define RT_GROUP 8            // spheres per filter group (SoA, 128 B)
+#ifndef RT_MF_SPH_LDS_MAX
+#define RT_MF_SPH_LDS_MAX 512 // RT_MF_SPH_LDS builds: walk records held in LDS (8 KB)
+#endif
 #ifndef RT_SLOT_BUF_CAP
 #define RT_SLOT_BUF_CAP 32    // slot-store buffer entries per wave (rt_kernels.hip)
 #endif
@@ -70,6 +73,8 @@ struct MfScene {
     const float4* sph;      // (cx, cy, cz, r^2) in the walk's order, nblk * 32 records
     const uint32_t* perm;   // walk position -> original sphere index
     uint32_t nblk;          // 32-sphere blocks (<= 2048)
+    uint32_t top;           // 1: B holds one more chunk after the ceil(nblk / 16) of block
+                            // bounds, the chunk-level bounds (row j = chunk j; 2..32 chunks)
     float qs, abs;          // 2^sq (quadratic features' ray-side scale), threshold margin
 };
 
@@ -139,7 +144,10 @@ struct KParams {
     // queue order (knob item_order, bits; default 3): bit 0 the block items
     // and the tail items, bit 1 the pixel items, pixel-major
     // (consecutive items: one pixel's pairs / samples / frames) instead of
-    // pair- / sample- / frame-major (consecutive items: neighbouring pixels)
+    // pair- / sample- / frame-major (consecutive items: neighbouring pixels);
+    // bit 2 (npix % 8 == 0 only) every region grouped: 8 neighbouring
+    // pixels' items back to back, frame / pair / sample-group major within
+    // the group (rt_dev_path.h grouped_split)
     uint32_t item_order;
     FastDiv div_nfpix; // by main_pix / npix (frames with pixel items)
     FastDiv div_nreg;  // by qmain - qpix (pairs of the block-item region)
@@ -170,6 +178,7 @@ struct KParams {
                           // the collect's system-scope write-through stores + a
                           // release per wave; no direct output then
     uint32_t collect_f0;  // first launch frame rt_collect_kernel folds
+    uint32_t dsys_release;  // dsys: each collect wave also issues a system-scope release (knob)
 };
 
 // Row block b of the image -> owning shard (rt_params: serpentine deal).

@@ -21,15 +21,21 @@
 // the output pixel itself (direct output); rt_collect_kernel folds the other
 // frames' slots in block / sample order -- the oracle's summation order.
 //
-// Intersection (the hot loop, intersect.wgsl:133-143): every sphere of the
-// list is tested for every live ray (brute force), in two stages. A
-// conservative filter proves most (sphere, ray) pairs miss: by default on the
-// matrix cores, one 32-term f16 hi/lo dot product per pair -- two chained
-// v_mfma_f32_32x32x16_f16 per 32-sphere x 32-ray tile give V = T0 - H0 and a
-// pair is a candidate iff V < 0 (rt_dev_intersect.h intersect_world_mfma,
-// DESIGN.md 4.2); the culled list, and waves with a ray outside the f16
-// split's range, run the same test as packed fp32 FMAs over groups of 8
-// spheres read with scalar loads (filter8):
+// Intersection (the hot loop, intersect.wgsl:133-143): the closest hit over
+// the whole list, with the brute-force loop's result, in stages that skip
+// most of its work. By default, the matrix-core walk: each 16-sphere half of
+// a 32-sphere block (the list in k-d spatial order) has a bounding sphere,
+// tested against the wave's rays on the matrix cores first, and a 32-ray
+// half-wave walks only the blocks whose bounds one of its rays passes near
+// (proof in rt_dev_intersect.h "Block bounds"); in a walked block a
+// conservative filter proves most (sphere, ray) pairs miss -- one 32-term
+// f16 hi/lo dot product per pair, two chained v_mfma_f32_32x32x16_f16 per
+// 32-sphere x 32-ray tile giving V = T0 - H0, a pair a candidate iff V < 0
+// (intersect_world_mfma). The packed VALU filter -- every
+// sphere, no bounds -- serves RT_FLAG_VALU_FILTER, waves with a ray outside
+// the f16 split's range and scenes outside it; the culled list (RT_FLAG_CULL)
+// runs it behind group bounds. It evaluates the same test as packed fp32
+// FMAs over groups of 8 spheres read with scalar loads (filter8):
 //   H - T = hb^2 + r^2 - (1 - m)|o - c|^2 + mu (|o|^2 + |c|^2),  hb = dn.(o - c)
 // H < T proves the reference's discriminant (intersect.wgsl:102) is negative.
 // Lanes queue their candidates in LDS; after the walk each lane runs the
@@ -180,7 +186,10 @@ __device__ __forceinline__ void store_system(float4* p, float4 v) {
 // The persistent render loop; CULL = false is rt_render_kernel (the brute-force
 // walk of the headline), CULL = true rt_render_cull_kernel (the permuted list
 // with group bounds, P.bnd / P.perm / P.nclusters; identical results).
-template <bool CULL>
+// SPH_LDS (RT_MF_SPH_LDS builds, rt_render_lds_kernel): the matrix-core
+// walk's records (mf.sph, <= RT_MF_SPH_LDS_MAX) copied into the workgroup's
+// LDS at the start, so the drain's dependent record load is an LDS read.
+template <bool CULL, bool SPH_LDS = false>
 __device__ __forceinline__ void render_body(
     const KParams& P, const float4* grp, const float4* __restrict__ sph,
     const float4* __restrict__ shd,
@@ -188,6 +197,14 @@ __device__ __forceinline__ void render_body(
     uint32_t* __restrict__ work_counter,
     unsigned long long* __restrict__ seg_counter, unsigned long long* __restrict__ dbg) {
     const uint32_t lane = __lane_id();
+#ifdef RT_MF_SPH_LDS
+    __shared__ float4 s_msph[SPH_LDS ? RT_MF_SPH_LDS_MAX : 1];
+    if constexpr (SPH_LDS) {
+        const uint32_t nrec = P.mf.nblk * 32u;  // <= RT_MF_SPH_LDS_MAX (rt_launch_render)
+        for (uint32_t i = threadIdx.x; i < nrec; i += RT_BLOCK_THREADS) s_msph[i] = P.mf.sph[i];
+        __syncthreads();
+    }
+#endif
     PROF_DECL
     PROF_START();
 #ifdef RT_PROFILE
@@ -388,7 +405,8 @@ __device__ __forceinline__ void render_body(
         PROF_MARK(0);
         PROF_ADD(4, 1);
 #ifdef RT_PROFILE
-        {   // diagnostic: distinct pixels per half-wave (c[6]) and lanes at bounce 0 (c[14])
+        {   // diagnostic: distinct pixels per half-wave (c[6]) and lanes at bounce 0 (c[14]);
+            // its own time goes to c[26] (excluded from the phase shares)
             uint64_t rest = rt_ballot(has_item);
             uint32_t distinct = 0;
             while (rest) {
@@ -401,6 +419,7 @@ __device__ __forceinline__ void render_body(
             }
             PROF_ADD(6, distinct);
             PROF_ADD(14, (unsigned long long)__popcll(rt_ballot(has_item && st.bounce == 0)));
+            PROF_MARK(26);
         }
 #endif
         PROF_ADD(9, (unsigned long long)__popcll(rt_ballot(has_item)));
@@ -428,18 +447,30 @@ __device__ __forceinline__ void render_body(
         int hi = -1;
         float t = VERY_FAR;
         const uint64_t live = rt_ballot(has_item);
-        if ((uint32_t)__popcll(live) <= P.wide_max) {  // nearly empty wave: sphere-parallel
+        // (branch weights: the matrix-core walk is the hot path; the
+        // sphere-parallel and VALU walks are placed out of its way, so the
+        // loop's hot blocks stay together in the instruction cache)
+        if (__builtin_expect((uint32_t)__popcll(live) <= P.wide_max, 0)) {  // nearly empty wave: sphere-parallel
             PROF_ADD(20, 1);
             intersect_wide<CULL>(sph, P.nspheres, P.scene_fast, live, st.o, st.d, hi, t, P.perm);
 #ifdef RT_MFMA_FILTER
-        } else if (!CULL && P.mf.A && mfma_wave_ok(st.o, has_item)) {  // the whole wave
+        } else if (__builtin_expect(!CULL && P.mf.A && mfma_wave_ok(st.o, has_item), 1)) {  // the whole wave
             PROF_ADD(18, 1);
+#ifdef RT_MF_SPH_LDS
+            const int h2 = intersect_world_mfma<false, SPH_LDS>(P.mf, P.scene_fast, st.o, st.d,
+                                                                has_item, live, t, cqm
+#ifdef RT_PROFILE
+                                                                , prof_
+#endif
+                                                                , nullptr, (lds_cfloat4*)s_msph);
+#else
             const int h2 = intersect_world_mfma(P.mf, P.scene_fast, st.o, st.d,
                                                 has_item, live, t, cqm
 #ifdef RT_PROFILE
                                                 , prof_
 #endif
                                                 );
+#endif
             if (has_item) hi = h2;
             else t = VERY_FAR;
 #endif
@@ -619,6 +650,17 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
     render_body<false>(P, grp, sph, shd, tab, block_sums, work_counter, seg_counter, dbg);
 }
 
+#ifdef RT_MF_SPH_LDS
+__global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_render_lds_kernel(
+    KParams P, const float4* grp, const float4* __restrict__ sph,
+    const float4* __restrict__ shd,
+    const PixelEntry* __restrict__ tab, float4* __restrict__ block_sums,
+    uint32_t* __restrict__ work_counter,
+    unsigned long long* __restrict__ seg_counter, unsigned long long* __restrict__ dbg) {
+    render_body<false, true>(P, grp, sph, shd, tab, block_sums, work_counter, seg_counter, dbg);
+}
+#endif
+
 __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD_CULL) void rt_render_cull_kernel(
     KParams P, const float4* grp, const float4* __restrict__ sph,
     const float4* __restrict__ shd,
@@ -797,7 +839,7 @@ __global__ void rt_collect_kernel(KParams P, const float4* __restrict__ block_su
     // of the wave) ends the wave's part of the hand-off; the reader acquires
     // (rt_acquire) after the host has seen the launch complete.
     if (P.dsys) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        if (P.dsys_release) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the asm store is invisible to hipcc)
     }
 }
@@ -861,6 +903,12 @@ hipError_t rt_launch_render(const KParams* P, const float4* grp, const float4* s
         hipLaunchKernelGGL(rt_render_cull_kernel, dim3(grid), dim3(RT_BLOCK_THREADS), dyn, stream,
                            *P, grp, sph, shd, reinterpret_cast<const PixelEntry*>(pd),
                            block_sums, work_counter, seg_counter, seg_counter + 2);
+#ifdef RT_MF_SPH_LDS
+    else if (P->mf.A && P->mf.nblk * 32u <= RT_MF_SPH_LDS_MAX)
+        hipLaunchKernelGGL(rt_render_lds_kernel, dim3(grid), dim3(RT_BLOCK_THREADS), dyn, stream, *P,
+                           grp, sph, shd, reinterpret_cast<const PixelEntry*>(pd),
+                           block_sums, work_counter, seg_counter, seg_counter + 2);
+#endif
     else
         hipLaunchKernelGGL(rt_render_kernel, dim3(grid), dim3(RT_BLOCK_THREADS), dyn, stream, *P,
                            grp, sph, shd, reinterpret_cast<const PixelEntry*>(pd),

@@ -6,8 +6,9 @@
 //! Per frame, in `update` (it has `&mut World`, runs after every RenderStage
 //! ::Prepare system, so sphere.rs / ray_trace_materials.rs / ray_trace_globals.rs
 //! have packed this frame's bytes):
-//!   1. with RT_MAX_PENDING (2) renders in flight, rt_wait for the older one
-//!      (enqueued two frames ago) -- its texels become the frame `run` shows;
+//!   1. with `frames_in_flight` renders pending (1 by default, at most
+//!      RT_MAX_PENDING = 2), rt_wait for the oldest -- its texels become the
+//!      frame `run` shows;
 //!   2. dirty-tracked scene upload: rt_update_* for a same-size edit,
 //!      rt_set_scene when the counts change, nothing when the bytes are equal
 //!      (the reference re-uploads everything every frame, sphere.rs:180-197);
@@ -16,14 +17,17 @@
 //!      render in flight, so a resize first completes the pending ones);
 //!   4. rt_render_async of this frame into a host buffer that is neither shown
 //!      nor in flight (three buffers).
-//! Two renders in flight: each pending frame has its own stream in the
-//! library, so frame n's device->host copy overlaps frame n+1's render (the
-//! copy is 45 % of a 1080p frame at 1 spp, profiles/r03_bench_reference1080.json;
-//! bench.py shim_sequence measures both depths). `run` only copies the
-//! finished frame into the texture. The displayed frame is two frames behind
-//! the camera, and the CPU never blocks on a render it just enqueued. A
-//! failing call is logged and skipped (the previous image stays); nothing
-//! panics across the render thread.
+//! Frames in flight (`RayTraceNode::with_frames_in_flight`): with 1 (the
+//! default, `new`) the frame enqueued in one update is shown by the next --
+//! one frame of latency, as the round-3 shim; with 2 each pending frame has
+//! its own stream in the library, so frame n's device->host copy overlaps
+//! frame n+1's render (the copy is 45 % of a 1080p frame at 1 spp,
+//! profiles/r03_bench_reference1080.json; bench.py shim_sequence measures
+//! both depths: 697 vs 1,365 frames/s) at the price of one more frame of
+//! input latency (the shown frame is two behind the camera). `run` only
+//! copies the finished frame into the texture. A failing call is logged and
+//! skipped (the previous image stays); nothing panics across the render
+//! thread.
 use std::num::NonZeroU32;
 
 use bevy::{
@@ -68,7 +72,8 @@ struct HostFrame {
     registered: Option<(usize, usize)>,
 }
 
-/// Host frame buffers: the shown one and RT_MAX_PENDING in flight.
+/// Host frame buffers: the shown one and up to RT_MAX_PENDING in flight
+/// (with fewer frames in flight the last ones are never allocated).
 const NBUF: usize = RT_MAX_PENDING as usize + 1;
 
 pub struct RayTraceNode {
@@ -80,10 +85,21 @@ pub struct RayTraceNode {
     pending: std::collections::VecDeque<usize>,
     /// index of the last finished frame (what `run` shows)
     ready: Option<usize>,
+    /// renders kept in flight across updates, 1..=RT_MAX_PENDING
+    frames_in_flight: usize,
 }
 
 impl RayTraceNode {
+    /// One render in flight: the frame enqueued in an update is shown by the
+    /// next one (one frame of latency).
     pub fn new(ctx: RtContext) -> Self {
+        Self::with_frames_in_flight(ctx, 1)
+    }
+
+    /// `depth` renders in flight (clamped to 1..=RT_MAX_PENDING): 2 overlaps a
+    /// frame's device->host copy with the next render (about twice the frame
+    /// rate at 1 spp) and shows frames two behind the camera.
+    pub fn with_frames_in_flight(ctx: RtContext, depth: u32) -> Self {
         RayTraceNode {
             ctx,
             uploaded: Uploaded::default(),
@@ -91,6 +107,7 @@ impl RayTraceNode {
             frames: Default::default(),
             pending: std::collections::VecDeque::new(),
             ready: None,
+            frames_in_flight: depth.clamp(1, RT_MAX_PENDING) as usize,
         }
     }
 
@@ -123,10 +140,10 @@ impl RayTraceNode {
         }
     }
 
-    /// Step 1: keep at most RT_MAX_PENDING - 1 renders in flight before
+    /// Step 1: keep at most frames_in_flight - 1 renders in flight before
     /// enqueueing this frame's.
     fn finish_pending(&mut self) {
-        while self.pending.len() >= RT_MAX_PENDING as usize {
+        while self.pending.len() >= self.frames_in_flight {
             self.finish_oldest();
         }
     }

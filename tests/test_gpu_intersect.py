@@ -254,6 +254,13 @@ def test_block_bounds_at_their_decision_boundary(renderer, name):
     nblk = (int(np.nonzero(perm >= 0)[0].max()) + 1 + 31) // 32
     assert total == 2 * nblk * (-(-len(rays) // 64)), (total, nblk)
     assert walked <= 0.7 * total, (walked, total)
+    # the chunk-level bounds (lists of 2..32 bound chunks) only remove tiles
+    renderer.tune(mf_top=0)
+    ni, nt = renderer.intersect(rays)
+    w_nt, t_nt = renderer.intersect_tiles()
+    exact(ni, nt, "block bounds without chunk bounds (mf_top=0)")
+    assert t_nt == total and w_nt >= walked
+    renderer.tune(None)
     renderer.tune(mf_cull=0)
     ai, at = renderer.intersect(rays)
     w_all, t_all = renderer.intersect_tiles()

@@ -247,10 +247,12 @@ def test_tail_split_identical(renderer, S):
                                            (64, "96", "0.01,0.01,0.01"), (64, "0", "0,1,1")])
 def test_item_order_identical(renderer, S, region, tail):
     """Pixel-major items (knob item_order bits: one pixel's pairs / tail
-    sample groups, and its frames, back to back in the queue) give the frames
-    of the pair- / sample- / frame-major order -- only the work order changes,
-    each item keeps its slot. Three frames in one launch, so the regions span
-    frames; the 0.01 tail holds 4-, 2- and 1-sample items."""
+    sample groups, and its frames, back to back in the queue), and grouped
+    items (bit 2: 8 pixels' items back to back, frame / pair / sample-group
+    major) give the frames of the pair- / sample- / frame-major order -- only
+    the work order changes, each item keeps its slot. Three frames in one
+    launch, so the regions span frames; the 0.01 tail holds 4-, 2- and
+    1-sample items; 72 x 40 = 360 groups of 8 pixels."""
     import torch
     sp, mt = arrays(scene.rtiow_final_scene())
     cam = default_camera_block()
@@ -258,7 +260,7 @@ def test_item_order_identical(renderer, S, region, tail):
     renderer.set_scene(sp, mt)
     renderer.tune(block_region=region, tail=tail)
     outs = []
-    for order in ("0", "1", "2", "3"):
+    for order in ("0", "1", "2", "3", "4", "7"):
         renderer.tune(item_order=order)
         buf = torch.empty((F, H, W, 4), dtype=torch.float32, device="cuda")
         renderer.render_frames_device(cam, F, buf.data_ptr(), W, H, S, 10, flags=NO_REUSE)

@@ -197,6 +197,10 @@ def test_flag_constants_agree_across_bindings():
     for name, v in flags.items():
         assert getattr(abi, name) == v, name
         assert rflags.get(name) == v, name
+    # the in-flight depth the shim sizes its host buffers by
+    pend = int(re.search(r"#define RT_MAX_PENDING\s+(\d+)", hdr).group(1))
+    rpend = int(re.search(r"pub const RT_MAX_PENDING: u32 = (\d+);", rs).group(1))
+    assert pend == rpend == abi.RT_MAX_PENDING
 
 
 def test_bench_roofline_recomputes_from_committed_counters():

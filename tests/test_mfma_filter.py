@@ -335,19 +335,25 @@ def forward_columns(rays):
     return np.stack(cols, 1)
 
 
-@pytest.mark.parametrize("name", sorted(SCENES))
-def test_block_bounds_are_conservative(name):
+BOUND_CASES = [(n, 16) for n in sorted(SCENES)] + [("spheres10k", 512)]
+
+
+@pytest.mark.parametrize("name,size", BOUND_CASES,
+                         ids=[f"{n}-{s}" for n, s in BOUND_CASES])
+def test_block_bounds_are_conservative(name, size):
     """The walk skips a 32-sphere block for a half-wave when no ray of the
     half has V_B < 0 on either of the block's two half-block bound rows (rt_dev_intersect.h "Block
     bounds"): every exact hit of a member sphere must have V_B < 0, in every
     summation order, on the adversarial ray sets (rays in the walk's domain:
-    mfma_wave_ok and |d|^2 in [2^-100, 2^100])."""
+    mfma_wave_ok and |d|^2 in [2^-100, 2^100]). size 512: the chunk-level
+    bounds of a list of 2..32 bound chunks ("Chunk bounds": 10,000 spheres,
+    20 chunks of 512 walk positions), built the same way."""
     from bevy_raytrace_amd import abi
     full = SCENES[name]()
     sq = qscale(full)
     perm = abi.cull_layout(full)[0]
-    nblk = (len(perm) - 8) // 16  # half-block bounds over whole clusters (+ one pad group)
-    C, S = block_bounds(full, perm, nblk)
+    nblk = -(-(len(perm) - 8) // size)  # bounds over whole clusters (+ one pad group)
+    C, S = block_bounds(full, perm, nblk, size=size)
     A = rows_of(C, S, sq, bound=True)
     sp = full[:SUBSET.get(name, len(full))]
     rays = _rays(sp, "blk" + name, 6_000 if len(sp) < 1000 else 2_000)
@@ -358,7 +364,7 @@ def test_block_bounds_are_conservative(name):
     hits = exact_hits(sp, rays)  # (rays, spheres of the subset)
     pos = np.full(len(full), -1)
     pos[perm[perm >= 0]] = np.nonzero(perm >= 0)[0]
-    blk = pos[:len(sp)] // 16  # the half-block bound of each checked sphere
+    blk = pos[:len(sp)] // size  # the bound of each checked sphere
     assert hits.sum() > 500
     for order in ORDERS:
         with np.errstate(invalid="ignore", over="ignore"):
@@ -368,18 +374,20 @@ def test_block_bounds_are_conservative(name):
                                 f"{np.argwhere(lost)[0].tolist()}")
 
 
-@pytest.mark.parametrize("name", sorted(SCENES))
-def test_forward_bounds_are_conservative(name):
+@pytest.mark.parametrize("name,size", BOUND_CASES,
+                         ids=[f"{n}-{s}" for n, s in BOUND_CASES])
+def test_forward_bounds_are_conservative(name, size):
     """The bound tile passes a (ray, half-block bound) pair only when its line
     row passes (V_B < 0) AND its forward row does (U >= +0: the bound is not
     wholly behind the ray's origin, rt_dev_intersect.h "Forward bounds"): every
-    exact hit of a member sphere must pass both, in every summation order."""
+    exact hit of a member sphere must pass both, in every summation order
+    (size 512: the chunk-level bounds)."""
     from bevy_raytrace_amd import abi
     full = SCENES[name]()
     sq = qscale(full)
     perm = abi.cull_layout(full)[0]
-    nblk = (len(perm) - 8) // 16
-    C, S, Lf = block_bounds(full, perm, nblk, return_forward=True)
+    nblk = -(-(len(perm) - 8) // size)
+    C, S, Lf = block_bounds(full, perm, nblk, size=size, return_forward=True)
     A = rows_of(C, S, sq, bound=True)
     Af = forward_rows(C, Lf)
     sp = full[:SUBSET.get(name, len(full))]
@@ -392,7 +400,7 @@ def test_forward_bounds_are_conservative(name):
     hits = exact_hits(sp, rays)
     pos = np.full(len(full), -1)
     pos[perm[perm >= 0]] = np.nonzero(perm >= 0)[0]
-    blk = pos[:len(sp)] // 16
+    blk = pos[:len(sp)] // size
     assert hits.sum() > 500
     cut = 0
     for order in ORDERS:

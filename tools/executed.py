@@ -31,6 +31,7 @@ NAMES = {
     13: "exact_rounds", 14: "bounce0_lanes", 15: "exact_tests", 17: "bound_chunks",
     18: "iters_mfma_walk", 19: "iters_valu_walk", 20: "iters_wide", 21: "exact_tests_full",
     22: "shade_rounds", 23: "group_appends", 24: "valu_walk_queue_max", 25: "valu_walk_full_max",
+    26: "t_diag", 27: "top_bound_tiles",
 }
 
 

@@ -18,6 +18,8 @@ timeout -k 10 300 python -u tools/executed.py $O/executed_raw.json > $O/executed
 step executed $?
 timeout -k 10 120 python -u tools/ray_dump.py $O/ray_dump.npy > $O/ray_dump.log 2>&1
 step ray_dump $?
+timeout -k 10 200 python -u tools/split_probe.py > $O/split.log 2>&1
+step split_probe $?
 CFG=spheres10k1080 FPL=2 OUT=$O/pmc_10k bash tools/pmc_round.sh > $O/pmc_10k.log 2>&1
 step pmc_10k $?
 CFG=rtiow4k FPL=1 OUT=$O/pmc_4k bash tools/pmc_round.sh > $O/pmc_4k.log 2>&1
