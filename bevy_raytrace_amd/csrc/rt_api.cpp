@@ -77,6 +77,7 @@ struct Tuning {
     // (profiles/r03/item_order/): full frame 243.7 -> 240.2 ms, N=8 shard
     // 34.9 -> 33.5 ms; 1 alone 242.6 / 33.5, 2 alone 241.0 / 35.4
     uint32_t item_order = 3;
+    uint32_t pix_group = 8;       // item_order bit 2: pixels per group (4 or 8)
     bool prefetch = true;         // waves prefetch their next work chunk
     uint32_t prio_mode = 1;       // s_setprio rotation: 0 off, 1 by iteration, 3 by wall time
     uint32_t prio_shift = 14;     // mode 3 step: 2^prio_shift ticks of 10 ns
@@ -97,10 +98,15 @@ struct Tuning {
     // lists of 2..32 bound chunks test the chunk-level bounds first
     // (MfScene::top); off: every chunk's block bounds (same bits)
     bool mf_top = true;
-    // RT_FLAG_IMAGE_OUT: a system-scope release per collect wave after its
-    // write-through stores (off: the stores drained by s_waitcnt vmcnt(0)
-    // only -- A/B)
-    bool dsys_release = true;
+    // RT_FLAG_IMAGE_OUT: a system-scope release (buffer_wbl2 sc0 sc1) per
+    // collect wave after its write-through stores. Off (the product): every
+    // byte of the hand-off is stored sc0 sc1 (write-through, nothing dirty
+    // left in this device's L2) and drained by s_waitcnt vmcnt(0), the
+    // producer form MI355X_MICROARCH.md lists beside the release when the
+    // consumer acquires (rt_acquire). The per-wave write-back of the L2 cost
+    // an N = 8 shard's 20-frame call 2.3 ms (2.51 -> 0.18 ms beyond the
+    // render, profiles/r05/split/); on: A/B only.
+    bool dsys_release = false;
 };
 
 struct rt_ctx {
@@ -260,6 +266,9 @@ static bool tune_set(Tuning& t, const char* name, const char* v) {
     } else if (!strcmp(name, "item_order")) {
         if (x < 0 || x > 7) return false;
         t.item_order = (uint32_t)x;
+    } else if (!strcmp(name, "pix_group")) {
+        if (x != 4 && x != 8) return false;
+        t.pix_group = (uint32_t)x;
     } else if (!strcmp(name, "block_region")) {
         if (x < 0) return false;
         t.block_region = x;
@@ -1465,7 +1474,9 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         K_.ti2 = K_.ti1 + (uint32_t)((g2 - g1 + 1) / 2 * npix);
         K_.tail_items = K_.ti2 + (uint32_t)((g_end - g2) * npix);
         // grouped order (bit 2) needs whole groups of 8 pixels; else pixel-major
-        K_.item_order = (tn.item_order & 4u) && npix % 8u != 0 ? (tn.item_order & 3u) | 3u : tn.item_order;
+        K_.pix_group_shift = tn.pix_group == 4 ? 2u : 3u;
+        K_.item_order = (tn.item_order & 4u) && npix % tn.pix_group != 0 ? (tn.item_order & 3u) | 3u
+                                                                        : tn.item_order;
         K_.div_nreg = make_fastdiv(K_.qmain > K_.qpix ? K_.qmain - K_.qpix : 1u);
         K_.div_nfpix = make_fastdiv(npix && K_.main_pix ? K_.main_pix / npix : 1u);
         K_.div_ng4 = make_fastdiv(g1 > g0 ? (uint32_t)((g1 - g0 + 3) / 4) : 1u);

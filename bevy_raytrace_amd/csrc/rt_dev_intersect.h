@@ -729,6 +729,11 @@ typedef float f16x __attribute__((ext_vector_type(16)));
 #ifndef RT_MF_CAP
 #define RT_MF_CAP 12  // queue entries per lane and half (LDS)
 #endif
+#ifndef RT_MF_CAP_LDS
+// ... in the kernel that also holds the walk's records in LDS (SPH_LDS:
+// 9 entries, so that 4 workgroups of 256 threads still fit a CU's 160 KB)
+#define RT_MF_CAP_LDS 9
+#endif
 // LDS words per wave of the matrix-core walk: the two halves' queues
 #define RT_MF_QW (2u * RT_MF_CAP * 64u)
 
@@ -784,7 +789,7 @@ __device__ __forceinline__ bool mfma_wave_ok(v3 o, bool live) {
 #define MF_ECNT_INC
 #endif
 // SP: the drain's record array, global (const float4*) or the workgroup's
-// LDS copy (lds_cfloat4*, RT_MF_SPH_LDS builds).
+// LDS copy (lds_cfloat4*, rt_render_kernel).
 typedef __attribute__((address_space(3))) const float4 lds_cfloat4;
 __device__ __forceinline__ float4 rec_load(const float4* __restrict__ p, uint32_t i) { return p[i]; }
 __device__ __forceinline__ float4 rec_load(lds_cfloat4* p, uint32_t i) {
@@ -793,7 +798,7 @@ __device__ __forceinline__ float4 rec_load(lds_cfloat4* p, uint32_t i) {
     const f4v v = ((lds_f4v*)p)[i];  // one ds_read_b128
     return make_float4(v.x, v.y, v.z, v.w);
 }
-template <bool FAST, typename SP>
+template <bool FAST, typename SP, uint32_t CAP = RT_MF_CAP>
 __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, uint32_t cnt1,
                                            SP sph, uint32_t nsph,
                                            const uint32_t* __restrict__ perm, v3 o,
@@ -808,7 +813,7 @@ __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, ui
     const auto c0 = __builtin_amdgcn_permlane32_swap(cnt0, cnt0, false, false);
     const auto c1 = __builtin_amdgcn_permlane32_swap(cnt1, cnt1, false, false);
     const uint32_t na = t ? c1[0] : c0[0], nb = t ? c1[1] : c0[1];
-    const uint32_t* q = cq + t * (RT_MF_CAP * 64u);
+    const uint32_t* q = cq + t * (CAP * 64u);
 #ifdef RT_PROFILE
     uint32_t* const ecnt = ecnt_;  // [0] exact tests, [1] past the certain-miss shortcut (this lane)
 #endif
@@ -827,7 +832,7 @@ __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, ui
         if (m == 0) {
             const bool s1 = i >= na;
             const uint32_t e =
-                q[RT_IDX(s1 ? i - na : i, RT_MF_CAP, RT_SITE_MFQ_READ) * 64u + (s1 ? j + 32u : j)];
+                q[RT_IDX(s1 ? i - na : i, CAP, RT_SITE_MFQ_READ) * 64u + (s1 ? j + 32u : j)];
             m = e & RT_MF_FLAGS;
             // group index 8b + 2q (mf_unspread), + h: the column's lane
             // j (h = 0) or j + 32 (h = 1) queued it
@@ -896,10 +901,16 @@ __device__ __forceinline__ void tile_or(const f16x& H, int* gq, int& g) {
 // rt_intersect_mfma_kernel; never the render): tile_cnt[0] += the (block,
 // half) tiles the wave walks, tile_cnt[1] += the 2 nblk it would walk without
 // block bounds (rt_debug_intersect_tiles).
-// SPH_LDS (RT_MF_SPH_LDS builds): the drain's exact tests read the records
+// SPH_LDS (rt_render_kernel): the drain's exact tests read the records
 // from the workgroup's LDS copy sph_lds (render_body copies mf.sph there when
 // it fits) instead of global memory.
-template <bool COUNT = false, bool SPH_LDS = false>
+// MULTI: any list (the chunk loop over ceil(nblk / 16) bound chunks, with the
+// chunk-level bounds when mf.top); false: lists of at most 16 blocks (512
+// walk positions, e.g. RTIOW's 484 spheres) -- one bound chunk, no loop, no
+// chunk-level code (rt_render_kernel; rt_render_multi_kernel takes the rest):
+// the loop's code in the single-chunk kernel cost its walk 2.2 % (register
+// allocation and placement, profiles/r05/bisect/).
+template <bool COUNT = false, bool SPH_LDS = false, bool MULTI = true, uint32_t CAP = RT_MF_CAP>
 __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
                                                     uint32_t scene_fast, v3 o, v3 d, bool live,
                                                     uint64_t live_mask, float& t_out,
@@ -928,8 +939,9 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
     // With chunk-level bounds (mf.top) the first bound chunk tested is the
     // chunk-level one, after the ceil(nblk / 16) block-bound chunks.
     const bool has_b = mf.B != nullptr;
-    const uint32_t nbchunk = (nblk + 15u) >> 4;  // block-bound chunks: 16 blocks, 2 bounds each
-    const uint4* pb0 = has_b ? mf.B + (mf.top ? (size_t)nbchunk * RT_MF_BCHUNK : 0) : mfA;
+    // block-bound chunks: 16 blocks, 2 bounds each (one when !MULTI)
+    const uint32_t nbchunk = MULTI ? (nblk + 15u) >> 4 : 1u;
+    const uint4* pb0 = has_b ? mf.B + (MULTI && mf.top ? (size_t)nbchunk * RT_MF_BCHUNK : 0) : mfA;
     const uint32_t pb0_n = has_b ? RT_MF_BCHUNK : RT_MF_BLK;  // uint4 entries of chunk / block 0
     (void)pb0_n;  // (read by the checked build's RT_IDX only)
     uint4 bq0, bq1;
@@ -1063,7 +1075,7 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
     // j passes row j. Its tile (the same three MFMAs per half) runs first; a
     // half that no ray of passes chunk j gets no block of chunk j, and a chunk
     // neither half passes is not tested at all.
-    const uint32_t nchunk = (nblk + 31u) >> 5;   // of the walk: 32 blocks
+    const uint32_t nchunk = MULTI ? (nblk + 31u) >> 5 : 1u;  // of the walk: 32 blocks
     uint32_t mv0 = 0xFFFFFFFFu, mv1 = 0xFFFFFFFFu;  // lane k: walk chunk k's masks, halves 0 / 1
     if (has_b && rt_ballot(live && !(dd >= 0x1p-100f && dd <= 0x1p100f)) == 0) {
         mv0 = mv1 = 0u;
@@ -1102,6 +1114,25 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
                 mk2[t] = (uint32_t)bm | (uint32_t)(bm >> 32);
             }
         };
+        // bound rows 2i, 2i + 1 are block 16 k + i's halves: its bit is
+        // their OR, the 16 block bits compressed from the even positions
+        auto fold = [](uint32_t m) {
+            m = (m | (m >> 1)) & 0x55555555u;
+            m = (m | (m >> 1)) & 0x33333333u;
+            m = (m | (m >> 2)) & 0x0F0F0F0Fu;
+            m = (m | (m >> 4)) & 0x00FF00FFu;
+            m = (m | (m >> 8)) & 0x0000FFFFu;
+            return m;
+        };
+        if constexpr (!MULTI) {  // one bound chunk, preloaded: lane 0's masks
+            uint32_t mk2[2];
+            bound_tiles(mk2);
+            if (lane == 0u) {
+                mv0 = fold(mk2[0]);
+                mv1 = fold(mk2[1]);
+            }
+            PROF_ADD(17, 1);
+        } else {
         const bool top = mf.top != 0u;
         uint32_t top2[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};  // chunks some ray of each half passes near
         if (top) {
@@ -1119,8 +1150,12 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
                 // scalar-base form with a 32-bit lane offset, not three
                 // per-lane 64-bit pointers stepped through the loop
                 const uint4* pb = mf.B + (size_t)RT_IDX(k, nbchunk, RT_SITE_MF_BOUND) * RT_MF_BCHUNK;
+#ifndef RT_CHUNK_LSR
                 asm volatile("" : "+s"(pb));
                 const uint32_t l = opaque_lane();
+#else  // (A/B builds only: the loads as hipcc strength-reduces them)
+                const uint32_t l = lane;
+#endif
                 bq0 = pb[l];
                 bq1 = pb[64u + l];
                 bq2 = reinterpret_cast<const uint2*>(pb)[256u + l];
@@ -1131,16 +1166,6 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
                 mk2[0] = ((top2[0] >> k) & 1u) ? mk2[0] : 0u;
                 mk2[1] = ((top2[1] >> k) & 1u) ? mk2[1] : 0u;
             }
-            // bound rows 2i, 2i + 1 are block 16 k + i's halves: its bit is
-            // their OR, the 16 block bits compressed from the even positions
-            auto fold = [](uint32_t m) {
-                m = (m | (m >> 1)) & 0x55555555u;
-                m = (m | (m >> 1)) & 0x33333333u;
-                m = (m | (m >> 2)) & 0x0F0F0F0Fu;
-                m = (m | (m >> 4)) & 0x00FF00FFu;
-                m = (m | (m >> 8)) & 0x0000FFFFu;
-                return m;
-            };
             const uint32_t sh = (k & 1u) * 16u;
             const uint32_t f0 = fold(mk2[0]) << sh, f1 = fold(mk2[1]) << sh;
             if (lane == (k >> 1)) {
@@ -1149,6 +1174,7 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
             }
             PROF_ADD(17, 1);  // bound chunks: 2 halves x (2 MFMA 32x32x16 + 1 MFMA 32x32x8)
         }
+        }  // MULTI
     }
     PROF_MARK(16);  // ray column + bound tiles
 
@@ -1158,7 +1184,7 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
     // queue: a DS address past the LDS window drops the write): an append is
     // one store and one add; the counts are derived when needed
     uint32_t* const q0 = cq + lane;
-    uint32_t* const q1 = cq + RT_MF_CAP * 64u + lane;
+    uint32_t* const q1 = cq + CAP * 64u + lane;
     uint32_t *qp0 = q0, *qp1 = q1;
     auto qcount = [](const uint32_t* p, const uint32_t* p0) { return (uint32_t)(p - p0) >> 6; };
 #ifdef RT_SENS_MFMA
@@ -1178,17 +1204,17 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
     auto drain = [&](uint32_t cnt0, uint32_t cnt1) {
         if constexpr (SPH_LDS) {
             if (__builtin_expect(fast, 1))
-                mfma_drain<true>(cq, cnt0, cnt1, sph_lds, nblk * 32u, mf.perm, o, d, a, ya, best_t,
+                mfma_drain<true, lds_cfloat4*, CAP>(cq, cnt0, cnt1, sph_lds, nblk * 32u, mf.perm, o, d, a, ya, best_t,
                                  best_i MF_ECNT_PASS);
             else
-                mfma_drain<false>(cq, cnt0, cnt1, sph_lds, nblk * 32u, mf.perm, o, d, a, ya, best_t,
+                mfma_drain<false, lds_cfloat4*, CAP>(cq, cnt0, cnt1, sph_lds, nblk * 32u, mf.perm, o, d, a, ya, best_t,
                                   best_i MF_ECNT_PASS);
         } else {
             if (__builtin_expect(fast, 1))  // (the IEEE drain is placed out of the way)
-                mfma_drain<true>(cq, cnt0, cnt1, sph, nblk * 32u, mf.perm, o, d, a, ya, best_t,
+                mfma_drain<true, const float4*, CAP>(cq, cnt0, cnt1, sph, nblk * 32u, mf.perm, o, d, a, ya, best_t,
                                  best_i MF_ECNT_PASS);
             else
-                mfma_drain<false>(cq, cnt0, cnt1, sph, nblk * 32u, mf.perm, o, d, a, ya, best_t,
+                mfma_drain<false, const float4*, CAP>(cq, cnt0, cnt1, sph, nblk * 32u, mf.perm, o, d, a, ya, best_t,
                                   best_i MF_ECNT_PASS);
         }
     };
@@ -1198,8 +1224,8 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
         // a block adds at most 4 entries to each half's queue: make room first,
         // while no tile result is live (the lanes' own counts are compared
         // only when the scalar bound says the queue may be full)
-        if (__builtin_expect(max(ub0, ub1) + 4u > RT_MF_CAP &&
-                             rt_ballot(max(qcount(qp0, q0), qcount(qp1, q1)) + 4u > RT_MF_CAP) != 0,
+        if (__builtin_expect(max(ub0, ub1) + 4u > CAP &&
+                             rt_ballot(max(qcount(qp0, q0), qcount(qp1, q1)) + 4u > CAP) != 0,
                              0)) {  // (rare: kept out of the walk's hot blocks)
             const uint32_t cnt0 = qcount(qp0, q0), cnt1 = qcount(qp1, q1);
             PROF_ADD(11, 1);  // queue flushes
@@ -1250,21 +1276,21 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
                     PROF_ADD(23, 1);  // group appends (wave-level)
                     const uint32_t m = mf_flags(H[4 * q], H[4 * q + 1], H[4 * q + 2], H[4 * q + 3]);
                     // Branch-free append: every lane writes its next slot
-                    // (< RT_MF_CAP: the check above) and keeps it only with a
+                    // (< CAP: the check above) and keeps it only with a
                     // flag set. A lane whose column has no live ray has no
                     // flags: its T0 = +inf makes every V = +inf (no -inf
                     // term: the pad rows' S' = -inf meets the ray's -1).
                     // b * 8 has its low 3 bits clear: spread(8b + 2q) = spread(8b) + 2q
                     const uint32_t f = m & RT_MF_FLAGS;
 #ifdef RT_CHECK_BOUNDS
-                    RT_IDX(qcount(qp, t ? q1 : q0), RT_MF_CAP, RT_SITE_MFQ);
+                    RT_IDX(qcount(qp, t ? q1 : q0), CAP, RT_SITE_MFQ);
                     // a column without a live ray (T0 = +inf) never queues:
                     // this lane holds column lane & 31 of half t, the ray of
                     // lane 32 t + (lane & 31)
                     RT_IDX(f != 0u ? 1u : 0u,
                            ((live_mask >> (32u * t + (lane & 31u))) & 1u) ? 2u : 1u,
                            RT_SITE_DEAD_QUEUE);
-                    if (qcount(qp, t ? q1 : q0) >= RT_MF_CAP) qp = t ? q1 : q0;
+                    if (qcount(qp, t ? q1 : q0) >= CAP) qp = t ? q1 : q0;
 #endif
                     // the group index as one opaque SGPR: v_or_b32 (dual-
                     // issued) rather than v_or3_b32 with an inline constant

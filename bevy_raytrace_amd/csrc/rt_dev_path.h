@@ -116,23 +116,26 @@ struct PixelEntry {
 // z = 4, 2 or 1 consecutive samples of one pixel, each sample's colour
 // stored on its own. item_order picks the item -> (frame / pair / group,
 // pixel) map: pixel-major (bits 0, 1) puts one pixel's items back to back;
-// with bit 2 (grouped; npix a multiple of 8, rt_api.cpp) the pixels go in
-// groups of RT_PIX_GROUP = 8 consecutive ones (one row of an 8-wide tile:
-// 128 contiguous output / slot bytes) and a group's items back to back,
-// frame / pair / sample group major, pixel minor: a wave's 64 items then
-// hold 8 pixels of 8 frames, so the slots and output pixels it writes are
-// whole 128-B lines (one XCD's L2 merges them) instead of 16-B pieces of
-// lines that other waves -- on other XCDs -- complete.
-// Grouped: item j of a region with X entries per pixel -> group g = (j >> 3)
-// / X (floor division nests), rem = j - 8 g X, entry rem >> 3, pixel
-// 8 g + (rem & 7).
-#define RT_PIX_GROUP 8u
-__device__ __forceinline__ void grouped_split(uint32_t j, const FastDiv& dx, uint32_t& entry,
-                                              uint32_t& k) {
-    const uint32_t g = fdiv(j >> 3, dx);
-    const uint32_t rem = j - g * (RT_PIX_GROUP * dx.d);
-    entry = rem >> 3;
-    k = g * RT_PIX_GROUP + (rem & 7u);
+// with bit 2 (grouped; npix a multiple of the group, rt_api.cpp) the pixels
+// go in groups of G = 2^P.pix_group_shift (4 or 8) consecutive ones (one
+// row of a tile: 64 / 128 contiguous output / slot bytes) and a group's
+// items back to back, frame / pair / sample group major, pixel minor: a
+// wave's 64 items then hold G pixels of 64 / G frames, so the slots and
+// output pixels it writes are whole 64- / 128-B pieces (one XCD's L2 merges
+// them) instead of 16-B pieces of lines that other waves -- on other XCDs
+// -- complete.
+// Grouped: item j of a region with X entries per pixel -> group g = (j >> s)
+// / X (floor division nests), rem = j - G g X, entry rem >> s, pixel
+// G g + (rem & (G - 1)).
+#ifndef RT_GROUPED_ON
+#define RT_GROUPED_ON 1  // (0: the grouped order compiled out -- A/B builds only)
+#endif
+__device__ __forceinline__ void grouped_split(uint32_t j, const FastDiv& dx, uint32_t gs,
+                                              uint32_t& entry, uint32_t& k) {
+    const uint32_t g = fdiv(j >> gs, dx);
+    const uint32_t rem = j - ((g * dx.d) << gs);
+    entry = rem >> gs;
+    k = (g << gs) + (rem & ((1u << gs) - 1u));
 }
 __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint32_t item,
                                            const PixelEntry* __restrict__ tab, ItemLds L) {
@@ -152,8 +155,8 @@ __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint
         uint32_t f, b0, b1;  // frame, the item's blocks [b0, b1) (pass-relative)
         float4 a0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (item < main_pix) {
-            if (P.item_order & 4u) {  // grouped: 8 pixels' frames, frame-major in the group
-                grouped_split(item, P.div_nfpix, f, k);
+            if (RT_GROUPED_ON && (P.item_order & 4u)) {  // grouped: 8 pixels' frames, frame-major in the group
+                grouped_split(item, P.div_nfpix, P.pix_group_shift, f, k);
                 slot = f * npix + k;
             } else if (P.item_order & 2u) {  // pixel-major: one pixel's frames back to back
                 k = fdiv(item, P.div_nfpix);
@@ -176,8 +179,8 @@ __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint
         } else {
             const uint32_t j = item - main_pix;
             uint32_t r;  // the pair (relative to qpix); slot main_pix + r * npix + k
-            if (P.item_order & 4u) {  // grouped: 8 pixels' pairs, pair-major in the group
-                grouped_split(j, P.div_nreg, r, k);
+            if (RT_GROUPED_ON && (P.item_order & 4u)) {  // grouped: 8 pixels' pairs, pair-major in the group
+                grouped_split(j, P.div_nreg, P.pix_group_shift, r, k);
                 slot = main_pix + r * npix + k;
             } else if (P.item_order & 1u) {  // pixel-major: one pixel's pairs back to back
                 k = fdiv(j, P.div_nreg);
@@ -209,9 +212,9 @@ __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint
         j -= four ? 0u : (two ? ti1 : ti2);
         const uint32_t gb = four ? g0 : (two ? g1 : g2), ge = four ? g1 : (two ? g2 : g_end);
         uint32_t g;  // the item's sample group within its region
-        if (P.item_order & 4u) {  // grouped: 8 pixels' sample groups, group-major
+        if (RT_GROUPED_ON && (P.item_order & 4u)) {  // grouped: 8 pixels' sample groups, group-major
             const FastDiv dz = four ? P.div_ng4 : (two ? P.div_ng2 : P.div_ng1);
-            grouped_split(j, dz, g, k);
+            grouped_split(j, dz, P.pix_group_shift, g, k);
         } else if (P.item_order & 1u) {  // pixel-major: one pixel's groups back to back
             const FastDiv dz = four ? P.div_ng4 : (two ? P.div_ng2 : P.div_ng1);
             k = fdiv(j, dz);

@@ -33,11 +33,12 @@
 #define RT_MF_BLK 96u
 #define RT_MF_BCHUNK 160u  // uint4 entries per bound chunk: line rows K 0..31, forward rows K 0..7
 #define RT_GROUP 8            // spheres per filter group (SoA, 128 B)
-#ifndef RT_MF_SPH_LDS_MAX
-#define RT_MF_SPH_LDS_MAX 512 // RT_MF_SPH_LDS builds: walk records held in LDS (8 KB)
-#endif
+#define RT_MF_SPH_LDS_MAX 512 // rt_render_kernel: the walk's records held in LDS (8 KB, <= 16 blocks)
 #ifndef RT_SLOT_BUF_CAP
 #define RT_SLOT_BUF_CAP 32    // slot-store buffer entries per wave (rt_kernels.hip)
+#endif
+#ifndef RT_SLOT_BUF_CAP_LDS
+#define RT_SLOT_BUF_CAP_LDS 24  // ... in rt_render_kernel, whose LDS also holds the walk's records
 #endif
 #ifndef RT_CQ_CAP
 #define RT_CQ_CAP 8           // candidate-queue entries per lane (LDS)
@@ -149,6 +150,7 @@ struct KParams {
     // pixels' items back to back, frame / pair / sample-group major within
     // the group (rt_dev_path.h grouped_split)
     uint32_t item_order;
+    uint32_t pix_group_shift;  // grouped order (bit 2): log2 of the pixel group (2 or 3)
     FastDiv div_nfpix; // by main_pix / npix (frames with pixel items)
     FastDiv div_nreg;  // by qmain - qpix (pairs of the block-item region)
     // by the sample groups per pixel of the tail regions: (g1 - g0 + 3) / 4,

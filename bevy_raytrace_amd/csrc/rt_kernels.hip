@@ -186,10 +186,15 @@ __device__ __forceinline__ void store_system(float4* p, float4 v) {
 // The persistent render loop; CULL = false is rt_render_kernel (the brute-force
 // walk of the headline), CULL = true rt_render_cull_kernel (the permuted list
 // with group bounds, P.bnd / P.perm / P.nclusters; identical results).
-// SPH_LDS (RT_MF_SPH_LDS builds, rt_render_lds_kernel): the matrix-core
-// walk's records (mf.sph, <= RT_MF_SPH_LDS_MAX) copied into the workgroup's
-// LDS at the start, so the drain's dependent record load is an LDS read.
-template <bool CULL, bool SPH_LDS = false>
+// SPH_LDS (rt_render_kernel): the matrix-core walk's records (mf.sph, at
+// most RT_MF_SPH_LDS_MAX = 512 for a list of at most 16 blocks) copied into
+// the workgroup's LDS at the start, so the drain's dependent record load is
+// an LDS read, not an L1 hit: -1.2 % cycles per headline launch net of the
+// queue entries it costs (9 per lane and half instead of 12; slot buffer 24
+// instead of 32: 4 workgroups per CU still fit), profiles/r05/lds/.
+// MULTI: the matrix-core walk for any list (rt_render_multi_kernel); false:
+// lists of at most 16 blocks (rt_render_kernel; intersect_world_mfma MULTI).
+template <bool CULL, bool SPH_LDS = false, bool MULTI = false>
 __device__ __forceinline__ void render_body(
     const KParams& P, const float4* grp, const float4* __restrict__ sph,
     const float4* __restrict__ shd,
@@ -197,14 +202,17 @@ __device__ __forceinline__ void render_body(
     uint32_t* __restrict__ work_counter,
     unsigned long long* __restrict__ seg_counter, unsigned long long* __restrict__ dbg) {
     const uint32_t lane = __lane_id();
-#ifdef RT_MF_SPH_LDS
+    // the queue and slot-buffer capacities of this kernel (LDS budget)
+    constexpr uint32_t MFCAP = SPH_LDS ? RT_MF_CAP_LDS : RT_MF_CAP;
+    constexpr uint32_t SBCAP = SPH_LDS ? RT_SLOT_BUF_CAP_LDS : RT_SLOT_BUF_CAP;
     __shared__ float4 s_msph[SPH_LDS ? RT_MF_SPH_LDS_MAX : 1];
     if constexpr (SPH_LDS) {
-        const uint32_t nrec = P.mf.nblk * 32u;  // <= RT_MF_SPH_LDS_MAX (rt_launch_render)
-        for (uint32_t i = threadIdx.x; i < nrec; i += RT_BLOCK_THREADS) s_msph[i] = P.mf.sph[i];
+        if (P.mf.A) {  // nblk <= 16: nblk * 32 <= RT_MF_SPH_LDS_MAX (rt_launch_render)
+            const uint32_t nrec = P.mf.nblk * 32u;
+            for (uint32_t i = threadIdx.x; i < nrec; i += RT_BLOCK_THREADS) s_msph[i] = P.mf.sph[i];
+        }
         __syncthreads();
     }
-#endif
     PROF_DECL
     PROF_START();
 #ifdef RT_PROFILE
@@ -227,8 +235,8 @@ __device__ __forceinline__ void render_body(
     // drains the queue of one walk before it starts another, so both share
     // one array (the brute-force kernel's LDS: 36 KB per workgroup)
 #ifdef RT_MFMA_FILTER
-    constexpr uint32_t QW = CULL ? 64u * RT_CQ_CAP : RT_MF_QW;  // words per wave
-    static_assert(2u * RT_MF_CAP >= RT_CQ_CAP, "the shared queue holds the VALU walk's");
+    constexpr uint32_t QW = CULL ? 64u * RT_CQ_CAP : 2u * MFCAP * 64u;  // words per wave
+    static_assert(2u * MFCAP >= RT_CQ_CAP, "the shared queue holds the VALU walk's");
 #else
     constexpr uint32_t QW = 64u * RT_CQ_CAP;
 #endif
@@ -245,12 +253,12 @@ __device__ __forceinline__ void render_body(
     // when it would overflow (and at the end). A vector store holds vmcnt
     // until the memory acknowledges it, so a store issued on its own makes the
     // wave's next wait on a load (table entry, A fragments) wait for the
-    // store too: one such wait per RT_SLOT_BUF_CAP slots instead of one per
+    // store too: one such wait per SBCAP slots instead of one per
     // iteration that stores. sbn: entries held (wave-uniform).
-    __shared__ float4 s_sbv[(RT_BLOCK_THREADS / 64) * RT_SLOT_BUF_CAP];
-    __shared__ uint32_t s_sbs[(RT_BLOCK_THREADS / 64) * RT_SLOT_BUF_CAP];
-    float4* const sbv = s_sbv + wave * RT_SLOT_BUF_CAP;
-    uint32_t* const sbs = s_sbs + wave * RT_SLOT_BUF_CAP;
+    __shared__ float4 s_sbv[(RT_BLOCK_THREADS / 64) * SBCAP];
+    __shared__ uint32_t s_sbs[(RT_BLOCK_THREADS / 64) * SBCAP];
+    float4* const sbv = s_sbv + wave * SBCAP;
+    uint32_t* const sbs = s_sbs + wave * SBCAP;
     uint32_t sbn = 0;
     // one finished slot: a block-sum slot, or (RT_DIRECT_ITEM) an output pixel
     // = fold / spp, alpha 1 -- rt_collect_kernel's arithmetic
@@ -456,21 +464,12 @@ __device__ __forceinline__ void render_body(
 #ifdef RT_MFMA_FILTER
         } else if (__builtin_expect(!CULL && P.mf.A && mfma_wave_ok(st.o, has_item), 1)) {  // the whole wave
             PROF_ADD(18, 1);
-#ifdef RT_MF_SPH_LDS
-            const int h2 = intersect_world_mfma<false, SPH_LDS>(P.mf, P.scene_fast, st.o, st.d,
-                                                                has_item, live, t, cqm
+            const int h2 = intersect_world_mfma<false, SPH_LDS, MULTI, MFCAP>(
+                P.mf, P.scene_fast, st.o, st.d, has_item, live, t, cqm
 #ifdef RT_PROFILE
-                                                                , prof_
+                , prof_
 #endif
-                                                                , nullptr, (lds_cfloat4*)s_msph);
-#else
-            const int h2 = intersect_world_mfma(P.mf, P.scene_fast, st.o, st.d,
-                                                has_item, live, t, cqm
-#ifdef RT_PROFILE
-                                                , prof_
-#endif
-                                                );
-#endif
+                , nullptr, (lds_cfloat4*)s_msph);
             if (has_item) hi = h2;
             else t = VERY_FAR;
 #endif
@@ -577,14 +576,14 @@ __device__ __forceinline__ void render_body(
             const uint64_t sm = rt_ballot(spend);
             if (sm != 0) {
                 const uint32_t n = (uint32_t)__popcll(sm);
-                if (sbn + n > RT_SLOT_BUF_CAP) sb_flush();
-                if (n > RT_SLOT_BUF_CAP) {
+                if (sbn + n > SBCAP) sb_flush();
+                if (n > SBCAP) {
                     if (spend) put(sslot, sval);
                 } else {
                     if (spend) {
                         const uint32_t r = sbn + lanemask_lt_count(sm);
-                        sbv[RT_IDX(r, RT_SLOT_BUF_CAP, RT_SITE_SLOTBUF)] = sval;
-                        sbs[RT_IDX(r, RT_SLOT_BUF_CAP, RT_SITE_SLOTBUF)] = sslot;
+                        sbv[RT_IDX(r, SBCAP, RT_SITE_SLOTBUF)] = sval;
+                        sbs[RT_IDX(r, SBCAP, RT_SITE_SLOTBUF)] = sslot;
                     }
                     sbn = __builtin_amdgcn_readfirstlane(sbn + n);
                 }
@@ -647,19 +646,19 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_re
     const PixelEntry* __restrict__ tab, float4* __restrict__ block_sums,
     uint32_t* __restrict__ work_counter,
     unsigned long long* __restrict__ seg_counter, unsigned long long* __restrict__ dbg) {
-    render_body<false>(P, grp, sph, shd, tab, block_sums, work_counter, seg_counter, dbg);
+    render_body<false, true, false>(P, grp, sph, shd, tab, block_sums, work_counter, seg_counter, dbg);
 }
 
-#ifdef RT_MF_SPH_LDS
-__global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_render_lds_kernel(
+// lists of more than 16 blocks (the bound-chunk loop, chunk-level bounds)
+__global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD) void rt_render_multi_kernel(
     KParams P, const float4* grp, const float4* __restrict__ sph,
     const float4* __restrict__ shd,
     const PixelEntry* __restrict__ tab, float4* __restrict__ block_sums,
     uint32_t* __restrict__ work_counter,
     unsigned long long* __restrict__ seg_counter, unsigned long long* __restrict__ dbg) {
-    render_body<false, true>(P, grp, sph, shd, tab, block_sums, work_counter, seg_counter, dbg);
+    render_body<false, false, true>(P, grp, sph, shd, tab, block_sums, work_counter, seg_counter, dbg);
 }
-#endif
+
 
 __global__ __launch_bounds__(RT_BLOCK_THREADS, RT_MIN_WAVES_PER_SIMD_CULL) void rt_render_cull_kernel(
     KParams P, const float4* grp, const float4* __restrict__ sph,
@@ -834,10 +833,15 @@ __global__ void rt_collect_kernel(KParams P, const float4* __restrict__ block_su
     // P.dsys (RT_FLAG_IMAGE_OUT, or a host-output call writing the caller's
     // registered buffer): the rows may live in another device's memory (rank
     // 0's image mapped over HIP IPC, bevy_raytrace_amd/distributed.py) or in
-    // host memory. The wave's stores above are system-scope write-through;
-    // this system-scope release (buffer_wbl2 sc0 sc1 + the wait for every store
-    // of the wave) ends the wave's part of the hand-off; the reader acquires
-    // (rt_acquire) after the host has seen the launch complete.
+    // host memory. Every byte the reader takes from this wave was stored
+    // above with a system-scope write-through store (sc0 sc1: the line leaves
+    // this device's L2, nothing of it stays dirty here), and the wave waits
+    // for every one of those stores to be acknowledged (vmcnt(0)) before it
+    // ends; the reader acquires (rt_acquire) after the host has seen the
+    // launch complete -- MI355X_MICROARCH.md's write-through
+    // producer form, which needs no release. P.dsys_release adds the
+    // per-wave system-scope release of the round-4 form (buffer_wbl2 sc0 sc1,
+    // a write-back of the whole L2: 2.3 ms per N = 8 shard call; A/B only).
     if (P.dsys) {
         if (P.dsys_release) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the asm store is invisible to hipcc)
@@ -903,12 +907,10 @@ hipError_t rt_launch_render(const KParams* P, const float4* grp, const float4* s
         hipLaunchKernelGGL(rt_render_cull_kernel, dim3(grid), dim3(RT_BLOCK_THREADS), dyn, stream,
                            *P, grp, sph, shd, reinterpret_cast<const PixelEntry*>(pd),
                            block_sums, work_counter, seg_counter, seg_counter + 2);
-#ifdef RT_MF_SPH_LDS
-    else if (P->mf.A && P->mf.nblk * 32u <= RT_MF_SPH_LDS_MAX)
-        hipLaunchKernelGGL(rt_render_lds_kernel, dim3(grid), dim3(RT_BLOCK_THREADS), dyn, stream, *P,
+    else if (P->mf.A && P->mf.nblk > 16u)  // more than one bound chunk
+        hipLaunchKernelGGL(rt_render_multi_kernel, dim3(grid), dim3(RT_BLOCK_THREADS), dyn, stream, *P,
                            grp, sph, shd, reinterpret_cast<const PixelEntry*>(pd),
                            block_sums, work_counter, seg_counter, seg_counter + 2);
-#endif
     else
         hipLaunchKernelGGL(rt_render_kernel, dim3(grid), dim3(RT_BLOCK_THREADS), dyn, stream, *P,
                            grp, sph, shd, reinterpret_cast<const PixelEntry*>(pd),
@@ -1056,6 +1058,10 @@ hipError_t rt_render_occupancy(int* blocks_per_cu, int* blocks_per_cu_cull) {
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_render_kernel,
                                                                 RT_BLOCK_THREADS, 0);
     if (e != hipSuccess) return e;
+    int multi = 0;  // the two brute-force kernels take the same grid
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&multi, rt_render_multi_kernel, RT_BLOCK_THREADS, 0);
+    if (e != hipSuccess) return e;
+    if (multi < *blocks_per_cu) *blocks_per_cu = multi;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu_cull, rt_render_cull_kernel,
                                                         RT_BLOCK_THREADS, 0);
 }

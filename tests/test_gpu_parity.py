@@ -260,8 +260,9 @@ def test_item_order_identical(renderer, S, region, tail):
     renderer.set_scene(sp, mt)
     renderer.tune(block_region=region, tail=tail)
     outs = []
-    for order in ("0", "1", "2", "3", "4", "7"):
-        renderer.tune(item_order=order)
+    for order in ("0", "1", "2", "3", "4", "7", "7/4"):  # 7/4: groups of 4 pixels
+        o, _, g = order.partition("/")
+        renderer.tune(item_order=o, pix_group=g or "8")
         buf = torch.empty((F, H, W, 4), dtype=torch.float32, device="cuda")
         renderer.render_frames_device(cam, F, buf.data_ptr(), W, H, S, 10, flags=NO_REUSE)
         st = renderer.wait()
