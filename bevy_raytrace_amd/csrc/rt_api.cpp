@@ -70,14 +70,19 @@ struct Tuning {
     bool split_all = false;       // without primary reuse, every block as single samples
     bool tail_split = true;       // single-sample tail items at the end of a launch
     double tail[3] = {0.0, 1.0, 1.0};  // tail regions (4-, 2-, 1-sample items) x D x lanes
-    double block_region = 96.0;   // single-block items before the tail, x D x lanes samples
+    double block_region = 64.0;   // single-block items before the tail, x D x lanes samples
     // KParams::item_order: pixel-major block / tail items (bit 0) and pixel
     // items (bit 1): a wave's lanes then share pixels, so its primary rays
     // (and first-bounce origins) coincide -- warm 20-frame launches, one box
     // (profiles/r03/item_order/): full frame 243.7 -> 240.2 ms, N=8 shard
     // 34.9 -> 33.5 ms; 1 alone 242.6 / 33.5, 2 alone 241.0 / 35.4
-    uint32_t item_order = 3;
-    uint32_t pix_group = 8;       // item_order bit 2: pixels per group (4 or 8)
+    // bit 2 (round 5): grouped by pix_group = 4 neighbouring pixels, so
+    // a wave's slot and output stores are whole 64-B pieces of lines its own
+    // XCD's L2 merges: render-kernel writes per headline launch 2.41 ->
+    // 1.74 GB at the same time (groups of 8: 1.73 GB but +0.4 % time, the
+    // rays of 8 pixels per wave less coherent), profiles/r05/item_order/
+    uint32_t item_order = 7;
+    uint32_t pix_group = 4;       // item_order bit 2: pixels per group (4 or 8)
     bool prefetch = true;         // waves prefetch their next work chunk
     uint32_t prio_mode = 1;       // s_setprio rotation: 0 off, 1 by iteration, 3 by wall time
     uint32_t prio_shift = 14;     // mode 3 step: 2^prio_shift ticks of 10 ns
@@ -1248,14 +1253,17 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         return L < 1 ? 1 : (L > pairs ? pairs : L);
     };
     // Block-item region: the last ~a8*D samples per lane of the main part are
-    // dealt as single-block items (knob block_region = a8, default 96), so the
+    // dealt as single-block items (knob block_region = a8, default 64), so the
     // lanes still holding a pixel item (up to spp*D iterations) when the main
     // part runs out finish inside the block items and the tail. It has to be
     // long: the SIMD arbiter issues by age, and the youngest waves of a SIMD
     // iterate several times slower than the oldest, so their
     // last pixel items end late. Measured at 1080p/64, 24-frame launches
     // (kernel ms, one box): a8 = 12: 521, 24: 524, 48: 517, 96: 511.5 -- the
-    // round-1 all-block-items kernel 511.7. In pairs:
+    // round-1 all-block-items kernel 511.7. Round 5, grouped item order,
+    // 20-frame launches (profiles/r05/block_region): 96: 191.8 ms, 64: 191.3,
+    // 48: 194.0; render-kernel writes 1.74 / 1.50 / 1.40 GB (fewer block
+    // items, fewer slots). In pairs:
     const uint64_t A8 = per_px(tn.block_region, 1);
     auto block_pairs = [&](uint64_t qmain) -> uint64_t {
         const uint64_t Q = (A8 + RT_SAMPLE_BLOCK - 1) / RT_SAMPLE_BLOCK;

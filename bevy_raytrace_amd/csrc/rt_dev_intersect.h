@@ -665,6 +665,10 @@ typedef float f16x __attribute__((ext_vector_type(16)));
 // exact products (two chained MFMAs, 33 roundings at most, each <= 2^-24 of
 // sum |p| <= 4.1 (|o|^2 + |c|^2) + |S'|) add <= 2^-16.9 (|o|^2 + |c|^2) +
 // 2^-19 |S'| (measured: <= 4.9 * 2^-24 sum |p|, profiles/r02_mfma_acc.log).
+// ASSUMPTION: that rounding model of the MFMA's f32 accumulation -- at most
+// one rounding per added term -- is measured (tools/ubench/mfma_acc.hip), not
+// a documented property of the hardware; DESIGN.md 4.2 states it and its
+// evidence.
 // The ray features' own roundings (one fma for L, two products for Q, the
 // fma of T0) add <= 2^-21 (|o|^2 + |c|^2), and the ray constants dn, k1, o2
 // are the VALU filter's (<= 25 * 2^-24 (|o|^2 + |c|^2), ray_filter_consts).

@@ -142,7 +142,7 @@ struct KParams {
     // matrix-core filter (RT_MFMA_FILTER builds, brute-force walk; mf.A null:
     // the packed VALU filter)
     MfScene mf;
-    // queue order (knob item_order, bits; default 3): bit 0 the block items
+    // queue order (knob item_order, bits; default 7, groups of 4): bit 0 the block items
     // and the tail items, bit 1 the pixel items, pixel-major
     // (consecutive items: one pixel's pairs / samples / frames) instead of
     // pair- / sample- / frame-major (consecutive items: neighbouring pixels);
