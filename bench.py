@@ -537,8 +537,9 @@ def main():
         if dist_on:
             dist.barrier()
         if use_ipc and rank == 0:
-            # every rank's rows are in rank 0's image (system-scope stores +
-            # release, each rank's launch complete before the barrier): the
+            # every rank's rows are in rank 0's image (system-scope
+            # write-through stores, acknowledged before each collect wave
+            # retires; each rank's launch complete before the barrier): the
             # acquire makes them visible to what rank 0 runs next
             r.acquire(stream.cuda_stream)
             torch.cuda.synchronize()

@@ -70,7 +70,7 @@ struct Tuning {
     bool split_all = false;       // without primary reuse, every block as single samples
     bool tail_split = true;       // single-sample tail items at the end of a launch
     double tail[3] = {0.0, 1.0, 1.0};  // tail regions (4-, 2-, 1-sample items) x D x lanes
-    double block_region = 64.0;   // single-block items before the tail, x D x lanes samples
+    double block_region = -1.0;   // single-block items before the tail, x D x lanes samples (-1: by spp / D)
     // KParams::item_order: pixel-major block / tail items (bit 0) and pixel
     // items (bit 1): a wave's lanes then share pixels, so its primary rays
     // (and first-bounce origins) coincide -- warm 20-frame launches, one box
@@ -1253,7 +1253,7 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         return L < 1 ? 1 : (L > pairs ? pairs : L);
     };
     // Block-item region: the last ~a8*D samples per lane of the main part are
-    // dealt as single-block items (knob block_region = a8, default 64), so the
+    // dealt as single-block items (knob block_region = a8, default by the call), so the
     // lanes still holding a pixel item (up to spp*D iterations) when the main
     // part runs out finish inside the block items and the tail. It has to be
     // long: the SIMD arbiter issues by age, and the youngest waves of a SIMD
@@ -1262,9 +1262,19 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     // (kernel ms, one box): a8 = 12: 521, 24: 524, 48: 517, 96: 511.5 -- the
     // round-1 all-block-items kernel 511.7. Round 5, grouped item order,
     // 20-frame launches (profiles/r05/block_region): 96: 191.8 ms, 64: 191.3,
-    // 48: 194.0; render-kernel writes 1.74 / 1.50 / 1.40 GB (fewer block
-    // items, fewer slots). In pairs:
-    const uint64_t A8 = per_px(tn.block_region, 1);
+    // 56: 190.6, 48: 194.0; render-kernel writes 1.74 / 1.50 / - / 1.40 GB
+    // (fewer block items, fewer slots). The region has to outlast the last
+    // pixel item, whose length is the frame's samples (spp x the path's
+    // iterations): the 10,000-sphere frame (128 spp, two-frame launches,
+    // profiles/r05/block_region/call11, call12) took 405 ms at 64, 160-175 at
+    // 96, 154.8 at 128 and 157.2 at 160. So by the call: a8 = 16 spp / D, at
+    // least 64 and at most 128 (headline 64; 10k, 4K and the 8K frame 128:
+    // 4K 182.3 vs 181.6 ms, 8K 2,292 vs 2,288 ms at 96 -- within their runs'
+    // spread).
+    const double a8 = tn.block_region >= 0.0
+                          ? tn.block_region
+                          : std::min(128.0, std::max(64.0, 16.0 * p.spp / std::max(p.max_depth, 1u)));
+    const uint64_t A8 = per_px(a8, 1);
     auto block_pairs = [&](uint64_t qmain) -> uint64_t {
         const uint64_t Q = (A8 + RT_SAMPLE_BLOCK - 1) / RT_SAMPLE_BLOCK;
         return Q > qmain ? qmain : Q;
@@ -1371,7 +1381,8 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     // image layout: one shard, or RT_FLAG_IMAGE_OUT); the launch's output
     // indices below RT_INDEX_LIMIT
     // another device's image (RT_FLAG_IMAGE_OUT): system-scope write-through
-    // stores and a release per wave (collect) -- and no direct output from the
+    // stores, acknowledged before each wave retires (collect; the per-wave
+    // release only with knob dsys_release) -- and no direct output from the
     // render kernel: a store that crosses xGMI or PCIe is acknowledged so late
     // that the wave's next load wait stalls on it (measured: the reference's
     // 1-spp frame written into a registered host buffer by the render kernel
