@@ -670,7 +670,9 @@ def main():
         "hbm_peak_gbps": 8000.0,
         "valu_busy": valu_report(pmc),
         "matrix_core": mfma_report(pmc),
-        "kernel": "rt_render_kernel",
+        # the render kernel of this workload (rt_render_kernel: lists of <= 16
+        # blocks; rt_render_multi_kernel: longer ones)
+        "kernel": (pmc or {}).get("render_kernel", "rt_render_kernel"),
         "kernel_ms_per_launch": round(kms_launch, 3),
         # the metric's fp32 roofline, kept as a ratio: the reference
         # algorithm's 18 x N fp32 flops per traced segment at this rate over

@@ -1191,10 +1191,6 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
     uint32_t* const q1 = cq + CAP * 64u + lane;
     uint32_t *qp0 = q0, *qp1 = q1;
     auto qcount = [](const uint32_t* p, const uint32_t* p0) { return (uint32_t)(p - p0) >> 6; };
-#ifdef RT_SENS_MFMA
-    h8v zeroB = {};
-    asm volatile("" : "+v"(zeroB));
-#endif
 #ifdef RT_PROFILE
     // this lane's exact tests (c[13]: wave max, c[15]: lane sum) and those
     // past the certain-miss shortcut (c[21]: lane sum)
@@ -1241,38 +1237,15 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
         h8v A0, A1;
         __builtin_memcpy(&A0, &x0, 16);
         __builtin_memcpy(&A1, &x1, 16);
-        // the two halves unrolled (no per-tile operand selects) but kept apart
-        // (sched_barrier): one tile's 16 result registers live at a time
-#pragma unroll
-        for (uint32_t t = 0; t < 2; ++t) {
-            if (t) __builtin_amdgcn_sched_barrier(0);
-            if ((((t ? m1 : m0) >> (b & 31u)) & 1u) == 0u) continue;  // no ray of the half near the block
-            PROF_ADD(10, 1);  // tiles walked
-#if defined(RT_SENS_MFMA) || defined(RT_SENS_VALU)
-            f16x H = __builtin_amdgcn_mfma_f32_32x32x16_f16(
-#else
-            const f16x H = __builtin_amdgcn_mfma_f32_32x32x16_f16(
-#endif
-                A1, t ? B11 : B01,
-                __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, t ? B10 : B00, zero, 0, 0, 0), 0, 0, 0);
-#ifdef RT_SENS_MFMA
-            // sensitivity probe (timing only, same bits): one more MFMA per
-            // tile on the matrix pipe, adding zero products to V
-            H = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, zeroB, H, 0, 0, 0);
-#endif
-#ifdef RT_SENS_VALU
-            // sensitivity probe (timing only): RT_SENS_VALU dual-issued moves
-            // per tile on the VALU issue port
-#pragma unroll
-            for (int k = 0; k < RT_SENS_VALU; ++k) asm volatile("v_mov_b32 %0, %0" : "+v"(H[k & 15]));
-#endif
+        const uint32_t sb = mf_spread(b * 8u);  // the block's group entries (wave-uniform, SALU)
+        // the appends of half t's tile H
+        auto tile = [&](const f16x& H, uint32_t t) {
             // per-group ORs (the lane's 4 groups of 4 spheres), then the tile's
             int gq[4], g;
             tile_or(H, gq, g);
             if (rt_ballot(g < 0) != 0) {
                 PROF_ADD(5, 1);  // tiles with a candidate
                 uint32_t*& qp = t ? qp1 : qp0;
-                const uint32_t sb = mf_spread(b * 8u);  // wave-uniform (SALU)
 #pragma unroll
                 for (uint32_t q = 0; q < 4; ++q) {
                     if (rt_ballot(gq[q] < 0) == 0) continue;  // no lane has one in this group
@@ -1308,6 +1281,36 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
                     qp += 64u * inc;
                 }
             }
+        };
+        auto mfma2 = [&](const h8v& Bk0, const h8v& Bk1) {
+            return __builtin_amdgcn_mfma_f32_32x32x16_f16(
+                A1, Bk1, __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bk0, zero, 0, 0, 0), 0, 0, 0);
+        };
+        const bool w0 = ((m0 >> (b & 31u)) & 1u) != 0u, w1 = ((m1 >> (b & 31u)) & 1u) != 0u;
+#ifdef RT_WALK_BOTH
+        if (w0 && w1) {
+            // both halves walk the block: the four MFMAs back to back, so
+            // half 1's run on the matrix pipe while half 0's results are ORed
+            PROF_ADD(10, 2);
+            const f16x Ha0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B00, zero, 0, 0, 0);
+            const f16x Hb0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B10, zero, 0, 0, 0);
+            const f16x H0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B01, Ha0, 0, 0, 0);
+            const f16x H1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B11, Hb0, 0, 0, 0);
+            tile(H0, 0u);
+            tile(H1, 1u);
+            return;
+        }
+#endif
+        // the two halves unrolled (no per-tile operand selects) but kept apart
+        // (sched_barrier): one tile's 16 result registers live at a time
+        if (w0) {
+            PROF_ADD(10, 1);  // tiles walked
+            tile(mfma2(B00, B01), 0u);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (w1) {
+            PROF_ADD(10, 1);
+            tile(mfma2(B10, B11), 1u);
         }
     };
     // The blocks some ray of the wave passes near (all blocks without bound

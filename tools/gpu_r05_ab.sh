@@ -2,6 +2,7 @@
 # driver-form bench (--steps 20) interleaved over several builds of the same
 # ABI, ROUNDS rounds (default 3).  usage:
 #   bash tools/gpu_r05_ab.sh <out dir> [--tests] <arm>=<lib|product>[:knob=v,knob=v] ... [-- extra bench args]
+# (a value holding commas is written with '/': tail=0/0.5/1)
 set -uo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
@@ -31,7 +32,7 @@ armargs() {
   if [ "$lib" != product ]; then out="--lib $lib"; fi
   if [ "$spec" != "$lib" ]; then
     tunes=${spec#*:}
-    for kv in ${tunes//,/ }; do out="$out --tune $kv"; done
+    for kv in ${tunes//,/ }; do out="$out --tune ${kv//\//,}"; done  # '/' in a value: ','  (tail=0/1/1)
   fi
   echo "$out"
 }

@@ -4,7 +4,9 @@
 # with the CPU baseline), driver form (--steps 20) and the same command under
 # rocprofv3 --kernel-trace --stats; rtiow4k (1 frame), spheres10k1080 (2),
 # rtiow8k (the 8K frame on one GPU); the reference's own frame through the
-# shim's call sequence.  usage: bash tools/gpu_r05_record.sh <out dir>
+# shim's call sequence; then the multi-rank rehearsal on this GPU
+# (tools/gpu_r04_multi.sh: all 8 N = 8 shards, 8 ranks through the IPC image
+# path, 2 through the RCCL gather).  usage: bash tools/gpu_r05_record.sh <out dir>
 set -uo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
@@ -33,4 +35,6 @@ step bench_8k_1gpu $?
 timeout -k 10 300 python -u bench.py --config reference1080 --steps 20 --warmup 4 \
     > $O/bench_reference1080.json 2> $O/bench_ref.err
 step ref $?
+bash tools/gpu_r04_multi.sh $O/multi
+step multi $?
 exit 0

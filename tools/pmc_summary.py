@@ -34,12 +34,16 @@ for f in glob.glob(os.path.join(out_dir, "pmc_*", "**", "*kernel_trace.csv"), re
             durs[k].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-6)
 
 mean = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in vals.items()}
-rk = mean.get("rt_render_kernel", {})
+# the render kernel the workload ran: rt_render_kernel (lists of <= 16
+# blocks) or rt_render_multi_kernel (longer lists), the one with the most time
+RK = max((k for k in durs if k in ("rt_render_kernel", "rt_render_multi_kernel")),
+         key=lambda k: sum(durs[k]), default="rt_render_kernel")
+rk = mean.get(RK, {})
 summary = {"command": "tools/pmc_round.sh: rocprofv3 --kernel-trace --pmc <group> -- python3 bench.py "
                       f"--steps {fpl} --warmup 0 --frames-per-launch {fpl} --no-cpu-baseline --reuse-steps 0",
+           "render_kernel": RK,
            "per_dispatch_mean": mean,
-           "render_kernel_ms_under_pmc": (sum(durs["rt_render_kernel"]) / len(durs["rt_render_kernel"])
-                                          if durs["rt_render_kernel"] else None)}
+           "render_kernel_ms_under_pmc": (sum(durs[RK]) / len(durs[RK]) if durs[RK] else None)}
 if rk:
     w = rk.get("SQ_WAVE_CYCLES"), rk.get("SQ_BUSY_CYCLES"), rk.get("GRBM_GUI_ACTIVE")
     if rk.get("SQ_ACTIVE_INST_VALU") and rk.get("SQ_WAVES"):
@@ -51,7 +55,7 @@ if "FETCH_SIZE" in rk and "WRITE_SIZE" in rk:
     write = rk["WRITE_SIZE"] * 1024
     tp = os.path.join(root, "profiles", "pmc_traffic.json")
     d = json.load(open(tp)) if os.path.exists(tp) else {}
-    d[wl] = {"hbm_bytes_per_launch": int(fetch + write), "fetch_bytes": int(fetch),
+    d[wl] = {"render_kernel": RK, "hbm_bytes_per_launch": int(fetch + write), "fetch_bytes": int(fetch),
              "write_bytes": int(write), "frames_per_launch": fpl,
              "source": f"profiles/{tag}_pmc_{wl}.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
                        "separate passes; FETCH_SIZE x2 per gfx950 correction, x1024 KB->B)",
