@@ -84,7 +84,7 @@ struct Tuning {
     uint32_t item_order = 7;
     uint32_t pix_group = 4;       // item_order bit 2: pixels per group (4 or 8)
     bool prefetch = true;         // waves prefetch their next work chunk
-    uint32_t prio_mode = 1;       // s_setprio rotation: 0 off, 1 by iteration, 3 by wall time
+    int32_t prio_mode = -1;       // s_setprio rotation: 0 off, 1 by iteration, 3 by wall time (-1: by the call)
     uint32_t prio_shift = 14;     // mode 3 step: 2^prio_shift ticks of 10 ns
     uint32_t wg_per_cu = 0;       // resident workgroups per CU (0 = by the call's size, enqueue)
     int64_t wide_max = -1;        // sphere-parallel threshold (-1 = cost model)
@@ -280,7 +280,7 @@ static bool tune_set(Tuning& t, const char* name, const char* v) {
     } else if (!strcmp(name, "prefetch")) {
         t.prefetch = x != 0;
     } else if (!strcmp(name, "prio_mode")) {
-        t.prio_mode = (uint32_t)x;
+        t.prio_mode = (int32_t)x;
     } else if (!strcmp(name, "prio_shift")) {
         t.prio_shift = (uint32_t)x;
     } else if (!strcmp(name, "wg_per_cu")) {
@@ -1433,7 +1433,16 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     K_.div_tw = make_fastdiv(tw);
     K_.div_wrem = make_fastdiv(K_.tile_wrem ? K_.tile_wrem : 1);
     K_.prefetch = tn.prefetch ? 1u : 0u;
-    K_.prio_mode = tn.prio_mode;
+    // The rotation evens out the SIMD's age-ordered issue where the launch's
+    // drain is a large share (DESIGN.md 4.1 issue fairness); in launches of
+    // many samples per lane it costs more than it returns. Round 5, one box
+    // (profiles/r05/prio/): off vs on -- headline (10,125 samples per lane)
+    // -0.33 %, 4K (8,100) -0.5 %; the N = 8 shard (1,266) +0.7 %, 10k
+    // spheres (2,025) +0.8 %. By the call: on below 4,096 samples per lane.
+    {
+        const double spl = (double)npix * p.spp * nframes / (double)std::max<uint64_t>(lanes, 1);
+        K_.prio_mode = tn.prio_mode >= 0 ? (uint32_t)tn.prio_mode : (spl < 4096.0 ? 1u : 0u);
+    }
     K_.prio_shift = tn.prio_shift;
     // wide (sphere-parallel) tracing pays ~32 VALU per 64 spheres per ray plus
     // a reduction; the ray-parallel walk ~34 per 8-sphere group per wave plus

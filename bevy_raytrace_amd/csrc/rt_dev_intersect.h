@@ -1287,22 +1287,11 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
                 A1, Bk1, __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, Bk0, zero, 0, 0, 0), 0, 0, 0);
         };
         const bool w0 = ((m0 >> (b & 31u)) & 1u) != 0u, w1 = ((m1 >> (b & 31u)) & 1u) != 0u;
-#ifdef RT_WALK_BOTH
-        if (w0 && w1) {
-            // both halves walk the block: the four MFMAs back to back, so
-            // half 1's run on the matrix pipe while half 0's results are ORed
-            PROF_ADD(10, 2);
-            const f16x Ha0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B00, zero, 0, 0, 0);
-            const f16x Hb0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B10, zero, 0, 0, 0);
-            const f16x H0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B01, Ha0, 0, 0, 0);
-            const f16x H1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B11, Hb0, 0, 0, 0);
-            tile(H0, 0u);
-            tile(H1, 1u);
-            return;
-        }
-#endif
         // the two halves unrolled (no per-tile operand selects) but kept apart
-        // (sched_barrier): one tile's 16 result registers live at a time
+        // (sched_barrier): one tile's 16 result registers live at a time --
+        // both halves' four MFMAs back to back (half 1's on the matrix pipe
+        // while half 0's results are ORed) spilled 5 VGPRs and cost 5.3 %
+        // (profiles/r05/walk_both/)
         if (w0) {
             PROF_ADD(10, 1);  // tiles walked
             tile(mfma2(B00, B01), 0u);
