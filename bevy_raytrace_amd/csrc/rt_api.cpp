@@ -1434,14 +1434,16 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     K_.div_wrem = make_fastdiv(K_.tile_wrem ? K_.tile_wrem : 1);
     K_.prefetch = tn.prefetch ? 1u : 0u;
     // The rotation evens out the SIMD's age-ordered issue where the launch's
-    // drain is a large share (DESIGN.md 4.1 issue fairness); in launches of
-    // many samples per lane it costs more than it returns. Round 5, one box
-    // (profiles/r05/prio/): off vs on -- headline (10,125 samples per lane)
-    // -0.33 %, 4K (8,100) -0.5 %; the N = 8 shard (1,266) +0.7 %, 10k
-    // spheres (2,025) +0.8 %. By the call: on below 4,096 samples per lane.
+    // drain is a large share, or its items long (DESIGN.md 4.1 issue
+    // fairness); elsewhere it costs more than it returns. Round 5, one box
+    // (profiles/r05/prio/): off vs on -- headline (10,125 samples per lane,
+    // 64-sample pixel items) -0.33 %, 4K (8,100; 256) -0.5 %; the N = 8
+    // shard (1,266) +0.7 %, 10k spheres (2,025) +0.8 %, the 8K frame
+    // (129,600; 1,024-sample items) +1.4 %. By the call: on below 4,096
+    // samples per lane or above 256 samples per pixel.
     {
         const double spl = (double)npix * p.spp * nframes / (double)std::max<uint64_t>(lanes, 1);
-        K_.prio_mode = tn.prio_mode >= 0 ? (uint32_t)tn.prio_mode : (spl < 4096.0 ? 1u : 0u);
+        K_.prio_mode = tn.prio_mode >= 0 ? (uint32_t)tn.prio_mode : (spl < 4096.0 || p.spp > 256u ? 1u : 0u);
     }
     K_.prio_shift = tn.prio_shift;
     // wide (sphere-parallel) tracing pays ~32 VALU per 64 spheres per ray plus

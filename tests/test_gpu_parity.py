@@ -274,6 +274,35 @@ def test_item_order_identical(renderer, S, region, tail):
     check_exact(outs[1][0][1], ref)
 
 
+def test_schedule_knobs_identical(renderer):
+    """The launch-shape rules chosen by the call (round 5: the block region
+    by spp / depth, the s_setprio rotation by samples per lane) and their
+    knob overrides change only which lane runs which item and when: the
+    frames and segment counts are those of every other setting, and the
+    oracle's."""
+    import torch
+    sp, mt = arrays(scene.rtiow_final_scene())
+    cam = default_camera_block()
+    W, H, F, S = 72, 40, 3, 64
+    renderer.set_scene(sp, mt)
+    outs = []
+    for knobs in ({}, {"prio_mode": "0"}, {"prio_mode": "1"}, {"prio_mode": "3"},
+                  {"block_region": "128"}, {"block_region": "16", "prio_mode": "0"}):
+        renderer.tune(None)
+        if knobs:
+            renderer.tune(**knobs)
+        buf = torch.empty((F, H, W, 4), dtype=torch.float32, device="cuda")
+        renderer.render_frames_device(cam, F, buf.data_ptr(), W, H, S, 10, flags=NO_REUSE)
+        st = renderer.wait()
+        outs.append((buf.cpu().numpy(), st["segments"]))
+    renderer.tune(None)
+    for o in outs[1:]:
+        check_exact(o[0], outs[0][0])
+        assert o[1] == outs[0][1]
+    ref, segs = O.render(cam, sp, mt, W, H, S, 10, frame0=2 * S)
+    check_exact(outs[0][0][2], ref)
+
+
 @pytest.mark.parametrize("K,B", [(3, 5), (8, 1)])
 def test_image_out_shards_fill_one_image(renderer, K, B):
     """RT_FLAG_IMAGE_OUT: K row shards of a 2-frame launch write their rows

@@ -32,7 +32,7 @@ img = torch.empty((F, H, W, 4), dtype=torch.float32, device="cuda:0")
 s = torch.cuda.Stream()
 IMAGE = os.environ.get("PROBE_PACKED", "0") != "1"  # PROBE_PACKED=1: the shard's packed rows, plain stores
 FL = abi.RT_FLAG_NO_PRIMARY_CACHE | (abi.RT_FLAG_IMAGE_OUT if IMAGE else 0)
-for kv in filter(None, os.environ.get("PROBE_TUNE", "").split(",")):
+for kv in filter(None, os.environ.get("PROBE_TUNE", "").split(";")):  # knob=value;knob=value
     r.tune(*kv.split("=", 1))
 r.reserve(F, W, H, S, D, row_block=rb, shard_count=N, shard_index=K, flags=FL)
 
