@@ -70,6 +70,7 @@ struct Tuning {
     bool split_all = false;       // without primary reuse, every block as single samples
     bool tail_split = true;       // single-sample tail items at the end of a launch
     double tail[3] = {0.0, 1.0, 1.0};  // tail regions (4-, 2-, 1-sample items) x D x lanes
+    bool tail_auto = true;        // the tail by the call (knob tail sets it explicitly)
     double block_region = -1.0;   // single-block items before the tail, x D x lanes samples (-1: by spp / D)
     // KParams::item_order: pixel-major block / tail items (bit 0) and pixel
     // items (bit 1): a wave's lanes then share pixels, so its primary rays
@@ -258,6 +259,7 @@ static bool tune_set(Tuning& t, const char* name, const char* v) {
         if (sscanf(v, "%lf,%lf,%lf", &w[0], &w[1], &w[2]) != 3 || w[0] < 0 || w[1] < 0 || w[2] < 0)
             return false;
         for (int i = 0; i < 3; ++i) t.tail[i] = w[i];
+        t.tail_auto = false;
         return true;
     }
     if (!num(x)) return false;
@@ -1238,7 +1240,15 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     }
     const uint64_t lanes = (uint64_t)ctx->cu_count * wg_run * RT_BLOCK_THREADS;
     bool tail_on = tn.tail_split;
-    const double* ta = tn.tail;
+    // Launches with about one pixel per lane (the N = 8 row shard of the
+    // headline: 259,200 pixels, 262,144 lanes) end better with a 4-sample
+    // region before the 2-sample one and a shorter single-sample one: shard 7
+    // of 8, 20 frames, tail 0,1,1 -> 1,1,0.25: 26.09 -> 25.43 ms render; the
+    // N = 4 / 2 shards (0.5 / 0.25 lanes per pixel) and whole frames lose with
+    // it (+0.3 % / +0.6 %; headline 1,1,1 +0.4 %, 10k spheres +2.2 %;
+    // profiles/r05/tail/).
+    static const double tail_shard[3] = {1.0, 1.0, 0.25};
+    const double* ta = tn.tail_auto && npix && 4 * lanes >= 3 * npix ? tail_shard : tn.tail;
     auto per_px = [&](double a, uint64_t mult) -> uint64_t {
         if (!npix || a <= 0.0) return 0;
         const uint64_t v = (uint64_t)std::ceil(a * p.max_depth * (double)lanes / (double)npix);
