@@ -90,14 +90,20 @@ def kd_order(idx, c):
 
 order = np.concatenate([big, -np.ones((-len(big)) % 32, np.int64),
                         np.array(kd_order(small, sph[:, :3].astype(np.float64)))])
-CH = 512
+CH = int(os.environ.get("CH", "512"))  # walk positions per chunk bound (SUB: bounds per chunk)
+SUB = int(os.environ.get("SUB", "1"))
 bnd = []
 for b in range(0, len(order), CH):
-    idx = order[b:b + CH]
-    idx = idx[idx >= 0]
-    c, r = sph[idx, :3].astype(np.float64), np.abs(sph[idx, 3]).astype(np.float64)
-    C = (c.min(0) + c.max(0)) / 2
-    bnd.append((C, np.max(np.linalg.norm(c - C, axis=1) + r)))
+    sub = []
+    for q in range(SUB):
+        idx = order[b + q * CH // SUB:b + (q + 1) * CH // SUB]
+        idx = idx[idx >= 0]
+        if len(idx) == 0:
+            continue
+        c, r = sph[idx, :3].astype(np.float64), np.abs(sph[idx, 3]).astype(np.float64)
+        C = (c.min(0) + c.max(0)) / 2
+        sub.append((C, np.max(np.linalg.norm(c - C, axis=1) + r)))
+    bnd.append(sub)
 
 
 def tests(C, R, rays, tl):
@@ -126,10 +132,14 @@ for _t in range(trials):
         rays.append(segs[q][k])
         tl.append(t_large[q][k])
     rays, tl = np.array(rays), np.array(tl)
-    for b, (C, R) in enumerate(bnd):
-        a, s = tests(C, R, rays, tl)
-        cur[b] += a.any()
-        new[b] += s.any()
+    for b, sub in enumerate(bnd):
+        anyc = anys = False
+        for (C, R) in sub:
+            a, s_ = tests(C, R, rays, tl)
+            anyc |= a.any()
+            anys |= s_.any()
+        cur[b] += anyc
+        new[b] += anys
 print(f"chunks {len(bnd)}; passed per half-wave: line+forward {cur.sum() / trials:.2f}, "
       f"+ segment limit {new.sum() / trials:.2f}")
 print("per chunk (cur/new): " + " ".join(f"{c / trials:.2f}/{n / trials:.2f}" for c, n in zip(cur, new)))
