@@ -69,7 +69,10 @@ struct Tuning {
     size_t scratch_bytes = (size_t)16 << 30;  // block sums per launch (of 288 GB HBM)
     bool split_all = false;       // without primary reuse, every block as single samples
     bool tail_split = true;       // single-sample tail items at the end of a launch
-    double tail[3] = {0.0, 1.0, 1.0};  // tail regions (4-, 2-, 1-sample items) x D x lanes
+    // tail regions (4-, 2-, 1-sample items) x D x lanes. Round 5: 0, 1, 0.5
+    // against 0, 1, 1 (profiles/r05/tail/): headline -0.18 %, 10k spheres
+    // -1.9 %, 4K -0.1 %, the N = 4 / 2 row shards -0.75 / -0.2 %
+    double tail[3] = {0.0, 1.0, 0.5};
     bool tail_auto = true;        // the tail by the call (knob tail sets it explicitly)
     double block_region = -1.0;   // single-block items before the tail, x D x lanes samples (-1: by spp / D)
     // KParams::item_order: pixel-major block / tail items (bit 0) and pixel
@@ -1210,10 +1213,11 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     const size_t per_block = (size_t)npix * sizeof(float4);  // one slot per pixel
     // Tail: per lane ~a1*D single samples, and before them optionally a2*D
     // samples in 2-sample items and a4*D in 4-sample items (knob tail="a4,a2,a1";
-    // default 0,1,1 since the pixel-major item order, the measured best on
-    // the N=8 shards -- 31.4 vs 33.0 ms per 20-frame launch for 0,0,6 -- at
-    // the same full frame, profiles/r03/item_order/sweep_tail*.log; 0,0,6
-    // with the pair-major order, 0,0,12 before the matrix-core kernel): a
+    // default 0,1,0.5 since round 5 -- 0,1,1 from the pixel-major item order
+    // on, the measured best on the N=8 shards then (31.4 vs 33.0 ms per
+    // 20-frame launch for 0,0,6) at the same full frame,
+    // profiles/r03/item_order/sweep_tail*.log; 0,0,6 with the pair-major
+    // order, 0,0,12 before the matrix-core kernel; and by the call below): a
     // block item (<= 8*D iterations) taken before the tail has finished when
     // the queue runs dry, and an item taken in the tail leaves at most one
     // short path per lane to drain. In samples per pixel:
@@ -1245,8 +1249,8 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     // region before the 2-sample one and a shorter single-sample one: shard 7
     // of 8, 20 frames, tail 0,1,1 -> 1,1,0.25: 26.09 -> 25.43 ms render; the
     // N = 4 / 2 shards (0.5 / 0.25 lanes per pixel) and whole frames lose with
-    // it (+0.3 % / +0.6 %; headline 1,1,1 +0.4 %, 10k spheres +2.2 %;
-    // profiles/r05/tail/).
+    // it (N = 4: 1,1,0.25 +0.35 % against 0,1,0.5 -0.75 %; N = 2 1,1,0.5
+    // +0.6 %; headline 1,1,1 +0.4 %, 10k spheres +2.2 %; profiles/r05/tail/).
     static const double tail_shard[3] = {1.0, 1.0, 0.25};
     const double* ta = tn.tail_auto && npix && 4 * lanes >= 3 * npix ? tail_shard : tn.tail;
     auto per_px = [&](double a, uint64_t mult) -> uint64_t {
