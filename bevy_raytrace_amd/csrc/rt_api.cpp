@@ -546,7 +546,11 @@ static float round_up_f32(double v) {
 // the matrix-core walk (build_mfma): original indices, 0xFFFFFFFF for a pad
 // position; its length is a multiple of RT_GROUP. sph: (cx, cy, cz, r*r) f32
 // records and S their filter constants, in the original order, n records.
-// O(N log^2 N): a stable sort per k-d level.
+// O(N log N): per k-d level a selection (std::nth_element) of the cut along
+// the axis in the total order (centre coordinate, original index), leaves
+// sorted in the same order -- deterministic whatever the ties. (Round 4's
+// stable sort per level, O(N log^2 N): 36 ms for 10,000 spheres, 168 ms for
+// 65,536, on every rt_set_scene / rt_update_spheres.)
 static std::vector<uint32_t> spatial_order(const float4* sph, const float* S, uint32_t n) {
     auto finite_rec = [&](uint32_t i) {
         const float4 q = sph[i];
@@ -586,12 +590,18 @@ static std::vector<uint32_t> spatial_order(const float4* sph, const float* S, ui
         int ax = 0;
         for (int a = 1; a < 3; ++a)
             if (bhi[a] - blo[a] > bhi[ax] - blo[ax]) ax = a;
-        std::stable_sort(kd.begin() + b, kd.begin() + e,
-                         [&](uint32_t x, uint32_t y) { return centre(x, ax) < centre(y, ax); });
-        if (n2 <= RT_GROUP) return;
+        auto less = [&](uint32_t x, uint32_t y) {
+            const double cx = centre(x, ax), cy = centre(y, ax);
+            return cx < cy || (cx == cy && x < y);
+        };
+        if (n2 <= RT_GROUP) {  // a leaf: sorted along its longest axis
+            std::sort(kd.begin() + b, kd.begin() + e, less);
+            return;
+        }
         const size_t unit = n2 > 64 ? 64 : (n2 > 32 ? 32 : RT_GROUP);
         size_t cut = std::max(unit, (size_t)std::llround((double)n2 / 2.0 / (double)unit) * unit);
         if (cut >= n2) cut = (n2 / 2 + RT_GROUP - 1) / RT_GROUP * RT_GROUP;
+        std::nth_element(kd.begin() + b, kd.begin() + b + cut, kd.begin() + e, less);
         split(b, b + cut);
         split(b + cut, e);
     };
