@@ -42,26 +42,32 @@ def main():
     res = {"lib": os.path.relpath(LIB), "names": {str(k): v for k, v in NAMES.items()}, "runs": {}}
     r = Renderer(0, lib_path=LIB)
     for case in cases:
-        key, nf = case.split(":")
-        nf = int(nf)
+        # key:frames, or key:frames:N:k -- row shard k of N (the bench's row blocks)
+        parts = case.split(":")
+        key, nf = parts[0], int(parts[1])
+        nsh, ksh = (int(parts[2]), int(parts[3])) if len(parts) == 4 else (1, 0)
         wl = configs.WORKLOADS[key]
         sc = wl.make_scene()
         sp, mt = sc.objects_gpu(), sc.materials_gpu()
         r.set_scene(sp, mt)
         W, H, S, D = wl.width, wl.height, wl.spp, wl.max_depth
-        buf = torch.empty((nf, H, W, 4), dtype=torch.float32, device="cuda:0")
+        rb = configs.pick_row_block(H, nsh)
+        rows = len(abi.shard_rows(H, rb, nsh, ksh))
+        buf = torch.empty((nf, rows, W, 4), dtype=torch.float32, device="cuda:0")
         flags = abi.RT_FLAG_NO_PRIMARY_CACHE
         runs = []
         for rep in range(2):  # warm, then the recorded launch
             t0 = time.perf_counter()
-            r.render_frames_device(cam, nf, buf.data_ptr(), W, H, S, D, frame0=0, flags=flags)
+            r.render_frames_device(cam, nf, buf.data_ptr(), W, H, S, D, 0, rb, nsh, ksh, flags)
             st = r.wait()
             c = r.debug_counters()
             runs.append({"wall_s": time.perf_counter() - t0, "stats": st, "counters": c})
             print(f"{key} x{nf} rep {rep}: kernel {st['kernel_ms']:.1f} ms, "
                   f"iters {c[4]}, tiles {c[10]}, exact rounds {c[13]}", flush=True)
         last = runs[-1]
-        res["runs"][key] = {"frames": nf, "width": W, "height": H, "spp": S, "max_depth": D,
+        if nsh > 1:
+            key = f"{key}_shard{ksh}of{nsh}"
+        res["runs"][key] = {"frames": nf, "shard": [nsh, ksh], "width": W, "height": H, "spp": S, "max_depth": D,
                             "spheres": int(len(sp)), "stats": last["stats"],
                             "counters": {NAMES.get(i, f"c{i}"): int(v)
                                          for i, v in enumerate(last["counters"])},
