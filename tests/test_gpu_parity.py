@@ -318,6 +318,7 @@ def test_image_out_shards_fill_one_image(renderer, K, B):
     renderer.render_frames_device(cam, F, full.data_ptr(), W, H, S, D, flags=NO_REUSE)
     renderer.wait()
     img = torch.full((F, H, W, 4), -7.0, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()  # the fill (torch's stream) done before the library's stream writes
     for k in range(K):
         renderer.render_frames_device(cam, F, img.data_ptr(), W, H, S, D, row_block=B,
                                       shard_count=K, shard_index=k,
@@ -363,6 +364,8 @@ def test_shards_and_device_assembly(renderer, K, B):
         assert torch.equal(buf.cpu(), torch.from_numpy(part)) or np.array_equal(
             buf.cpu().numpy(), part, equal_nan=True)
     img = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+    # the library runs on its own stream: torch's writes of g must be done
+    torch.cuda.synchronize()
     renderer.assemble_shards(g.data_ptr(), mr, img.data_ptr(), W, H, B, K)
     torch.cuda.synchronize()
     check_exact(img.cpu().numpy(), full)
@@ -380,11 +383,15 @@ def test_assemble_shard_frames_matches_per_frame(renderer, K, B, H):
     mr = max(len(abi.shard_rows(H, B, K, k)) for k in range(K))
     g = torch.randn((K, F, mr, W, 4), dtype=torch.float32, device="cuda")
     img = torch.full((F, H, W, 4), -7.0, dtype=torch.float32, device="cuda")
+    # the library runs on its own stream (no stream argument): torch's writes
+    # of its inputs must be complete first (the bench passes its stream)
+    torch.cuda.synchronize()
     renderer.assemble_shard_frames(g.data_ptr(), mr, F, img.data_ptr(), W, H, B, K)
     lay = ShardLayout(H, B, K)
     for f in range(F):
         slabs = g[:, f].contiguous()
         one = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
         renderer.assemble_shards(slabs.data_ptr(), mr, one.data_ptr(), W, H, B, K)
         torch.cuda.synchronize()
         assert torch.equal(img[f], one)
@@ -661,6 +668,7 @@ def test_frames_batch_identical(renderer, flags, K, k, scratch):
     elif scratch == "pass":  # less than one frame: several passes per frame
         renderer.tune(scratch_bytes=rows * W * 16 * 9)
     out = torch.full((F, rows, W, 4), -1.0, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()  # the fill (torch's stream) done before the library's stream writes
     renderer.render_frames_device(cam, F, out.data_ptr(), W, H, S, D, frame0=f0, row_block=B,
                                   shard_count=K, shard_index=k, flags=flags)
     st = renderer.wait()
@@ -959,6 +967,7 @@ def test_direct_output_identical(renderer, S, F, flags):
     for direct in (0, 1):
         renderer.tune("direct_out", str(direct))
         out = torch.full((F, H, W, 4), -3.0, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()  # the fill (torch's stream) done before the library's stream writes
         renderer.render_frames_device(cam, F, out.data_ptr(), W, H, S, D, frame0=7, flags=flags)
         st = renderer.wait()
         outs.append((out.cpu().numpy(), st["segments"]))
@@ -1020,6 +1029,7 @@ def test_block_culled_walk_identical(renderer, which):
     for cull in (0, 1):
         renderer.tune("mf_cull", str(cull))
         out = torch.full((F, H, W, 4), -3.0, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()  # the fill (torch's stream) done before the library's stream writes
         renderer.render_frames_device(cam, F, out.data_ptr(), W, H, S, D, frame0=3, flags=NO_REUSE)
         st = renderer.wait()
         outs.append((out.cpu().numpy(), st["segments"]))
