@@ -173,8 +173,8 @@ typedef struct rt_params {
  * e.g. rank 0's buffer mapped into every rank (hipIpcOpenMemHandle), so the
  * row tiling needs no gather. The reference has no
  * counterpart (one device, ray_trace_node.rs:213-224). Visibility: the image
- * rows are written with system-scope write-through stores and every writing
- * wave ends with a system-scope release, so once the host has seen the call
+ * rows are written with system-scope write-through stores that every writing
+ * wave waits on before it ends (nothing is left in its L2), so once the host has seen the call
  * complete (rt_wait / a stream sync, then e.g. a process barrier) the device
  * that owns the image reads them after rt_acquire(). */
 #define RT_FLAG_IMAGE_OUT 0x20u
