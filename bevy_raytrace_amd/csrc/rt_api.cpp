@@ -172,6 +172,13 @@ struct rt_ctx {
     float4* d_mf_sph = nullptr;
     uint32_t* d_mf_perm = nullptr;
     size_t mfB_cap = 0, mf_sph_cap = 0, mf_perm_cap = 0;
+    // the shading records in the walk's order (2 float4 per walk position;
+    // the render shades by walk position, rt_dev_path.h) and original index
+    // -> walk position (the VALU and sphere-parallel walks' answers)
+    float4* d_mf_shd = nullptr;
+    uint32_t* d_mf_iperm = nullptr;
+    size_t mf_shd_cap = 0, mf_iperm_cap = 0;
+    std::vector<uint32_t> h_mf_perm;  // walk position -> original index (0xFFFFFFFF: pad)
 
     // frames in flight: RT_MAX_PENDING slots of per-frame work buffers, each
     // with its own stream, so frame i+1 can start while frame i drains
@@ -398,6 +405,8 @@ void rt_destroy(rt_ctx* ctx) {
     hipFree(ctx->d_mfB);
     hipFree(ctx->d_mf_sph);
     hipFree(ctx->d_mf_perm);
+    hipFree(ctx->d_mf_shd);
+    hipFree(ctx->d_mf_iperm);
     for (Frame& f : ctx->fr) {
         hipFree(f.d_block_sums);
         hipFree(f.d_acc);
@@ -462,6 +471,19 @@ static int upload_shd(rt_ctx* ctx, size_t first, size_t count) {
                            hipMemcpyHostToDevice));
     return RT_OK;
 }
+
+#ifdef RT_MFMA_FILTER
+// The shading records in the matrix-core walk's order (build_mfma; pads zero,
+// never shaded), from the host mirrors (quiesced).
+static int upload_shd_mf(rt_ctx* ctx) {
+    const std::vector<uint32_t>& perm = ctx->h_mf_perm;
+    std::vector<float4> rec(2 * perm.size(), make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    for (size_t p = 0; p < perm.size(); ++p)
+        if (perm[p] != 0xFFFFFFFFu) shade_records(&ctx->h_rm[perm[p]], 1, ctx->h_mats, &rec[2 * p]);
+    HIP_TRY(ctx, hipMemcpy(ctx->d_mf_shd, rec.data(), sizeof(float4) * rec.size(), hipMemcpyHostToDevice));
+    return RT_OK;
+}
+#endif
 
 // The exact sphere test's short correctly-rounded sqrt/divide forms (rt_math.h)
 // need their operands inside [2^-100, 2^100] / [2^-60, 2^60]. The kernel checks
@@ -992,12 +1014,27 @@ static int build_mfma(rt_ctx* ctx) {
     if (!rc) rc = ensure(ctx, &ctx->d_mfB, &ctx->mfB_cap, nchunk_max * RT_MF_BCHUNK * 16);
     if (!rc) rc = ensure(ctx, &ctx->d_mf_sph, &ctx->mf_sph_cap, (size_t)nblk_max * 32 * sizeof(float4));
     if (!rc) rc = ensure(ctx, &ctx->d_mf_perm, &ctx->mf_perm_cap, (size_t)nblk_max * 32 * sizeof(uint32_t));
+    if (!rc) rc = ensure(ctx, &ctx->d_mf_shd, &ctx->mf_shd_cap, (size_t)nblk_max * 32 * 2 * sizeof(float4));
+    if (!rc) rc = ensure(ctx, &ctx->d_mf_iperm, &ctx->mf_iperm_cap, (size_t)n * sizeof(uint32_t));
     if (rc) return rc;
     HIP_TRY(ctx, hipMemcpy(ctx->d_mfA, h.data(), h.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
     HIP_TRY(ctx, hipMemcpy(ctx->d_mfB, hb.data(), hb.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
     HIP_TRY(ctx, hipMemcpy(ctx->d_mf_sph, msph.data(), msph.size() * sizeof(float4), hipMemcpyHostToDevice));
     HIP_TRY(ctx, hipMemcpy(ctx->d_mf_perm, mperm.data(), mperm.size() * sizeof(uint32_t),
                            hipMemcpyHostToDevice));
+    {  // original index -> walk position, and the walk-order shading records
+        std::vector<uint32_t> iperm(n, 0u);
+        ctx->h_mf_perm.assign(npos, 0xFFFFFFFFu);
+        for (uint32_t p = 0; p < npos; ++p) {
+            const uint32_t i = perm_at(p);
+            ctx->h_mf_perm[p] = i;
+            if (i != 0xFFFFFFFFu) iperm[i] = p;
+        }
+        HIP_TRY(ctx, hipMemcpy(ctx->d_mf_iperm, iperm.data(), iperm.size() * sizeof(uint32_t),
+                               hipMemcpyHostToDevice));
+        rc = upload_shd_mf(ctx);
+        if (rc) return rc;
+    }
     ctx->mf_nblk = nblk;
     ctx->mf_top = top;
     ctx->mf_qs = (float)std::ldexp(1.0, sq);
@@ -1073,6 +1110,8 @@ static MfScene mf_scene(const rt_ctx* ctx) {
     mf.B = ctx->tune.mf_cull ? ctx->d_mfB : nullptr;
     mf.sph = ctx->d_mf_sph;
     mf.perm = ctx->d_mf_perm;
+    mf.shd = ctx->d_mf_shd;
+    mf.iperm = ctx->d_mf_iperm;
     mf.nblk = ctx->mf_nblk;
     mf.top = ctx->mf_top && ctx->tune.mf_top ? 1u : 0u;
     mf.qs = ctx->mf_qs;
@@ -1167,6 +1206,12 @@ int rt_update_materials(rt_ctx* ctx, uint32_t first, const rt_material* material
     // bounds do not change)
     rc = upload_shd(ctx, 0, ctx->h_rm.size());
     if (rc) return rc;
+#ifdef RT_MFMA_FILTER
+    if (ctx->mf_ok && !ctx->mf_dirty) {  // (a pending rebuild uploads them anyway)
+        rc = upload_shd_mf(ctx);
+        if (rc) return rc;
+    }
+#endif
     if (!ctx->cull_dirty) {
         rc = upload_shd_c(ctx);
         if (rc) {
@@ -1443,7 +1488,13 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     if (tn.chk_shrink == 5) K_.chk_nrm = 0;
     if (tn.chk_shrink == 7) K_.chk_slots = 0;
 #ifdef RT_MFMA_FILTER
-    if (!cull && ctx->mf_ok && !(p.flags & RT_FLAG_VALU_FILTER)) K_.mf = mf_scene(ctx);
+    if (!cull && ctx->mf_ok && !(p.flags & RT_FLAG_VALU_FILTER)) {
+        K_.mf = mf_scene(ctx);
+        K_.chk_wsph = (uint32_t)(ctx->mf_sph_cap / sizeof(float4));
+        K_.chk_wrm = (uint32_t)(ctx->mf_shd_cap / (2 * sizeof(float4)));
+        if (tn.chk_shrink == 4) K_.chk_wsph = 0;
+        if (tn.chk_shrink == 5) K_.chk_wrm = 0;
+    }
 #endif
     std::memcpy(K_.T, cam->transform, sizeof(K_.T));
     K_.tan_half = (float)std::tan((double)(cam->fov / 2.0f));                 // generate.wgsl:67

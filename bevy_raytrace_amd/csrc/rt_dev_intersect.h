@@ -914,7 +914,8 @@ __device__ __forceinline__ void tile_or(const f16x& H, int* gq, int& g) {
 // chunk-level code (rt_render_kernel; rt_render_multi_kernel takes the rest):
 // the loop's code in the single-chunk kernel cost its walk 2.2 % (register
 // allocation and placement, profiles/r05/bisect/).
-template <bool COUNT = false, bool SPH_LDS = false, bool MULTI = true, uint32_t CAP = RT_MF_CAP>
+template <bool COUNT = false, bool SPH_LDS = false, bool MULTI = true, uint32_t CAP = RT_MF_CAP,
+          bool ORIG = true>
 __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
                                                     uint32_t scene_fast, v3 o, v3 d, bool live,
                                                     uint64_t live_mask, float& t_out,
@@ -1356,8 +1357,9 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
     }
     PROF_MARK(1);
     drain(qcount(qp0, q0), qcount(qp1, q1));
-    // the walk position of the winner -> its original index
-    if (best_i >= 0) best_i = (int)mf.perm[RT_IDX((uint32_t)best_i, nblk * 32u, RT_SITE_PERM)];
+    // the walk position of the winner -> its original index (ORIG; the render
+    // shades by walk position: the records in the walk's order, MfScene)
+    if (ORIG && best_i >= 0) best_i = (int)mf.perm[RT_IDX((uint32_t)best_i, nblk * 32u, RT_SITE_PERM)];
     PROF_MARK(2);
 #ifdef RT_PROFILE
     {   // (diagnostic reductions: their time goes to c[26])

@@ -252,9 +252,13 @@ __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint
 //   select  : per-material arithmetic producing the vector to normalize
 //   post    : normalize(d) for the sky, the new direction otherwise
 // Every lane performs exactly the reference's op sequence for its case.
+// sph / shd: the exact-test records and the shading records in the index
+// space of hi (the original list, or the matrix-core walk's order with its
+// records in LDS or global memory: SP); nsph / nshd: their counts.
+template <typename SP>
 __device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, float t,
-                                      const float4* __restrict__ sph,
-                                      const float4* __restrict__ shd) {
+                                      SP sph, const float4* __restrict__ shd, uint32_t nsph,
+                                      uint32_t nshd) {
     const bool miss = hi < 0;
     if (!miss && st.bounce == P.max_depth - 1) {  // shade.wgsl:236-238
         st.color = mk(0.0f, 0.0f, 0.0f);
@@ -272,8 +276,8 @@ __device__ __forceinline__ bool shade(const KParams& P, PathState& st, int hi, f
         // the centre (exact-test record) and the shading record (radius, the
         // material's reflectance / fuzziness / index of refraction, colour):
         // three independent loads (rt_api.cpp shade_records)
-        const float4 s = sph[RT_IDX(hi, P.chk_nsph, RT_SITE_SPH)];
-        const uint32_t r = RT_IDX((uint32_t)hi, P.chk_nrm, RT_SITE_RM);
+        const float4 s = rec_load(sph, RT_IDX((uint32_t)hi, nsph, RT_SITE_SPH));
+        const uint32_t r = RT_IDX((uint32_t)hi, nshd, RT_SITE_RM);
         const float4 a = shd[2 * r];
         mc = shd[2 * r + 1];
         const float radius = a.x;

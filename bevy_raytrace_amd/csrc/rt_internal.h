@@ -73,6 +73,8 @@ struct MfScene {
     const uint4* B;         // null: every block is walked (knob mf_cull 0)
     const float4* sph;      // (cx, cy, cz, r^2) in the walk's order, nblk * 32 records
     const uint32_t* perm;   // walk position -> original sphere index
+    const float4* shd;      // shading records in the walk's order, 2 per position (render)
+    const uint32_t* iperm;  // original sphere index -> walk position
     uint32_t nblk;          // 32-sphere blocks (<= 2048)
     uint32_t top;           // 1: B holds one more chunk after the ceil(nblk / 16) of block
                             // bounds, the chunk-level bounds (row j = chunk j; 2..32 chunks)
@@ -161,6 +163,7 @@ struct KParams {
     // RT_IDX; the product build reads none of them).
     uint32_t chk_nsph;   // sph / grp records (padded list)
     uint32_t chk_nrm;    // shading records (2 float4 each)
+    uint32_t chk_wsph, chk_wrm;  // the same in the matrix-core walk's order (mf.sph, mf.shd)
     uint32_t chk_items;  // work items of the launch (main_all + tail_items)
     uint64_t chk_slots;  // block_sums slots
     uint64_t chk_out;    // float4 pixels behind the launch's output pointer

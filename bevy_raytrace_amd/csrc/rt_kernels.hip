@@ -312,6 +312,18 @@ __device__ __forceinline__ void render_body(
     const bool use_cache =
         (P.flags & (RT_FLAG_NO_PRIMARY_CACHE | RT_FLAG_JITTER | RT_FLAG_THIN_LENS)) == 0;
 
+    // Shading by walk position (round 5): with the matrix-core walk the hit
+    // is its walk position, shaded from the records in the walk's order
+    // (LDS in rt_render_kernel, MfScene.sph / .shd) -- no permutation load
+    // between the drain and the shading; the other walks' answers map
+    // through MfScene.iperm. Without it (the culled list, or no matrix-core
+    // scene) the original list.
+#ifdef RT_MFMA_FILTER
+    const bool widx = !CULL && P.mf.A != nullptr;
+#else
+    const bool widx = false;
+#endif
+    const uint32_t nsph_sh = widx ? P.chk_wsph : P.chk_nsph;  // (RT_IDX bounds)
     PathState st;
     bool has_item = false;
     uint32_t q_next = 0, q_end = 0;  // wave-uniform chunk of work items
@@ -462,9 +474,12 @@ __device__ __forceinline__ void render_body(
             PROF_ADD(20, 1);
             intersect_wide<CULL>(sph, P.nspheres, P.scene_fast, live, st.o, st.d, hi, t, P.perm);
 #ifdef RT_MFMA_FILTER
+            if (widx && hi >= 0) hi = (int)P.mf.iperm[hi];
+#endif
+#ifdef RT_MFMA_FILTER
         } else if (__builtin_expect(!CULL && P.mf.A && mfma_wave_ok(st.o, has_item), 1)) {  // the whole wave
             PROF_ADD(18, 1);
-            const int h2 = intersect_world_mfma<false, SPH_LDS, MULTI, MFCAP>(
+            const int h2 = intersect_world_mfma<false, SPH_LDS, MULTI, MFCAP, false>(
                 P.mf, P.scene_fast, st.o, st.d, has_item, live, t, cqm
 #ifdef RT_PROFILE
                 , prof_
@@ -480,6 +495,9 @@ __device__ __forceinline__ void render_body(
                                        prof_,
 #endif
                                        P.bnd, P.perm, P.nclusters, P.cull_supers != 0);
+#ifdef RT_MFMA_FILTER
+            if (widx && hi >= 0) hi = (int)P.mf.iperm[hi];
+#endif
         }
         traced = __builtin_amdgcn_readfirstlane(traced + (uint32_t)__popcll(live));
         if (use_cache && has_item && st.bounce == 0)  // the item's first sample: its primary hit
@@ -501,7 +519,12 @@ __device__ __forceinline__ void render_body(
             PROF_ADD(22, 1);  // shading rounds (wave-level)
             segs = __builtin_amdgcn_readfirstlane(segs + (uint32_t)__popcll(sh));
             if (shading) {
-                const bool done = shade(P, st, hi, t, sph, shd);
+                bool done;
+                if constexpr (SPH_LDS)  // (only with the matrix-core scene: rt_launch_render)
+                    done = shade(P, st, hi, t, (lds_cfloat4*)s_msph, P.mf.shd, P.chk_wsph, P.chk_wrm);
+                else
+                    done = shade(P, st, hi, t, widx ? P.mf.sph : sph, widx ? P.mf.shd : shd, nsph_sh,
+                                 widx ? P.chk_wrm : P.chk_nrm);
                 shading = false;
                 if (done) {
                     // path finished: accumulate (collect.wgsl:115-120, blocked);
@@ -560,7 +583,7 @@ __device__ __forceinline__ void render_body(
                         start_sample(P, st, lds);
                         if (use_cache) {
                             const float2 c = lds->cache;
-                            hi = (int)RT_IDX((uint32_t)(__float_as_int(c.x) + 1), P.chk_nsph + 1u,
+                            hi = (int)RT_IDX((uint32_t)(__float_as_int(c.x) + 1), nsph_sh + 1u,
                                              RT_SITE_CACHE) - 1;
                             t = c.y;
                             shading = true;
@@ -907,7 +930,7 @@ hipError_t rt_launch_render(const KParams* P, const float4* grp, const float4* s
         hipLaunchKernelGGL(rt_render_cull_kernel, dim3(grid), dim3(RT_BLOCK_THREADS), dyn, stream,
                            *P, grp, sph, shd, reinterpret_cast<const PixelEntry*>(pd),
                            block_sums, work_counter, seg_counter, seg_counter + 2);
-    else if (P->mf.A && P->mf.nblk > 16u)  // more than one bound chunk
+    else if (!P->mf.A || P->mf.nblk > 16u)  // more than one bound chunk, or no matrix-core walk
         hipLaunchKernelGGL(rt_render_multi_kernel, dim3(grid), dim3(RT_BLOCK_THREADS), dyn, stream, *P,
                            grp, sph, shd, reinterpret_cast<const PixelEntry*>(pd),
                            block_sums, work_counter, seg_counter, seg_counter + 2);
