@@ -76,6 +76,10 @@ struct Tuning {
     bool tail_auto = true;        // the tail by the call (knob tail sets it explicitly)
     double block_region = -1.0;   // single-block items before the tail, x D x lanes samples (-1: by spp / D)
     bool block_align = true;      // the pixel region ends at a frame boundary (block_pairs)
+    // lead items: every frame past the pixel region starts with one pixel item
+    // of its first block_lead blocks (one slot instead of block_lead); 0 = off,
+    // -1 = by the call (regions below)
+    int32_t block_lead = -1;
     // KParams::item_order: pixel-major block / tail items (bit 0) and pixel
     // items (bit 1): a wave's lanes then share pixels, so its primary rays
     // (and first-bounce origins) coincide -- warm 20-frame launches, one box
@@ -289,6 +293,9 @@ static bool tune_set(Tuning& t, const char* name, const char* v) {
         t.pix_group = (uint32_t)x;
     } else if (!strcmp(name, "block_align")) {
         t.block_align = x != 0;
+    } else if (!strcmp(name, "block_lead")) {
+        if (x < -1 || x > 64) return false;
+        t.block_lead = (int32_t)x;
     } else if (!strcmp(name, "block_region")) {
         if (x < 0) return false;
         t.block_region = x;
@@ -1372,13 +1379,42 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     // slots per pixel of a launch of F frames x blocks [bb, bb + nb): one per
     // frame with pixel-item blocks (its lane-folded sum), one per block item,
     // one per tail sample
+    // The main part's item regions: pixel items for the frames with pairs
+    // below qpix (fp of them) and, with lead items (knob block_lead, m < nb),
+    // one more pixel item per frame past them that has main pairs (fl - fp
+    // frames), covering its first min(m, its main pairs) blocks, dealt after
+    // the pixel items; block items for the other pairs in [qpix, qmain) --
+    // nreg per pixel. Lead items cut the slots the block region writes and the
+    // collect reads; by the call m = 2 where a pixel region exists (fp > 0).
+    // Measured, same box, against no lead items (profiles/r05/block_lead/):
+    // headline render-kernel writes 1.43 -> 1.36 GB per 20-frame launch at
+    // +0.1 % cycles (m = 3: 1.29 GB, +0.2 %; 4: 1.22, +0.2-0.6 %; 5: 1.15,
+    // +2.4 %); the N = 8 row shard -1.5 % render; 4K unchanged (one frame per
+    // launch: no frame past the pixel region). Without a pixel region (10k
+    // spheres' two-frame launches: block items only) every frame would get
+    // one, +0.5-2.5 %: off there.
+    struct Regions {
+        uint64_t fp, fl, lead, nreg;
+    };
+    auto regions = [&](uint64_t qmain, uint64_t qpix, uint64_t nb) -> Regions {
+        Regions r{(qpix + nb - 1) / nb, 0, 0, qmain - qpix};
+        r.fl = r.fp;
+        const uint64_t m = tn.block_lead >= 0 ? (uint64_t)tn.block_lead : (r.fp ? 2u : 0u);
+        if (m && m < nb) {
+            r.lead = m;
+            for (uint64_t f = r.fp; f * nb < qmain; ++f, ++r.fl)
+                r.nreg -= std::min<uint64_t>(r.lead, qmain - f * nb);
+        }
+        return r;
+    };
     auto launch_slots = [&](uint64_t F, uint64_t nb, uint64_t bb) -> uint64_t {
         const uint64_t pairs = F * nb, L = tail_pairs(pairs);
         const uint64_t qmain = pairs - L, qpix = qmain - block_pairs(qmain, nb);
         const uint64_t g_end = (F - 1) * p.spp +
                                std::min<uint64_t>(p.spp, (bb + nb) * RT_SAMPLE_BLOCK);
         const uint64_t g0 = L ? pair_g(pairs - L, nb, bb) : g_end;
-        return (qpix + nb - 1) / nb + (qmain - qpix) + (g_end - g0);
+        const Regions rg = regions(qmain, qpix, nb);
+        return rg.fl + rg.nreg + (g_end - g0);
     };
     if (npix) {
         uint64_t slots_cap = tn.scratch_bytes / per_block;
@@ -1582,8 +1618,15 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         const uint64_t g0 = L ? pair_g(pairs - L, ps.nblocks, ps.block_begin) : g_end;
         K_.qmain = (uint32_t)(pairs - L);
         K_.qpix = K_.qmain - (uint32_t)block_pairs(K_.qmain, ps.nblocks);
-        K_.main_pix = (K_.qpix + ps.nblocks - 1) / ps.nblocks * npix;  // (frame, pixel) items
-        K_.main_all = K_.main_pix + (K_.qmain - K_.qpix) * npix;         // + (pair, pixel) items
+        const Regions rg = regions(K_.qmain, K_.qpix, ps.nblocks);
+        K_.fp = (uint32_t)rg.fp;
+        K_.lead = (uint32_t)rg.lead;
+        K_.c0 = (uint32_t)(rg.fp * ps.nblocks - K_.qpix);
+        K_.div_nbl = make_fastdiv(ps.nblocks - K_.lead);
+        K_.main_pix = (uint32_t)rg.fl * npix;                     // (frame, pixel) items
+        K_.main_fp = (uint32_t)rg.fp * npix;  // lead items after them
+        K_.div_nlead = make_fastdiv(rg.fl > rg.fp ? (uint32_t)(rg.fl - rg.fp) : 1u);
+        K_.main_all = K_.main_pix + (uint32_t)rg.nreg * npix;     // + (pair, pixel) items
         // tail regions from the end: single samples, 2-sample, 4-sample items
         const uint64_t g2 = g_end - std::min<uint64_t>(A1, g_end - g0);
         const uint64_t g1 = g2 - std::min<uint64_t>(A2, g2 - g0);
@@ -1596,10 +1639,11 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         K_.tail_items = K_.ti2 + (uint32_t)((g_end - g2) * npix);
         // grouped order (bit 2) needs whole groups of 8 pixels; else pixel-major
         K_.pix_group_shift = tn.pix_group == 4 ? 2u : 3u;
+        K_.lead_group_shift = (tn.item_order & 4u) && npix % tn.pix_group == 0 ? K_.pix_group_shift : 0u;
         K_.item_order = (tn.item_order & 4u) && npix % tn.pix_group != 0 ? (tn.item_order & 3u) | 3u
                                                                         : tn.item_order;
-        K_.div_nreg = make_fastdiv(K_.qmain > K_.qpix ? K_.qmain - K_.qpix : 1u);
-        K_.div_nfpix = make_fastdiv(npix && K_.main_pix ? K_.main_pix / npix : 1u);
+        K_.div_nreg = make_fastdiv(rg.nreg ? (uint32_t)rg.nreg : 1u);
+        K_.div_nfpix = make_fastdiv(rg.fp ? (uint32_t)rg.fp : 1u);  // frames with pixel pairs
         K_.div_ng4 = make_fastdiv(g1 > g0 ? (uint32_t)((g1 - g0 + 3) / 4) : 1u);
         K_.div_ng2 = make_fastdiv(g2 > g1 ? (uint32_t)((g2 - g1 + 1) / 2) : 1u);
         K_.div_ng1 = make_fastdiv(g_end > g2 ? (uint32_t)(g_end - g2) : 1u);
@@ -2055,7 +2099,7 @@ int rt_debug_intersect_tiles(const rt_ctx* ctx, uint64_t* out2) {
 // Internal (not in include/rt_hip.h): set one A/B or fault-injection knob of
 // ctx (struct Tuning above; names: scratch_bytes, split_all, tail_split, tail
 // "a4,a2,a1", prefetch, prio_mode, prio_shift, wg_per_cu, wide_max,
-// fast_exact, fail_alloc_after, block_region, block_align, chk_shrink, direct_out). name == NULL restores every default. Used by
+// fast_exact, fail_alloc_after, block_region, block_align, block_lead, chk_shrink, direct_out). name == NULL restores every default. Used by
 // the tests and tools/ only; the product path never calls it.
 int rt_debug_tune(rt_ctx* ctx, const char* name, const char* value) {
     if (!ctx) return RT_ERR_INVALID_ARG;

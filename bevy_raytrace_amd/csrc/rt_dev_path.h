@@ -112,7 +112,10 @@ struct PixelEntry {
 // once, at slot f*npix + k. Pairs [qpix, qmain) as block items (item <
 // main_all): one block of one pixel, its sum stored at slot main_pix +
 // r*npix + k (r = q - qpix) -- short items at the end of the main part, so
-// no lane holds a long pixel item when the queue runs dry. A tail item is
+// no lane holds a long pixel item when the queue runs dry. With lead items
+// (P.lead > 0, knob block_lead) every frame f >= fp with main pairs also has
+// a pixel item, of its first min(lead, ...) blocks, and the block items are
+// the other pairs, r counting them in pair order. A tail item is
 // z = 4, 2 or 1 consecutive samples of one pixel, each sample's colour
 // stored on its own. item_order picks the item -> (frame / pair / group,
 // pixel) map: pixel-major (bits 0, 1) puts one pixel's items back to back;
@@ -155,19 +158,23 @@ __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint
         uint32_t f, b0, b1;  // frame, the item's blocks [b0, b1) (pass-relative)
         float4 a0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (item < main_pix) {
-            if (RT_GROUPED_ON && (P.item_order & 4u)) {  // grouped: 8 pixels' frames, frame-major in the group
+            if (item >= P.main_fp) {  // lead items: after the pixel items, own order
+                grouped_split(item - P.main_fp, P.div_nlead, P.lead_group_shift, f, k);
+                f += P.fp;
+                slot = f * npix + k;
+            } else if (RT_GROUPED_ON && (P.item_order & 4u)) {  // grouped: 8 pixels' frames, frame-major in the group
                 grouped_split(item, P.div_nfpix, P.pix_group_shift, f, k);
                 slot = f * npix + k;
             } else if (P.item_order & 2u) {  // pixel-major: one pixel's frames back to back
                 k = fdiv(item, P.div_nfpix);
-                f = item - k * (main_pix / npix);
+                f = item - k * P.div_nfpix.d;
                 slot = f * npix + k;
             } else {
                 f = fdiv(item, P.div_npix);
                 k = item - f * npix;
             }
             b0 = 0;
-            b1 = min(nblocks, qpix - f * nblocks);
+            b1 = f < P.fp ? min(nblocks, qpix - f * nblocks) : min(P.lead, P.qmain - f * nblocks);
             whole = f < P.dfull;
             // a later pass over the frame's blocks (frames above the scratch
             // budget) continues the fold of the earlier passes (rt_collect_kernel
@@ -184,15 +191,22 @@ __device__ __forceinline__ void start_item(const KParams& P, PathState& st, uint
                 slot = main_pix + r * npix + k;
             } else if (P.item_order & 1u) {  // pixel-major: one pixel's pairs back to back
                 k = fdiv(j, P.div_nreg);
-                r = j - k * (P.qmain - qpix);
+                r = j - k * P.div_nreg.d;
                 slot = main_pix + r * npix + k;
             } else {
                 r = fdiv(j, P.div_npix);
                 k = j - r * npix;
             }
-            const uint32_t q = qpix + r;
-            f = fdiv(q, P.div_nblocks);
-            b0 = q - f * nblocks;
+            // pair order: the pixel region's last frame's c0 pairs, then
+            // nblocks - lead per frame (lead items take the first lead)
+            if (r < P.c0) {
+                f = P.fp - 1u;
+                b0 = qpix + r - f * nblocks;
+            } else {
+                const uint32_t r1 = r - P.c0, fr = fdiv(r1, P.div_nbl);
+                f = P.fp + fr;
+                b0 = P.lead + (r1 - fr * P.div_nbl.d);
+            }
             b1 = b0 + 1;
             whole = P.dwhole_blk != 0;
         }
@@ -364,7 +378,9 @@ __device__ __forceinline__ void fold_frame(const KParams& P, uint32_t f, uint32_
                                            float& ax, float& ay, float& az, LD ld) {
     const uint32_t q0 = f * P.nblocks;
     auto blocks_below = [&](uint32_t q) { return q > q0 ? min(P.nblocks, q - q0) : 0u; };
-    const uint32_t bp = blocks_below(P.qpix), bm = blocks_below(P.qmain);
+    // frames past the pixel pairs (f >= fp): their lead item's blocks
+    const bool lf = f >= P.fp;
+    const uint32_t bm = blocks_below(P.qmain), bp = lf ? min(P.lead, bm) : blocks_below(P.qpix);
     auto fold = [&](float vx, float vy, float vz) {
         if (have) {
             ax = ax + vx; ay = ay + vy; az = az + vz;
@@ -379,7 +395,8 @@ __device__ __forceinline__ void fold_frame(const KParams& P, uint32_t f, uint32_
         have = true;
     }
     for (uint32_t b = bp; b < bm; ++b) {  // block items
-        const float4 v = ld((size_t)P.main_pix + (size_t)(q0 + b - P.qpix) * P.npix + k);
+        const uint32_t r = lf ? P.c0 + (f - P.fp) * P.div_nbl.d + (b - P.lead) : q0 + b - P.qpix;
+        const float4 v = ld((size_t)P.main_pix + (size_t)r * P.npix + k);
         fold(v.x, v.y, v.z);
     }
     for (uint32_t b = bm; b < P.nblocks; ++b) {  // tail blocks: their samples' colours

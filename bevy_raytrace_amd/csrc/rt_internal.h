@@ -107,6 +107,18 @@ struct KParams {
     // rt_collect_kernel folds them per pixel in block / sample order.
     uint32_t nframes, sample_base, qmain, main_all;
     uint32_t qpix, main_pix;
+    // lead items (knob block_lead): frames f >= fp (past the pixel pairs) with
+    // main pairs get one pixel item of their first min(lead, ...) blocks, in
+    // [0, main_pix) too; the block items are then the other pairs in
+    // [qpix, qmain), in pair order: c0 = fp*nblocks - qpix of the pixel
+    // region's last frame, then nblocks - lead per later frame (div_nbl)
+    uint32_t fp, lead, c0;
+    FastDiv div_nbl;
+    // the lead items' place: items [main_fp = fp*npix, main_pix) after the
+    // pixel items, grouped by 2^lead_group_shift pixels (0: pixel-major),
+    // frame-major in the group (div_nlead: by the fl - fp lead frames)
+    uint32_t main_fp, lead_group_shift;
+    FastDiv div_nlead;
     uint32_t g0, g1, g2, g_end;
     uint32_t ti1, ti2, tail_items;  // tail item offsets of the 2- and 1-sample regions, count
     FastDiv div_nblocks;
@@ -153,8 +165,8 @@ struct KParams {
     // the group (rt_dev_path.h grouped_split)
     uint32_t item_order;
     uint32_t pix_group_shift;  // grouped order (bit 2): log2 of the pixel group (2 or 3)
-    FastDiv div_nfpix; // by main_pix / npix (frames with pixel items)
-    FastDiv div_nreg;  // by qmain - qpix (pairs of the block-item region)
+    FastDiv div_nfpix; // by fp (frames with pixel pairs; main_fp / npix)
+    FastDiv div_nreg;  // by the block items per pixel (qmain - qpix without lead items)
     // by the sample groups per pixel of the tail regions: (g1 - g0 + 3) / 4,
     // (g2 - g1 + 1) / 2, g_end - g2 (4-, 2-, 1-sample items)
     FastDiv div_ng4, div_ng2, div_ng1;

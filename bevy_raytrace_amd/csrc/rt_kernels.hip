@@ -810,10 +810,11 @@ __global__ __launch_bounds__(RT_BLOCK_THREADS) void rt_intersect_mfma_kernel(
 // pass, write out = acc / spp with alpha 1 (collect.wgsl:115-125). One thread
 // per pixel of the processing order k (-> image pixel p = order_to_pixel).
 // Launch frame f = blockIdx.y, its blocks in order: those of its pixel item
-// (pairs q = f*nblocks + b < qpix), already folded by the lane that traced them
-// (first block as is -- or acc + it on a later pass -- then acc + block sum)
-// at slot f*npix + k; then its block items (qpix <= q < qmain), each sum at
-// main_pix + (q - qpix)*npix + k; then its tail blocks, whose samples' colours
+// (pairs q = f*nblocks + b < qpix, or a later frame's first `lead` blocks),
+// already folded by the lane that traced them (first block as is -- or acc +
+// it on a later pass -- then acc + block sum) at slot f*npix + k; then its
+// block items (the other pairs below qmain), each sum at main_pix + r*npix + k
+// (r: the pair's rank among them, rt_dev_path.h fold_frame); then its tail blocks, whose samples' colours
 // sit at main_all + (g - g0)*npix + k (g = f*spp + s), summed here exactly as
 // a lane sums a block, ((0 + c0) + c1) + ..., in sample order. Each is folded
 // as the lane folds (first as is, then acc + it).

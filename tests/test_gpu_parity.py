@@ -277,7 +277,8 @@ def test_item_order_identical(renderer, S, region, tail):
 def test_schedule_knobs_identical(renderer):
     """The launch-shape rules chosen by the call (round 5: the block region
     by spp / depth and aligned to a frame boundary, the s_setprio rotation by
-    samples per lane) and their
+    samples per lane, lead items -- block_lead, with and without a partial
+    pixel-region frame and with several launches per call) and their
     knob overrides change only which lane runs which item and when: the
     frames and segment counts are those of every other setting, and the
     oracle's."""
@@ -289,7 +290,10 @@ def test_schedule_knobs_identical(renderer):
     outs = []
     for knobs in ({}, {"prio_mode": "0"}, {"prio_mode": "1"}, {"prio_mode": "3"},
                   {"block_region": "128"}, {"block_region": "16", "prio_mode": "0"},
-                  {"block_align": "0"}, {"block_align": "0", "block_region": "40"}):
+                  {"block_align": "0"}, {"block_align": "0", "block_region": "40"},
+                  {"block_lead": "0"}, {"block_lead": "4"}, {"block_lead": "3", "block_region": "16"},
+                  {"block_lead": "2", "block_align": "0", "block_region": "40"},
+                  {"block_lead": "2", "scratch_bytes": str(W * H * 16 * 6)}):
         renderer.tune(None)
         if knobs:
             renderer.tune(**knobs)
