@@ -431,6 +431,38 @@ def test_full_1080p64_properties(renderer):
     assert nan_px.sum() < 200
 
 
+def test_full_1080p64_lead_items(renderer):
+    """Lead items by the call at full size: a 3-frame 1080p/64 launch has a
+    pixel region (frame 0) and two frames past it (block region 64 x depth
+    samples per lane, rt_api.cpp regions: fp = 1, each later frame's first 2
+    blocks one item). Frames and segment counts identical to the plan
+    without lead items (block_lead=0) and sampled rows of the lead frames
+    bit-exact against the oracle."""
+    import torch
+    sp, mt = arrays(scene.rtiow_final_scene())
+    cam = default_camera_block()
+    renderer.set_scene(sp, mt)
+    W, H, S, D, F = 1920, 1080, 64, 16, 3
+    outs = []
+    for knobs in ({}, {"block_lead": "0"}):
+        renderer.tune(None)
+        if knobs:
+            renderer.tune(**knobs)
+        buf = torch.empty((F, H, W, 4), dtype=torch.float32, device="cuda")
+        renderer.render_frames_device(cam, F, buf.data_ptr(), W, H, S, D)
+        st = renderer.wait()
+        torch.cuda.synchronize()
+        outs.append((buf.cpu().numpy(), st["segments"]))
+        del buf
+    renderer.tune(None)
+    check_exact(outs[0][0], outs[1][0])
+    assert outs[0][1] == outs[1][1]
+    rows = [0, 415, 540, 1079]
+    for f in (1, 2):
+        ref, _ = O.render_rows(cam, sp, mt, W, H, S, D, rows, frame0=f * S)
+        check_exact(outs[0][0][f][rows], ref)
+
+
 def test_4k_sampled_rows(renderer):
     """BASELINE config 3 (4K, 256 spp, depth 32): 64 rows spread over the
     frame bit-exact against the oracle."""
