@@ -278,7 +278,8 @@ def test_schedule_knobs_identical(renderer):
     """The launch-shape rules chosen by the call (round 5: the block region
     by spp / depth and aligned to a frame boundary, the s_setprio rotation by
     samples per lane, lead items -- block_lead, with and without a partial
-    pixel-region frame and with several launches per call) and their
+    pixel-region frame and with several launches per call; the regions made
+    to exist at this size by a short tail) and their
     knob overrides change only which lane runs which item and when: the
     frames and segment counts are those of every other setting, and the
     oracle's."""
@@ -288,12 +289,22 @@ def test_schedule_knobs_identical(renderer):
     W, H, F, S = 72, 40, 3, 64
     renderer.set_scene(sp, mt)
     outs = []
+    # At this size the default tail covers the whole launch (every pair a tail
+    # sample); with a short tail (T) the main part's regions exist, and the
+    # block region picks them (tests/test_plan_model.py: 0.3 -> pixel
+    # frames 0-1, a lead item in frame 2; 0.55 unaligned -> frame 0 partial,
+    # lead items in frames 1-2)
+    T = "0,0,0.01"
     for knobs in ({}, {"prio_mode": "0"}, {"prio_mode": "1"}, {"prio_mode": "3"},
                   {"block_region": "128"}, {"block_region": "16", "prio_mode": "0"},
-                  {"block_align": "0"}, {"block_align": "0", "block_region": "40"},
-                  {"block_lead": "0"}, {"block_lead": "4"}, {"block_lead": "3", "block_region": "16"},
-                  {"block_lead": "2", "block_align": "0", "block_region": "40"},
-                  {"block_lead": "2", "scratch_bytes": str(W * H * 16 * 6)}):
+                  {"block_align": "0"}, {"tail": T}, {"tail": T, "block_region": "128"},
+                  {"tail": T, "block_region": "0.3"}, {"tail": T, "block_region": "0.3", "prio_mode": "0"},
+                  {"tail": T, "block_region": "0.3", "block_lead": "0"},
+                  {"tail": T, "block_region": "0.3", "block_lead": "4"},
+                  {"tail": T, "block_region": "0.55", "block_align": "0"},
+                  {"tail": T, "block_region": "0.55", "block_align": "0", "block_lead": "3"},
+                  {"tail": T, "block_lead": "2", "scratch_bytes": str(W * H * 16 * 6)},
+                  {"tail": T, "block_region": "0.3", "scratch_bytes": str(W * H * 16 * 12)}):
         renderer.tune(None)
         if knobs:
             renderer.tune(**knobs)

@@ -106,3 +106,36 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def host_plan(npix, spp, depth, nframes, lanes, tail=(0.0, 1.0, 0.5), block_region=None,
+              block_align=True, block_lead=-1, sample_block=8):
+    """rt_api.cpp enqueue's plan for a one-pass launch (no scratch limit):
+    -> dict(qmain, qpix, fp, fl, lead, nreg, c0)."""
+    import math
+    nb = (spp + sample_block - 1) // sample_block
+
+    def per_px(a, mult):
+        if a <= 0:
+            return 0
+        v = math.ceil(a * depth * lanes / npix)
+        return (v + mult - 1) // mult * mult
+
+    A4, A2, A1 = per_px(tail[0], 4), per_px(tail[1], 2), per_px(tail[2], 1)
+    pairs = nframes * nb
+    L = (A4 + A2 + A1 + sample_block - 1) // sample_block
+    L = 1 if L < 1 else min(L, pairs)
+    qmain = pairs - L
+    a8 = block_region if block_region is not None else min(128.0, max(64.0, 16.0 * spp / depth))
+    Q = (per_px(a8, 1) + sample_block - 1) // sample_block
+    if Q >= qmain:
+        Q = qmain
+    elif block_align and nb > 1:
+        qa = (qmain - Q + nb - 1) // nb * nb
+        if qa < qmain and 4 * (qmain - qa) >= 3 * Q:
+            Q = qmain - qa
+    qpix = qmain - Q
+    fp = (qpix + nb - 1) // nb
+    m = block_lead if block_lead >= 0 else (2 if fp else 0)
+    fp_, fl, lead, nreg, c0 = plan(nframes, nb, qpix, qmain, m)
+    return dict(qmain=qmain, qpix=qpix, fp=fp_, fl=fl, lead=lead, nreg=nreg, c0=c0)
