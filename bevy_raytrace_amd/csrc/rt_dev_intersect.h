@@ -1102,7 +1102,9 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
         }
         // one bound chunk's tiles: per half the 32-bit mask of its rows some
         // ray of the half passes
-        auto bound_tiles = [&](uint32_t* mk2) {
+        // (hook: called once the tile's last MFMAs have been issued, so the
+        // next chunk's rows can load into bq while this chunk's ORs run)
+        auto bound_tiles = [&](uint32_t* mk2, auto&& hook) {
             h8v F0, F1;
             h4v F2;
             __builtin_memcpy(&F0, &bq0, 16);
@@ -1114,6 +1116,7 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
                     t ? B11 : B01, F1, __builtin_amdgcn_mfma_f32_32x32x16_f16(t ? B10 : B00, F0, zero, 0, 0, 0),
                     0, 0, 0);
                 const f16x U = __builtin_amdgcn_mfma_f32_32x32x8f16(t ? G1 : G0, F2, zero, 0, 0, 0);
+                if (t == 1) hook();
                 const uint32_t acc = tile_or_fwd(V, U);
                 const uint64_t bm = rt_ballot((int)acc < 0);
                 mk2[t] = (uint32_t)bm | (uint32_t)(bm >> 32);
@@ -1131,7 +1134,7 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
         };
         if constexpr (!MULTI) {  // one bound chunk, preloaded: lane 0's masks
             uint32_t mk2[2];
-            bound_tiles(mk2);
+            bound_tiles(mk2, [] {});
             if (lane == 0u) {
                 mv0 = fold(mk2[0]);
                 mv1 = fold(mk2[1]);
@@ -1141,32 +1144,54 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
         const bool top = mf.top != 0u;
         uint32_t top2[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};  // chunks some ray of each half passes near
         if (top) {
-            bound_tiles(top2);  // the preloaded chunk-level fragments
+            bound_tiles(top2, [] {});  // the preloaded chunk-level fragments
             PROF_ADD(27, 1);    // chunk-level bound tiles (2 halves x 3 MFMAs)
         }
-        for (uint32_t k = 0; k < nbchunk; ++k) {
-            // (with chunk bounds, at most 32 chunks: k < 32)
-            if (top && (((top2[0] | top2[1]) >> (k & 31u)) & 1u) == 0u) continue;
-            // chunk 0's fragments were loaded first (without chunk bounds); a
-            // later chunk's load here (no prefetch: its registers would spill,
-            // and up to 512 spheres have one chunk)
-            if (k != 0u || top) {
-                // the chunk's base an opaque SGPR pair: the loads take the
-                // scalar-base form with a 32-bit lane offset, not three
-                // per-lane 64-bit pointers stepped through the loop
-                const uint4* pb = mf.B + (size_t)RT_IDX(k, nbchunk, RT_SITE_MF_BOUND) * RT_MF_BCHUNK;
+        // one bound chunk's rows into bq: the chunk's base an opaque SGPR
+        // pair, so the loads take the scalar-base form with a 32-bit lane
+        // offset, not three per-lane 64-bit pointers stepped through the loop
+        auto chunk_load = [&](uint32_t k) {
+            const uint4* pb = mf.B + (size_t)RT_IDX(k, nbchunk, RT_SITE_MF_BOUND) * RT_MF_BCHUNK;
 #ifndef RT_CHUNK_LSR
-                asm volatile("" : "+s"(pb));
-                const uint32_t l = opaque_lane();
+            asm volatile("" : "+s"(pb));
+            const uint32_t l = opaque_lane();
 #else  // (A/B builds only: the loads as hipcc strength-reduces them)
-                const uint32_t l = lane;
+            const uint32_t l = lane;
 #endif
-                bq0 = pb[l];
-                bq1 = pb[64u + l];
-                bq2 = reinterpret_cast<const uint2*>(pb)[256u + l];
+            bq0 = pb[l];
+            bq1 = pb[64u + l];
+            bq2 = reinterpret_cast<const uint2*>(pb)[256u + l];
+        };
+        // The bound chunks to test, in order: with chunk bounds those some
+        // half passes near (at most 32 chunks), else all (chunk 0 preloaded).
+        // Software-pipelined: the next chunk's rows load into bq as soon as
+        // the current chunk's last MFMAs have read them (bound_tiles' hook;
+        // no extra registers, so no spills), and the L2 round trip overlaps
+        // this chunk's ORs, ballots and folds; the last chunk reloads itself
+        // (an L1 hit), so every load stays unconditional and hipcc's vmcnt
+        // waits count exactly.
+        uint32_t cm = top ? (top2[0] | top2[1]) : 0u;  // (top) chunks not yet taken
+        uint32_t k = 0;
+        bool any = nbchunk != 0u;
+        if (top) {
+            any = cm != 0u;
+            k = any ? (uint32_t)__builtin_ctz(cm) : 0u;
+            cm &= cm - 1u;
+            if (any) chunk_load(k);
+        }
+        while (any) {
+            bool more;
+            uint32_t kn;
+            if (top) {
+                more = cm != 0u;
+                kn = more ? (uint32_t)__builtin_ctz(cm) : k;
+                cm &= cm - 1u;
+            } else {
+                more = k + 1u < nbchunk;
+                kn = more ? k + 1u : k;
             }
             uint32_t mk2[2];
-            bound_tiles(mk2);
+            bound_tiles(mk2, [&] { chunk_load(kn); });
             if (top) {  // a half that passes no ray near the chunk gets none of its blocks
                 mk2[0] = ((top2[0] >> k) & 1u) ? mk2[0] : 0u;
                 mk2[1] = ((top2[1] >> k) & 1u) ? mk2[1] : 0u;
@@ -1178,6 +1203,8 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
                 mv1 |= f1;
             }
             PROF_ADD(17, 1);  // bound chunks: 2 halves x (2 MFMA 32x32x16 + 1 MFMA 32x32x8)
+            k = kn;
+            any = more;
         }
         }  // MULTI
     }
