@@ -73,7 +73,6 @@ struct Tuning {
     // against 0, 1, 1 (profiles/r05/tail/): headline -0.18 %, 10k spheres
     // -1.9 %, 4K -0.1 %, the N = 4 / 2 row shards -0.75 / -0.2 %
     double tail[3] = {0.0, 1.0, 0.5};
-    bool tail_auto = true;        // the tail by the call (knob tail sets it explicitly)
     double block_region = -1.0;   // single-block items before the tail, x D x lanes samples (-1: by spp / D)
     bool block_align = true;      // the pixel region ends at a frame boundary (block_pairs)
     // lead items: every frame past the pixel region starts with one pixel item
@@ -274,7 +273,6 @@ static bool tune_set(Tuning& t, const char* name, const char* v) {
         if (sscanf(v, "%lf,%lf,%lf", &w[0], &w[1], &w[2]) != 3 || w[0] < 0 || w[1] < 0 || w[2] < 0)
             return false;
         for (int i = 0; i < 3; ++i) t.tail[i] = w[i];
-        t.tail_auto = false;
         return true;
     }
     if (!num(x)) return false;
@@ -1309,15 +1307,12 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     }
     const uint64_t lanes = (uint64_t)ctx->cu_count * wg_run * RT_BLOCK_THREADS;
     bool tail_on = tn.tail_split;
-    // Launches with about one pixel per lane (the N = 8 row shard of the
-    // headline: 259,200 pixels, 262,144 lanes) end better with a 4-sample
-    // region before the 2-sample one and a shorter single-sample one: shard 7
-    // of 8, 20 frames, tail 0,1,1 -> 1,1,0.25: 26.09 -> 25.43 ms render; the
-    // N = 4 / 2 shards (0.5 / 0.25 lanes per pixel) and whole frames lose with
-    // it (N = 4: 1,1,0.25 +0.35 % against 0,1,0.5 -0.75 %; N = 2 1,1,0.5
-    // +0.6 %; headline 1,1,1 +0.4 %, 10k spheres +2.2 %; profiles/r05/tail/).
-    static const double tail_shard[3] = {1.0, 1.0, 0.25};
-    const double* ta = tn.tail_auto && npix && 4 * lanes >= 3 * npix ? tail_shard : tn.tail;
+    // One tail for every launch. (Launches with about one pixel per lane, the
+    // N = 8 row shard of the headline, took 1, 1, 0.25 from the first tail
+    // sweep of round 5 -- 26.09 -> 25.43 ms against 0, 1, 1; profiles/r05/tail/
+    // -- until the lead items and end-of-launch chunks of 32 items: then
+    // 0, 1, 0.5 measured 24.80 ms against 24.98, profiles/r05/tail/call52/.)
+    const double* ta = tn.tail;
     auto per_px = [&](double a, uint64_t mult) -> uint64_t {
         if (!npix || a <= 0.0) return 0;
         const uint64_t v = (uint64_t)std::ceil(a * p.max_depth * (double)lanes / (double)npix);
