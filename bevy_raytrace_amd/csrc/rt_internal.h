@@ -13,7 +13,8 @@
 #ifndef RT_WAVE_CHUNK_TAIL
 // ... in the last 2 x 64 x waves items of the queue. Round 5, same box
 // against 16 (profiles/r05/chunk_tail/): the N = 8 row shard -0.6 / -0.75 %
-// (two calls), headline and 4K within +-0.1 %, 10k spheres +0.1 % (noise);
+// (two calls), the N = 4 / 2 shards -0.25 % (c54), headline and 4K within
+// +-0.1 %, 10k spheres +0.1 % (noise);
 // 4 / 8 slower (shard +1.9 / +0.3 %, headline +0.4 / +0.2 %), 64: shard
 // -0.4 %, headline -0.2 %, 10k +1 %
 #define RT_WAVE_CHUNK_TAIL 32
