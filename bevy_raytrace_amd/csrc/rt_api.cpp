@@ -93,6 +93,7 @@ struct Tuning {
     uint32_t pix_group = 4;       // item_order bit 2: pixels per group (4 or 8)
     bool prefetch = true;         // waves prefetch their next work chunk
     int32_t prio_mode = -1;       // s_setprio rotation: 0 off, 1 by iteration, 3 by wall time (-1: by the call)
+    int32_t wave_chunk = -1;      // work items per atomic before the launch's tail (-1: RT_WAVE_CHUNK)
     uint32_t prio_shift = 14;     // mode 3 step: 2^prio_shift ticks of 10 ns
     uint32_t wg_per_cu = 0;       // resident workgroups per CU (0 = by the call's size, enqueue)
     int64_t wide_max = -1;        // sphere-parallel threshold (-1 = cost model)
@@ -299,6 +300,9 @@ static bool tune_set(Tuning& t, const char* name, const char* v) {
         t.block_region = x;
     } else if (!strcmp(name, "prefetch")) {
         t.prefetch = x != 0;
+    } else if (!strcmp(name, "wave_chunk")) {
+        if (x != -1 && (x < 16 || x > 1024)) return false;
+        t.wave_chunk = (int32_t)x;
     } else if (!strcmp(name, "prio_mode")) {
         t.prio_mode = (int32_t)x;
     } else if (!strcmp(name, "prio_shift")) {
@@ -1643,10 +1647,15 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         K_.div_ng2 = make_fastdiv(g2 > g1 ? (uint32_t)((g2 - g1 + 1) / 2) : 1u);
         K_.div_ng1 = make_fastdiv(g_end > g2 ? (uint32_t)(g_end - g2) : 1u);
         const uint64_t items = (uint64_t)K_.main_all + K_.tail_items;
-        const uint64_t chunks = (items + RT_WAVE_CHUNK - 1) / RT_WAVE_CHUNK;
+        // Work chunk per atomic: 64 items (knob wave_chunk). 128 measured, same
+        // box: headline -1.7 % but spread 437-448 Mcycles against 449.1-449.9,
+        // 4K +15 %, 10k spheres +6 %, the N = 8 shard +8-18 %: a wave holding
+        // a larger chunk ends later (profiles/r05/wave_chunk/).
+        K_.chunk = tn.wave_chunk > 0 ? (uint32_t)tn.wave_chunk : (uint32_t)RT_WAVE_CHUNK;
+        const uint64_t chunks = (items + K_.chunk - 1) / K_.chunk;
         const uint64_t need_blocks = (chunks + (RT_BLOCK_THREADS / 64) - 1) / (RT_BLOCK_THREADS / 64);
         const uint32_t grid = (uint32_t)(need_blocks < grid_full ? need_blocks : grid_full);
-        const uint64_t tail_items = 2ull * RT_WAVE_CHUNK * grid * (RT_BLOCK_THREADS / 64);
+        const uint64_t tail_items = 2ull * K_.chunk * grid * (RT_BLOCK_THREADS / 64);
         K_.tail_start = (uint32_t)(items > tail_items ? items - tail_items : 0);
         K_.chk_items = (uint32_t)items;
         K_.chk_out = tn.chk_shrink == 16 ? 0 : (uint64_t)ps.nframes * fstride;
@@ -2094,7 +2103,7 @@ int rt_debug_intersect_tiles(const rt_ctx* ctx, uint64_t* out2) {
 // Internal (not in include/rt_hip.h): set one A/B or fault-injection knob of
 // ctx (struct Tuning above; names: scratch_bytes, split_all, tail_split, tail
 // "a4,a2,a1", prefetch, prio_mode, prio_shift, wg_per_cu, wide_max,
-// fast_exact, fail_alloc_after, block_region, block_align, block_lead, chk_shrink, direct_out). name == NULL restores every default. Used by
+// fast_exact, fail_alloc_after, block_region, block_align, block_lead, wave_chunk, chk_shrink, direct_out). name == NULL restores every default. Used by
 // the tests and tools/ only; the product path never calls it.
 int rt_debug_tune(rt_ctx* ctx, const char* name, const char* value) {
     if (!ctx) return RT_ERR_INVALID_ARG;

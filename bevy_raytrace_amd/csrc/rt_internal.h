@@ -140,6 +140,7 @@ struct KParams {
     float coc;             // lens_focal_length / (2 * fstop), generate.wgsl:97 (thin-lens flag)
     FastDiv div_npix, div_width, div_row_block;
     uint32_t tail_start;   // queue position from which waves take RT_WAVE_CHUNK_TAIL items
+    uint32_t chunk;        // items a wave takes per atomic before tail_start (rt_api.cpp: by the call)
     // processing order of a pass's pixels: tile_h x tile_w tiles (rows of
     // tiles, each tile row-major inside), then the rows % tile_h leftover rows
     // row-major (rt_dev_path.h order_to_pixel)

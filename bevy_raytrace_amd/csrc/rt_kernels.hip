@@ -356,7 +356,7 @@ __device__ __forceinline__ void render_body(
                     chunk = pref_chunk;
                     base = pref;
                 } else {
-                    chunk = q_end >= P.tail_start ? RT_WAVE_CHUNK_TAIL : RT_WAVE_CHUNK;
+                    chunk = q_end >= P.tail_start ? RT_WAVE_CHUNK_TAIL : P.chunk;
                     if (lane == 0) base = atomicAdd(work_counter, chunk);
                 }
                 base = __builtin_amdgcn_readlane(base, 0);
@@ -378,7 +378,7 @@ __device__ __forceinline__ void render_body(
                 }
 #endif
                 if (P.prefetch) {
-                    pref_chunk = q_end >= P.tail_start ? RT_WAVE_CHUNK_TAIL : RT_WAVE_CHUNK;
+                    pref_chunk = q_end >= P.tail_start ? RT_WAVE_CHUNK_TAIL : P.chunk;
                     if (lane == 0) pref = atomicAdd(work_counter, pref_chunk);
                 }
             }

@@ -304,7 +304,8 @@ def test_schedule_knobs_identical(renderer):
                   {"tail": T, "block_region": "0.55", "block_align": "0"},
                   {"tail": T, "block_region": "0.55", "block_align": "0", "block_lead": "3"},
                   {"tail": T, "block_lead": "2", "scratch_bytes": str(W * H * 16 * 6)},
-                  {"tail": T, "block_region": "0.3", "scratch_bytes": str(W * H * 16 * 12)}):
+                  {"tail": T, "block_region": "0.3", "scratch_bytes": str(W * H * 16 * 12)},
+                  {"wave_chunk": "16"}, {"tail": T, "block_region": "0.3", "wave_chunk": "128"}):
         renderer.tune(None)
         if knobs:
             renderer.tune(**knobs)
