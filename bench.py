@@ -24,8 +24,8 @@ the render kernel's issue cycles per launch, MEASURED from the rocprofv3 PMC
 record of the workload (profiles/pmc_traffic.json, tools/pmc_summary.py):
 4 x (SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2) -- the quad-cycles the VALU
 issue port was held, gfx950's dual-issued pairs counted once -- + 4 x
-SQ_INSTS_MFMA (an MFMA holds the issue 8 cycles), scaled to this run's launch
-(per frame, and per pixel at N > 1), over that launch's duration (HIP events
+SQ_INSTS_MFMA (an MFMA holds the issue 8 cycles), scaled per frame to this
+run's launch, over that launch's duration (HIP events
 on the stream the kernel runs on), against 1024 SIMDs x this run's own shader
 clock (rt_stats.clock_ghz, measured inside the timed launches); the line's
 `formula` and `peak_formula` fields say the same. The metric's fp32 roofline
@@ -33,6 +33,16 @@ clock (rt_stats.clock_ghz, measured inside the timed launches); the line's
 as `fp32_algorithm_ratio`: the kernel runs the brute-force walk's filter as
 f16 MFMA tiles and the exact fp32 test only on candidates, so that ratio
 exceeds 1. Matrix pipe, VALU busy and HBM traffic come from the same record.
+At N > 1 a rank renders a row shard, for which no PMC record exists: its issue
+cycles and traffic are the whole-frame record scaled by the rank's pixel share
+-- a MODEL, not a measurement, and the line says so
+(`roofline.record_scaled_by_pixel_share`, `roofline.modelled`).
+
+N > 1 self-check: after the timed region rank 0 re-renders the first, middle
+and last row of every rank's shard of the timed frame on its own GPU and
+compares them bit for bit with the rows the ranks delivered into its image
+(`cross_rank_check`, `ranks.cross_rank_rows_bit_exact`); a mismatch exits
+non-zero. `ranks.peer_access` records hipDeviceCanAccessPeer per rank pair.
 
 cpu_baseline: the C oracle (oracle/, a scalar port of the WGSL) timed on this
 host on a bounded row sample of the same frame, rank 0 at N=1 only.
@@ -83,6 +93,14 @@ def parse():
                          "mapping fails on any rank")
     ap.add_argument("--check", action="store_true",
                     help="add a checksum of the assembled frames to the JSON line")
+    ap.add_argument("--no-cross-check", action="store_true",
+                    help="N>1: skip the cross-rank row check (by default rank 0 re-renders the "
+                         "first, middle and last row of every rank's shard of the timed run's "
+                         "frame and compares them bit for bit with its image; a mismatch "
+                         "exits non-zero)")
+    ap.add_argument("--debug-skip-collect-rank", type=int, default=-1, metavar="K",
+                    help="fault injection: rank K's calls write no output (knob skip_collect), "
+                         "so its rows in rank 0's image stay stale; the cross-rank check must fail")
     ap.add_argument("--force-dist", action="store_true",
                     help="take the N>1 path (process group, shard gather, assembly) "
                          "even at world size 1")
@@ -404,6 +422,18 @@ def main():
     r = Renderer(local, lib_path=args.lib)
     for kv in args.tune:
         r.tune(*kv.split("=", 1))
+    if rank == args.debug_skip_collect_rank:
+        r.tune("skip_collect", 1)
+    # every rank's device and whether it can reach every other rank's device
+    # (hipDeviceCanAccessPeer; None = the same device, a one-GPU rehearsal)
+    peer_access = None
+    if dist_on:
+        from bevy_raytrace_amd import distributed as rdist
+        devs = [None] * world
+        dist.all_gather_object(devs, local)
+        mine = [rdist.can_access_peer(local, d) for d in devs]
+        peer_access = [None] * world
+        dist.all_gather_object(peer_access, mine)
     r.set_scene(spheres, mats)
     # work buffers of the largest launch this run makes, allocated before any
     # step (rt_reserve) so no allocation lands inside a timed region
@@ -422,14 +452,14 @@ def main():
              if rank == 0 else None)
     # N>1: rank 0's image mapped into every rank, unless the
     # mapping fails on some rank (then every rank takes the gather path)
-    use_ipc, img_ptr, ipc_map = False, None, None
+    use_ipc, img_ptr, ipc_map, ipc_errors = False, None, None, None
     if dist_on and args.gather in ("auto", "ipc"):
-        from bevy_raytrace_amd import distributed as rdist
-        blob = None
+        blob, err = None, None
         if rank == 0:
             try:
                 blob = rdist.ipc_export(image.data_ptr())
             except Exception as e:  # noqa: BLE001 -- reported, then the gather path
+                err = f"export: {e}"
                 print(f"bench.py: IPC export failed: {e}", file=sys.stderr)
         objs = [blob]
         dist.broadcast_object_list(objs, src=0)
@@ -440,11 +470,14 @@ def main():
             try:
                 ipc_map, img_ptr = rdist.ipc_import(objs[0])
             except Exception as e:  # noqa: BLE001
+                err = f"open: {e}"
                 print(f"bench.py: IPC import failed on rank {rank}: {e}", file=sys.stderr)
                 ok = False
-        flag = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=red_dev)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        use_ipc = float(flag.item()) == 1.0
+        # every rank's outcome (and error text) reaches rank 0's line
+        res = [None] * world
+        dist.all_gather_object(res, (ok, err))
+        use_ipc = all(o for o, _ in res)
+        ipc_errors = {str(k): e for k, (_, e) in enumerate(res) if e}
         if not use_ipc:
             if ipc_map is not None:
                 rdist.ipc_close(ipc_map)
@@ -556,7 +589,7 @@ def main():
     # the timed headline run's first frame of its last launch, kept for the
     # parity check below before the reuse / cull runs overwrite the buffer
     head_idx = args.steps - sizes[-1]
-    head_frame = image[0].clone() if (rank == 0 and world == 1) else None
+    head_frame = image[0].clone() if rank == 0 else None
     # --check: the headline run's last launch's frames, hashed now (the reuse
     # and cull runs below render into the same buffer from frame 0 on)
     check = None
@@ -564,6 +597,11 @@ def main():
         import hashlib
         check = {f"frame{head_idx + i}": hashlib.sha1(image[i].cpu().numpy().tobytes()).hexdigest()[:16]
                  for i in range(sizes[-1])}
+    if dist_on:
+        # on the IPC path the other ranks' next launch writes into rank 0's
+        # image: none starts before rank 0 has copied (and hashed) the frames
+        torch.cuda.synchronize()
+        dist.barrier()
     segs_local = sum(s["segments"] for s in stats)
     traced_local = sum(s["traced_segments"] for s in stats)
     kms = [s["kernel_ms"] for s in stats]
@@ -592,6 +630,8 @@ def main():
                     "call_ms": [round(float(p[2].item()), 3) for p in parts],
                     "wall_ms": [round(float(p[4].item()), 3) for p in parts],
                     "segments": [int(p[1].item()) for p in parts],
+                    "peer_access": peer_access,
+                    "ipc_errors": ipc_errors,
                     "note": ("render_ms: the rank's render kernels; transfer_ms: ipc -- its library "
                              "calls beyond the render (pixel table + collect writing its rows into "
                              "rank 0's image), rccl/gloo -- the gather + re-assembly; wall_ms: the "
@@ -660,7 +700,9 @@ def main():
 
     roofline = simd_issue_roofline(pmc, fpl_eff, kms_launch, clock_run)
     if px_share < 1.0:
+        # no PMC record of a row shard: the whole frame's, scaled (a model)
         roofline["record_scaled_by_pixel_share"] = round(px_share, 6)
+        roofline["modelled"] = True
     roofline.update({
         "executed": executed_report(load_executed(wl.key), fpl_eff),
         "traffic": traffic,
@@ -720,6 +762,16 @@ def main():
 
     if check is not None:
         out["check"] = check
+    rc = 0
+    if dist_on and not args.no_cross_check:
+        out["cross_rank_check"] = cross_rank_check(r, cam, W, H, S, D, B, world, head_idx,
+                                                   head_frame, NO_REUSE, stream,
+                                                   "ipc" if use_ipc else "gather")
+        out["ranks"]["cross_rank_rows_bit_exact"] = out["cross_rank_check"]["bit_exact"]
+        if not out["cross_rank_check"]["bit_exact"]:
+            print("bench.py: cross-rank check FAILED: rows %s differ from rank 0's image"
+                  % out["cross_rank_check"]["mismatched"], file=sys.stderr)
+            rc = 4
     if args.tune:
         out["tune"] = args.tune
     if args.lib:
@@ -742,6 +794,37 @@ def main():
     os.write(json_fd, (json.dumps(out) + "\n").encode())
     if dist_on:
         dist.destroy_process_group()
+    return rc
+
+
+def cross_rank_check(r, cam, W, H, S, D, B, world, head_idx, head_frame, flags, stream, path):
+    """N>1 self-check of the image path: rank 0 re-renders on its own GPU the
+    first, middle and last row owned by every rank (row y alone = shard y of H
+    with one-row blocks) of the timed run's frame `head_idx` and compares them
+    bit for bit (NaN payloads included) with the rows the ranks delivered into
+    its image -- through HIP IPC after rt_acquire, or the RCCL gather after the
+    re-assembly. A stale or torn row from any rank shows as a mismatch."""
+    import torch
+    from bevy_raytrace_amd import distributed as rdist
+    rows = [abi.shard_rows(H, B, world, k) for k in range(world)]
+    picks = rdist.check_rows(rows)
+    buf = torch.empty((1, W, 4), dtype=torch.float32, device="cuda")
+    bad = []
+    t0 = time.perf_counter()
+    for k, y in picks:
+        r.render_device(cam, buf.data_ptr(), W, H, S, D, head_idx * S, 1, H, y, flags,
+                        stream=stream.cuda_stream)
+        r.wait()
+        ndiff = int((buf[0].view(torch.int32) != head_frame[y].view(torch.int32)).any(-1).sum().item())
+        if ndiff:
+            bad.append([k, y, ndiff])
+    return {"bit_exact": not bad, "path": path, "frame": head_idx,
+            "rows_checked": len(picks), "ranks_covered": len({k for k, _ in picks}),
+            "rows": [[k, y] for k, y in picks], "mismatched": bad,
+            "check_s": round(time.perf_counter() - t0, 3),
+            "note": "rank 0 re-renders the first, middle and last row of every rank's shard of "
+                    "the timed run's first frame of its last launch and compares the bits with "
+                    "its image; mismatched = [rank, row, differing pixels]"}
 
 
 def cpu_quota():
@@ -798,4 +881,4 @@ def cpu_baseline(cam, spheres, mats, W, H, S, D, nrows, head_frame, head_idx, gp
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -190,6 +190,9 @@ def load(path=None):
     if hasattr(lib, "rt_debug_math"):  # internal diagnostic symbol (tests/test_gpu_math.py)
         lib.rt_debug_math.restype = ctypes.c_int
         lib.rt_debug_math.argtypes = [ctypes.c_int, _VP, ctypes.c_uint32, _VP]
+    if hasattr(lib, "rt_debug_mfma_acc"):  # internal (tests/test_gpu_mfma_acc.py)
+        lib.rt_debug_mfma_acc.restype = ctypes.c_int
+        lib.rt_debug_mfma_acc.argtypes = [_VP, _VP, _VP, ctypes.c_uint32]
     if hasattr(lib, "rt_debug_counters"):  # internal diagnostic symbol
         lib.rt_debug_counters.restype = ctypes.c_int
         lib.rt_debug_counters.argtypes = [_VP, ctypes.POINTER(ctypes.c_uint64)]

@@ -121,6 +121,11 @@ struct Tuning {
     // an N = 8 shard's 20-frame call 2.3 ms (2.51 -> 0.18 ms beyond the
     // render, profiles/r05/split/); on: A/B only.
     bool dsys_release = false;
+    // fault injection (bench.py --debug-skip-collect-rank): the call writes no
+    // output at all -- no direct output, no collect -- so the frame's pixels
+    // keep whatever the buffer held, the stale rows a lost hand-off would
+    // leave; the N>1 cross-rank check must catch them. Not a same-bits knob.
+    bool skip_collect = false;
 };
 
 struct rt_ctx {
@@ -323,6 +328,8 @@ static bool tune_set(Tuning& t, const char* name, const char* v) {
         t.mf_top = x != 0;
     } else if (!strcmp(name, "dsys_release")) {
         t.dsys_release = x != 0;
+    } else if (!strcmp(name, "skip_collect")) {
+        t.skip_collect = x != 0;
     } else if (!strcmp(name, "chk_shrink")) {
         if (x != 0 && x != 4 && x != 5 && x != 7 && x != 16) return false;
         t.chk_shrink = (uint32_t)x;
@@ -1509,7 +1516,7 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     // took 2.8 ms of kernel instead of 0.77, profiles/r04/direct/)
     K_.dsys = (p.flags & RT_FLAG_IMAGE_OUT) ? 1u : 0u;
     K_.dsys_release = tn.dsys_release ? 1u : 0u;
-    const bool direct = tn.direct_out && prog_mode == 0 && !passes.empty() && !K_.dsys &&
+    const bool direct = tn.direct_out && !tn.skip_collect && prog_mode == 0 && !passes.empty() && !K_.dsys &&
                         passes[0].block_begin == 0 && passes[0].nblocks == blocks_total &&
                         (K == 1 || (p.flags & RT_FLAG_IMAGE_OUT));
     K_.dstride = (uint32_t)fstride;
@@ -1693,9 +1700,10 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         HIP_TRY_Q(hipEventRecord(f.ev[2 * i + 1], stream));
         const bool first_pass = ps.block_begin == 0;
         const bool last_pass = ps.block_begin + ps.nblocks == blocks_total;
-        HIP_TRY_Q(rt_launch_collect(&K_, f.d_block_sums, f.d_acc, first_pass, last_pass,
-                                       (float)p.spp, d_out + (size_t)ps.frame_begin * fstride,
-                                       ctx->d_prog, prog_mode, prog_total, stream));
+        if (!tn.skip_collect)
+            HIP_TRY_Q(rt_launch_collect(&K_, f.d_block_sums, f.d_acc, first_pass, last_pass,
+                                           (float)p.spp, d_out + (size_t)ps.frame_begin * fstride,
+                                           ctx->d_prog, prog_mode, prog_total, stream));
     }
     HIP_TRY_Q(hipMemcpyAsync(f.h_segs, f.d_counters, RT_CNT_U64 * sizeof(unsigned long long),
                                 hipMemcpyDeviceToHost, stream));
@@ -2103,7 +2111,7 @@ int rt_debug_intersect_tiles(const rt_ctx* ctx, uint64_t* out2) {
 // Internal (not in include/rt_hip.h): set one A/B or fault-injection knob of
 // ctx (struct Tuning above; names: scratch_bytes, split_all, tail_split, tail
 // "a4,a2,a1", prefetch, prio_mode, prio_shift, wg_per_cu, wide_max,
-// fast_exact, fail_alloc_after, block_region, block_align, block_lead, wave_chunk, chk_shrink, direct_out). name == NULL restores every default. Used by
+// fast_exact, fail_alloc_after, block_region, block_align, block_lead, wave_chunk, chk_shrink, direct_out, skip_collect). name == NULL restores every default. Used by
 // the tests and tools/ only; the product path never calls it.
 int rt_debug_tune(rt_ctx* ctx, const char* name, const char* value) {
     if (!ctx) return RT_ERR_INVALID_ARG;

@@ -12,7 +12,7 @@
 // (frame, pixel), covering the frame's sample blocks of RT_SAMPLE_BLOCK
 // samples in the region, folded in block order in LDS), then *block items*
 // (pixel, one block), then *tail items* (2-sample, then single-sample; knob
-// `tail`, default 0,1,1), so no lane holds a long item when the queue runs
+// `tail`, default 0,1,0.5), so no lane holds a long item when the queue runs
 // dry. Waves take chunks of items with one atomic (prefetched a chunk ahead);
 // a lane whose path ends starts the next sample of its item, a lane whose item
 // ends stores its slot (through a per-wave LDS buffer) and takes the next
@@ -521,7 +521,9 @@ __device__ __forceinline__ void render_body(
             if (shading) {
                 bool done;
                 if constexpr (SPH_LDS)  // (only with the matrix-core scene: rt_launch_render)
-                    done = shade(P, st, hi, t, (lds_cfloat4*)s_msph, P.mf.shd, P.chk_wsph, P.chk_wrm);
+                    done = shade(P, st, hi, t, (lds_cfloat4*)s_msph, P.mf.shd,
+                                 P.chk_wsph < RT_MF_SPH_LDS_MAX ? P.chk_wsph : RT_MF_SPH_LDS_MAX,
+                                 P.chk_wrm);  // (the checked build's bound: the LDS array's)
                 else
                     done = shade(P, st, hi, t, widx ? P.mf.sph : sph, widx ? P.mf.shd : shd, nsph_sh,
                                  widx ? P.chk_wrm : P.chk_nrm);
@@ -1066,6 +1068,49 @@ int rt_debug_math(int mode, const float* in_device, uint32_t n, float* out_devic
                        out_device);
     return hipDeviceSynchronize() == hipSuccess ? 0 : -3;
 }
+
+// Diagnostic entry (not part of include/rt_hip.h; tests/test_gpu_mfma_acc.py):
+// the matrix-core filter's accumulation, the one hardware property its margin
+// proof assumes rather than derives (rt_dev_intersect.h above RT_MF_MU: at
+// most one rounding of <= 2^-24 |running sum| per added term, 33 over the two
+// chained MFMAs). Per 32 x 32 tile, the walk's own chain -- D = mfma(A1, B1,
+// mfma(A0, B0, 0)), v_mfma_f32_32x32x16_f16 twice, K 0..15 then 16..31 --
+// built with the product's flags. A: 32 rows x 32 K, B: 32 K x 32 columns,
+// f16 bits row-major per tile; D: 32 x 32 f32 row-major. One wave per tile.
+#ifdef RT_MFMA_FILTER
+__global__ void __launch_bounds__(64) rt_mfma_acc_kernel(const uint16_t* __restrict__ A,
+                                                         const uint16_t* __restrict__ B,
+                                                         float* __restrict__ D, uint32_t ntiles) {
+    const uint32_t l = threadIdx.x, t = blockIdx.x;
+    if (t >= ntiles) return;
+    const uint16_t* a = A + (size_t)t * 1024;
+    const uint16_t* b = B + (size_t)t * 1024;
+    h8v a0, a1, b0, b1;
+    for (int i = 0; i < 8; ++i) {  // lane l: row / column l & 31, K 8 (l >> 5) + i of each group
+        const uint32_t k = 8 * (l >> 5) + i;
+        a0[i] = __builtin_bit_cast(_Float16, a[(l & 31) * 32 + k]);
+        a1[i] = __builtin_bit_cast(_Float16, a[(l & 31) * 32 + 16 + k]);
+        b0[i] = __builtin_bit_cast(_Float16, b[k * 32 + (l & 31)]);
+        b1[i] = __builtin_bit_cast(_Float16, b[(16 + k) * 32 + (l & 31)]);
+    }
+    const f16x zero = {};
+    const f16x d = __builtin_amdgcn_mfma_f32_32x32x16_f16(
+        a1, b1, __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, zero, 0, 0, 0), 0, 0, 0);
+    for (int i = 0; i < 16; ++i) {  // D row (i & 3) + 8 (i >> 2) + 4 (l >> 5), column l & 31
+        const uint32_t row = (i & 3) + 8 * (i >> 2) + 4 * (l >> 5);
+        D[(size_t)t * 1024 + row * 32 + (l & 31)] = d[i];
+    }
+}
+
+int rt_debug_mfma_acc(const uint16_t* a_device, const uint16_t* b_device, float* d_device,
+                      uint32_t ntiles) {
+    if (ntiles && (!a_device || !b_device || !d_device)) return -1;
+    if (!ntiles) return 0;
+    hipLaunchKernelGGL(rt_mfma_acc_kernel, dim3(ntiles), dim3(64), 0, 0, a_device, b_device, d_device,
+                       ntiles);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -3;
+}
+#endif  // RT_MFMA_FILTER
 
 #ifdef RT_CHECK_BOUNDS
 int rt_check_bounds_take(unsigned int out[4]) {

@@ -101,6 +101,9 @@ def _hip():
         h.hipMemGetAddressRange.restype = ctypes.c_int
         h.hipMemGetAddressRange.argtypes = [ctypes.POINTER(ctypes.c_void_p),
                                             ctypes.POINTER(ctypes.c_size_t), ctypes.c_void_p]
+        h.hipDeviceCanAccessPeer.restype = ctypes.c_int
+        h.hipDeviceCanAccessPeer.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                                             ctypes.c_int]
         _HIP = h
     return _HIP
 
@@ -136,3 +139,27 @@ def ipc_import(blob: bytes):
 
 def ipc_close(mapping: int):
     _hip().hipIpcCloseMemHandle(ctypes.c_void_p(mapping))
+
+
+def can_access_peer(device: int, peer: int):
+    """hipDeviceCanAccessPeer(device, peer): True / False, or None for the same
+    device (a rehearsal with every rank on one GPU) or a failed query."""
+    if device == peer:
+        return None
+    v = ctypes.c_int(0)
+    rc = _hip().hipDeviceCanAccessPeer(ctypes.byref(v), int(device), int(peer))
+    return None if rc != 0 else bool(v.value)
+
+
+def check_rows(rows):
+    """The rows the N>1 cross-rank check re-renders on rank 0: for every rank,
+    its first, middle and last owned row (`rows[k]` = rank k's image rows in
+    its order), each once -- the rows at both ends of every rank's shard."""
+    out = []
+    for k, rk in enumerate(rows):
+        if not rk:
+            continue
+        for y in (rk[0], rk[len(rk) // 2], rk[-1]):
+            if all(y != y2 for _, y2 in out):
+                out.append((k, int(y)))
+    return out

@@ -230,7 +230,7 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n,
  * Replace records [first, first+count) of the current scene; counts N and M
  * are unchanged. Only the touched sphere records and 8-sphere groups are
  * re-packed and uploaded. The matrix-core filter's f16 sphere rows (their
- * scale 2^-sq and their k-d spatial order depend on every centre: O(N log^2 N)
+ * scale 2^-sq and their k-d spatial order depend on every centre: O(N log N)
  * on the host for the order, 64 B per sphere uploaded; buffers sized for the
  * worst-case order, so the rebuild never allocates) are rebuilt once, at the
  * next call that walks them (a caller that renders only the culled list never

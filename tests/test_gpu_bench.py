@@ -16,13 +16,23 @@ ARGS = ["--config", "config1", "--steps", "4", "--warmup", "1", "--frames-per-la
         "--no-cpu-baseline", "--reuse-steps", "0", "--cull-steps", "0", "--check"]
 
 
-def _bench(*extra):
+def _bench(*extra, rc=0):
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *ARGS, *extra],
                        cwd=ROOT, capture_output=True, text=True, timeout=100)
-    assert p.returncode == 0, p.stderr[-2000:]
+    assert (p.returncode == 0) == (rc == 0), (p.returncode, p.stderr[-2000:])
     lines = p.stdout.splitlines()
     assert len(lines) == 1, p.stdout[-2000:]
     return json.loads(lines[0])
+
+
+def _cross_ok(b, n, path):
+    """The N>1 line's own pixel check: rank 0 re-rendered the first, middle
+    and last row of every rank's shard and found them bit-exact in its image."""
+    c = b["cross_rank_check"]
+    assert c["bit_exact"] is True and c["mismatched"] == [], c
+    assert b["ranks"]["cross_rank_rows_bit_exact"] is True
+    assert c["path"] == path and c["ranks_covered"] == n and c["rows_checked"] >= 2 * n
+    assert len(b["ranks"]["peer_access"]) == n
 
 
 @pytest.mark.gpu
@@ -36,6 +46,8 @@ def test_rccl_gather_path_matches_single_gpu(gather):
     assert ("RCCL gather" if gather == "rccl" else "rank 0's image") in b["config"]["parallelism"]
     assert a["check"] == b["check"] and len(a["check"]) == 2  # the last launch's frames
     assert a["segments_per_frame"] == b["segments_per_frame"]
+    assert "cross_rank_check" not in a
+    _cross_ok(b, 1, gather if gather == "ipc" else "gather")
 
 
 @pytest.mark.gpu
@@ -54,6 +66,24 @@ def test_bench_launches_its_own_ranks(n, gather):
     assert ("rank 0's image" in b["config"]["parallelism"]) == (gather == "ipc")
     assert a["check"] == b["check"]
     assert a["segments_per_frame"] == b["segments_per_frame"]
+    _cross_ok(b, n, "ipc" if gather == "ipc" else "gather")
+    # every rank on the one device: no peer pairs to query
+    assert all(v is None for row in b["ranks"]["peer_access"] for v in row)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gather", ["rccl", "ipc"])
+def test_cross_rank_check_catches_a_stale_shard(gather):
+    """Fault injection: rank 1 renders but writes no output (knob
+    skip_collect), so its rows of rank 0's image are whatever the buffer held.
+    The N>1 line must say so -- cross_rank_rows_bit_exact false, rank 1's rows
+    named, rank 0's own rows fine -- and the run must exit non-zero."""
+    b = _bench("--gpus", "2", "--same-device", "--dist-backend", "gloo", "--gather", gather,
+               "--debug-skip-collect-rank", "1", rc=4)
+    c = b["cross_rank_check"]
+    assert c["bit_exact"] is False and b["ranks"]["cross_rank_rows_bit_exact"] is False
+    assert {k for k, _, _ in c["mismatched"]} == {1}
+    assert len(c["mismatched"]) == sum(1 for k, _ in c["rows"] if k == 1)
 
 
 @pytest.mark.gpu

@@ -1,4 +1,4 @@
-"""Print an A/B table of bench.py JSON lines (tools/gpu_r04_ab.sh,
+"""Print an A/B table of bench.py JSON lines (tools/calls/gpu_r04_ab.sh,
 gpu_r04_sens.sh output: ab_<arm>_<i>.json): Mrays/s, ms per step,
 render-kernel ms per launch, the run's clock and the launch's cycles
 (clock-independent), then each arm's mean cycles against `base`.

@@ -1,5 +1,5 @@
 """The per-form issue-price table of the render kernel's VALU forms
-(DESIGN.md §5), from one tools/gpu_r04_call2.sh run:
+(DESIGN.md §5), from one tools/calls/gpu_r04_call2.sh run:
 
   - cycles per instruction per SIMD at 1, 2, 4, 6 waves per SIMD
     (tools/ubench/valu_forms: in-kernel s_memtime; the slowest wave's
