@@ -208,6 +208,12 @@ def load(path=None):
     if hasattr(lib, "rt_debug_alloc_count"):  # internal (tests)
         lib.rt_debug_alloc_count.restype = ctypes.c_uint64
         lib.rt_debug_alloc_count.argtypes = [_VP]
+    if hasattr(lib, "rt_debug_mf_rebuilds"):  # internal (tests/test_gpu_parity.py)
+        lib.rt_debug_mf_rebuilds.restype = ctypes.c_int
+        lib.rt_debug_mf_rebuilds.argtypes = [_VP, ctypes.POINTER(ctypes.c_uint64)]
+    if hasattr(lib, "rt_debug_mf_update"):  # internal, host only (tests/test_scene_update.py)
+        lib.rt_debug_mf_update.restype = ctypes.c_int
+        lib.rt_debug_mf_update.argtypes = [_VP, _U32, _VP, _VP, _U32, _VP]
     if hasattr(lib, "rt_debug_cull_layout"):  # internal, host only (tests/test_cull.py)
         lib.rt_debug_cull_layout.restype = ctypes.c_int
         lib.rt_debug_cull_layout.argtypes = [_VP, _U32, _VP, _VP, _U32, _VP, _U32]

@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <algorithm>
 #include <cstring>
+#include <ctime>
 #include <string>
 #include <functional>
 #include <vector>
@@ -128,6 +129,22 @@ struct Tuning {
     bool skip_collect = false;
 };
 
+// The matrix-core walk's scene on the host -- exactly what its device buffers
+// hold (build_mfma fills it from a spatial order; mf_update keeps it current
+// for moved spheres without a new order).
+struct MfHost {
+    bool ok = false;
+    int sq = 0;                    // quadratic features scaled by 2^-sq
+    uint32_t nblk = 0, npos = 0, nchunk = 0;
+    bool top = false;              // a chunk-level bound chunk follows the block bounds
+    std::vector<uint32_t> order;   // walk position -> original index (0xFFFFFFFF: pad), npos
+    std::vector<uint16_t> A;       // A fragments, RT_MF_BLK uint4 per 32-sphere block
+    std::vector<uint16_t> B;       // bound chunks (+ the chunk-level one), RT_MF_BCHUNK uint4 each
+    std::vector<float4> msph;      // (cx, cy, cz, r^2) in walk order (pads r^2 = -inf)
+    std::vector<uint32_t> mperm;   // walk position -> original index (pads 0)
+    std::vector<uint32_t> iperm;   // original index -> walk position
+};
+
 struct rt_ctx {
     int device = 0;
     std::string err;
@@ -187,7 +204,13 @@ struct rt_ctx {
     float4* d_mf_shd = nullptr;
     uint32_t* d_mf_iperm = nullptr;
     size_t mf_shd_cap = 0, mf_iperm_cap = 0;
-    std::vector<uint32_t> h_mf_perm;  // walk position -> original index (0xFFFFFFFF: pad)
+    MfHost mfh;                     // the matrix-core walk's host mirror (build_mfma)
+    // spheres rt_update_spheres changed since the layout was built (flags by
+    // original index, and the list): mfma_ready moves them into the layout
+    // in place when it can (mf_update), else rebuilds it
+    std::vector<uint8_t> mf_moved_flag;
+    std::vector<uint32_t> mf_moved;
+    uint64_t mf_builds = 0, mf_inplace = 0;  // layouts built whole / updated in place
 
     // frames in flight: RT_MAX_PENDING slots of per-frame work buffers, each
     // with its own stream, so frame i+1 can start while frame i drains
@@ -492,7 +515,7 @@ static int upload_shd(rt_ctx* ctx, size_t first, size_t count) {
 // The shading records in the matrix-core walk's order (build_mfma; pads zero,
 // never shaded), from the host mirrors (quiesced).
 static int upload_shd_mf(rt_ctx* ctx) {
-    const std::vector<uint32_t>& perm = ctx->h_mf_perm;
+    const std::vector<uint32_t>& perm = ctx->mfh.order;
     std::vector<float4> rec(2 * perm.size(), make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     for (size_t p = 0; p < perm.size(); ++p)
         if (perm[p] != 0xFFFFFFFFu) shade_records(&ctx->h_rm[perm[p]], 1, ctx->h_mats, &rec[2 * p]);
@@ -864,198 +887,332 @@ static void f16_split(double x, uint16_t& hi, uint16_t& lo) {
     lo = f16_bits(x - (double)hv);
 }
 
-static int build_mfma(rt_ctx* ctx) {
-    const uint32_t n = ctx->n;
-    ctx->mf_ok = false;
-    if (!n) return RT_OK;
-    const double kS = 1.0 - 0x1p-16 - 0x1p-16;  // 1 - m - mu' (RT_MF_MU)
+static const int MF_QA[6] = {0, 1, 2, 0, 0, 1}, MF_QB[6] = {0, 1, 2, 1, 2, 2};
+static const double MF_KS = 1.0 - 0x1p-16 - 0x1p-16;           // 1 - m - mu' (RT_MF_MU)
+static const double MF_KB = 1.0 - 0x1p-16 - 0x1p-16 - 0x1p-8;  // 1 - m - mu' - muB (RT_MF_MUB)
+
+// sq of n records: the quadratic features' scale (max |c_a c_b| 2^-sq <= 2^14,
+// <= 10 for |c| <= 2^12), or -1 when a record is outside the f16 split's range
+static int mf_scale(const float4* sph, uint32_t n) {
     double qmax = 1.0;
     for (uint32_t j = 0; j < n; ++j) {
-        const float4 q = ctx->h_sph[j];
+        const float4 q = sph[j];
         if (!(std::fabs(q.x) <= 0x1p12f && std::fabs(q.y) <= 0x1p12f && std::fabs(q.z) <= 0x1p12f &&
               q.w >= 0.0f && q.w <= 0x1p24f))
-            return RT_OK;  // outside the f16 split's range: VALU filter
+            return -1;
         const double c[3] = {q.x, q.y, q.z};
         for (int a = 0; a < 3; ++a)
             for (int b = 0; b < 3; ++b) qmax = std::max(qmax, std::fabs(c[a] * c[b]));
     }
     int sq = 0;
-    while (qmax * std::ldexp(1.0, -sq) > 0x1p14) ++sq;  // <= 10 for |c| <= 2^12
-    // the walk's order: the culled list's (large spheres first, padded to a
-    // whole block, the rest in k-d order), walked in 32-sphere blocks; only
-    // the order is computed (no groups or bounds of the culled list)
-    const std::vector<uint32_t> order = spatial_order(ctx->h_sph.data(), ctx->h_S.data(), n);
-    const uint32_t nblk = (uint32_t)((order.size() + 31) / 32);
-    // queue entries hold a 14-bit group index (rt_dev_intersect.h mf_spread):
-    // larger lists use the VALU filter
-    if (nblk > 2048u) return RT_OK;
-    const uint32_t npos = nblk * 32;
-    auto perm_at = [&](uint32_t p) { return p < order.size() ? order[p] : 0xFFFFFFFFu; };
-    // buffers sized for the largest order n spheres can have: a rebuild after
-    // rt_update_spheres never reallocates (a reserved render allocates nothing)
-    const uint32_t nblk_max = (spatial_order_max(n) + 31) / 32;
-    static const int QA[6] = {0, 1, 2, 0, 0, 1}, QB[6] = {0, 1, 2, 1, 2, 2};
-    // the row of a sphere or bound (c, S'): K 0..31 (f16 bits); pad: S' = -inf
-    auto make_row = [&](const double c[3], double S, uint16_t row[32]) {
-        std::memset(row, 0, 64);
-        uint16_t hi[9], lo[9];
-        for (int a = 0; a < 3; ++a) f16_split(c[a], hi[a], lo[a]);
-        for (int f = 0; f < 6; ++f) f16_split(std::ldexp(c[QA[f]] * c[QB[f]], -sq), hi[3 + f], lo[3 + f]);
-        for (int f = 0; f < 8; ++f) {
-            row[f] = hi[f];       // w0..w3
-            row[8 + f] = lo[f];   // w4..w7
-            row[16 + f] = hi[f];  // w8..w11
-        }
-        row[24] = row[25] = hi[8];  // w12
-        row[26] = lo[8];            // w13
-        row[27] = row[28] = f16_bits(1.0);  // against the ray's T0 hi, lo
-        if (std::isinf(S)) row[29] = f16_bits(S);
-        else f16_split(S, row[29], row[30]);  // w14 hi half, w15 lo half
-    };
-    std::vector<uint16_t> h((size_t)nblk * RT_MF_BLK * 8);
-    std::vector<float4> msph(npos, make_float4(0.0f, 0.0f, 0.0f, -INFINITY));
-    std::vector<uint32_t> mperm(npos, 0u);
-    for (uint32_t p = 0; p < npos; ++p) {
-        const uint32_t b = p / 32, l0 = p & 31;
-        uint16_t row[32];
-        const uint32_t i = perm_at(p);
-        if (i != 0xFFFFFFFFu) {
-            const float4 q = ctx->h_sph[i];
-            msph[p] = q;
-            mperm[p] = i;
-            const double c[3] = {q.x, q.y, q.z};
-            const double S = (double)q.w - kS * (c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
-            if (!(std::fabs(S) <= 0x1p15)) return RT_OK;
-            make_row(c, S, row);
-        } else {
-            const double c[3] = {0.0, 0.0, 0.0};
-            make_row(c, -INFINITY, row);
-        }
-        // A0 (K 0..15) of every lane at entry l; A1 (K 16..31) of lanes
-        // 32..63 at entry 64 + (l - 32). Lanes 0..31 of A1 hold K 16..23 =
-        // the hi parts again, equal to their A0 (K 0..7): the kernel reads
-        // A0's entry for them (rt_dev_intersect.h intersect_world_mfma)
-        uint16_t* blk = &h[(size_t)b * RT_MF_BLK * 8];
-        std::memcpy(&blk[(size_t)l0 * 8], &row[0], 16);            // lane l0 (hh = 0)
-        std::memcpy(&blk[(size_t)(l0 + 32) * 8], &row[8], 16);     // lane l0 + 32 (hh = 1)
-        std::memcpy(&blk[(size_t)(64 + l0) * 8], &row[24], 16);   // A1 of lane l0 + 32
+    while (qmax * std::ldexp(1.0, -sq) > 0x1p14) ++sq;
+    return sq;
+}
+
+// S' of a record (the row's constant; the walk takes |S'| <= 2^15)
+static double mf_S(const float4 q) {
+    const double c[3] = {q.x, q.y, q.z};
+    return (double)q.w - MF_KS * (c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+}
+
+// the row of a sphere or bound (c, S'): K 0..31 (f16 bits); pad: S' = -inf
+static void mf_make_row(const double c[3], double S, int sq, uint16_t row[32]) {
+    std::memset(row, 0, 64);
+    uint16_t hi[9], lo[9];
+    for (int a = 0; a < 3; ++a) f16_split(c[a], hi[a], lo[a]);
+    for (int f = 0; f < 6; ++f) f16_split(std::ldexp(c[MF_QA[f]] * c[MF_QB[f]], -sq), hi[3 + f], lo[3 + f]);
+    for (int f = 0; f < 8; ++f) {
+        row[f] = hi[f];       // w0..w3
+        row[8 + f] = lo[f];   // w4..w7
+        row[16 + f] = hi[f];  // w8..w11
     }
-    // block bounds (rt_dev_intersect.h "Block bounds"): per chunk of 32
-    // blocks, rows = the blocks' bounding spheres in the sphere rows' layout
-    // two bounds per block, one per half (16 spheres; a block is walked for a
-    // half-wave when either passes): bound row r of chunk k = half r & 1 of
-    // block 16 k + (r >> 1), so one chunk of 32 rows covers 16 blocks
-    // A bound row has K 31 = 1, against the ray column's -RN_f16(2^-7 |o|^2)
-    // (the margin muB|o|^2 of T0_B; sphere rows have 0 there). Each chunk
-    // also holds the bounds' forward rows (rt_dev_intersect.h "Forward
-    // bounds"; v_mfma_f32_32x32x8_f16 B fragments, 8 bytes per lane at uint2
-    // 256 + lane): C hi x3, 1 | L' (rounded up), 0 x3 against the ray's dn
-    // hi x3, c0 hi | 1, 0 x3.
-    const uint32_t nchunk = (nblk + 15) / 16;
-    // chunk-level bounds (lists of 2..32 bound chunks, 513..16,384 walk
-    // positions): one more chunk after the others, row j = the bound of
-    // chunk j's 512 walk positions, tested first, so a half-wave only tests
-    // the block bounds of the chunks it passes near (rt_dev_intersect.h "Chunk
-    // bounds"; 10,000 spheres: 20 chunks)
-    const bool top = nchunk >= 2 && nchunk <= 32;
-    std::vector<uint16_t> hb((size_t)(nchunk + (top ? 1 : 0)) * RT_MF_BCHUNK * 8);
-    const double kB = 1.0 - 0x1p-16 - 0x1p-16 - 0x1p-8;  // 1 - m - mu' - muB (RT_MF_MUB)
-    // the bound of walk positions [p0, p1) as row j of bound chunk blk (line
-    // row K 0..31 and forward row K 0..7); no member: never passes
-    auto bound_row = [&](uint32_t p0, uint32_t p1, uint16_t* blk, uint32_t j) {
-        double lo3[3] = {INFINITY, INFINITY, INFINITY}, hi3[3] = {-INFINITY, -INFINITY, -INFINITY};
-        bool any = false;
+    row[24] = row[25] = hi[8];  // w12
+    row[26] = lo[8];            // w13
+    row[27] = row[28] = f16_bits(1.0);  // against the ray's T0 hi, lo
+    if (std::isinf(S)) row[29] = f16_bits(S);
+    else f16_split(S, row[29], row[30]);  // w14 hi half, w15 lo half
+}
+
+// walk position p's record and sphere row (its original index H.order[p],
+// or a pad); false when |S'| leaves the split's range
+static bool mf_set_pos(MfHost& H, uint32_t p, const float4* sph) {
+    const uint32_t b = p / 32, l0 = p & 31;
+    uint16_t row[32];
+    const uint32_t i = H.order[p];
+    if (i != 0xFFFFFFFFu) {
+        const float4 q = sph[i];
+        H.msph[p] = q;
+        H.mperm[p] = i;
+        H.iperm[i] = p;
+        const double c[3] = {q.x, q.y, q.z};
+        const double S = mf_S(q);
+        if (!(std::fabs(S) <= 0x1p15)) return false;
+        mf_make_row(c, S, H.sq, row);
+    } else {
+        const double c[3] = {0.0, 0.0, 0.0};
+        mf_make_row(c, -INFINITY, H.sq, row);
+    }
+    // A0 (K 0..15) of every lane at entry l; A1 (K 16..31) of lanes 32..63 at
+    // entry 64 + (l - 32). Lanes 0..31 of A1 hold K 16..23 = the hi parts
+    // again, equal to their A0 (K 0..7): the kernel reads A0's entry for them
+    // (rt_dev_intersect.h intersect_world_mfma)
+    uint16_t* blk = &H.A[(size_t)b * RT_MF_BLK * 8];
+    std::memcpy(&blk[(size_t)l0 * 8], &row[0], 16);           // lane l0 (hh = 0)
+    std::memcpy(&blk[(size_t)(l0 + 32) * 8], &row[8], 16);    // lane l0 + 32 (hh = 1)
+    std::memcpy(&blk[(size_t)(64 + l0) * 8], &row[24], 16);   // A1 of lane l0 + 32
+    return true;
+}
+
+// The bound of walk positions [p0, p1) as row j of bound chunk blk: line row
+// K 0..31 and forward row K 0..7 (rt_dev_intersect.h "Block bounds",
+// "Forward bounds"); no member: never passes. A bound row has K 31 = 1,
+// against the ray column's -RN_f16(muB |o|^2); the forward row is C hi x3, 1 |
+// L' (rounded up), 0 x3 against the ray's dn hi x3, c0 hi | 1, 0 x3
+// (v_mfma_f32_32x32x8_f16 B fragments, 8 bytes per lane at uint2 256 + lane).
+static void mf_bound_row(const MfHost& H, uint32_t p0, uint32_t p1, uint16_t* blk, uint32_t j) {
+    double lo3[3] = {INFINITY, INFINITY, INFINITY}, hi3[3] = {-INFINITY, -INFINITY, -INFINITY};
+    bool any = false;
+    for (uint32_t p = p0; p < p1; ++p) {
+        if (H.order[p] == 0xFFFFFFFFu) continue;
+        any = true;
+        const float4 q = H.msph[p];
+        const double c[3] = {q.x, q.y, q.z};
+        for (int a = 0; a < 3; ++a) {
+            lo3[a] = std::min(lo3[a], c[a]);
+            hi3[a] = std::max(hi3[a], c[a]);
+        }
+    }
+    double C[3] = {0.0, 0.0, 0.0}, SB = -INFINITY;  // empty: never passes
+    double Lf = 0.0;  // the forward row's L' (empty: 0, never reached)
+    if (any) {
+        for (int a = 0; a < 3; ++a) C[a] = (double)(float)((lo3[a] + hi3[a]) * 0.5);
+        double Lm = 0.0;
         for (uint32_t p = p0; p < p1; ++p) {
-            if (perm_at(p) == 0xFFFFFFFFu) continue;
-            any = true;
-            const float4 q = msph[p];
-            const double c[3] = {q.x, q.y, q.z};
+            if (H.order[p] == 0xFFFFFFFFu) continue;
+            const float4 q = H.msph[p];
+            const double dx = q.x - C[0], dy = q.y - C[1], dz = q.z - C[2];
+            Lm = std::max(Lm, std::sqrt(dx * dx + dy * dy + dz * dz) * (1.0 + 0x1p-40) +
+                                  std::sqrt((double)q.w) * (1.0 + 0x1p-18));
+        }
+        // (1 + 2^-4), not the culled list's (1 + 2^-3): rt_dev_intersect.h "Block bounds"
+        const double R2 = (1.0 + 0x1p-4) * Lm * Lm * (1.0 + 0x1p-40) + 0x1p-60;
+        const double CC = C[0] * C[0] + C[1] * C[1] + C[2] * C[2];
+        SB = (double)round_up_f32((R2 - MF_KB * CC) * (1.0 + 0x1p-40) + 0x1p-60);
+        if (!(std::fabs(SB) <= 0x1p15)) SB = INFINITY;  // out of the split's range: always passes
+        // L' = (1 + 2^-3) L + 2^-7 |C|_1 + 2^-14, rounded up; +inf (the
+        // forward row always passes) with the line row's or beyond f16
+        const double C1 = std::fabs(C[0]) + std::fabs(C[1]) + std::fabs(C[2]);
+        Lf = (1.0 + 0x1p-3) * Lm + 0x1p-7 * C1 + 0x1p-14;
+        if (std::isinf(SB) || !(Lf <= 0x1p15)) Lf = INFINITY;
+    }
+    uint16_t row[32];
+    mf_make_row(C, SB, H.sq, row);
+    row[31] = f16_bits(1.0);  // against the ray's -RN_f16(muB |o|^2)
+    for (int hh = 0; hh < 2; ++hh)
+        for (int half = 0; half < 2; ++half)  // B0: K 0..15, B1: K 16..31
+            std::memcpy(&blk[((size_t)half * 64 + 32 * hh + j) * 8], &row[16 * half + 8 * hh], 16);
+    uint16_t fw[8] = {};
+    for (int a = 0; a < 3; ++a) fw[a] = f16_bits(C[a]);
+    fw[3] = f16_bits(1.0);  // against the ray's c0
+    fw[4] = f16_bits(Lf);   // against the ray's 1; rounded up below
+    {
+        _Float16 hv;
+        std::memcpy(&hv, &fw[4], 2);
+        if ((double)hv < Lf) ++fw[4];  // the next f16 up (Lf > 0)
+    }
+    for (int hh = 0; hh < 2; ++hh) std::memcpy(&blk[(size_t)128 * 8 + (32 * hh + j) * 4], &fw[4 * hh], 8);
+}
+
+// Block bounds: per chunk of 32 bound rows, two bounds per 32-sphere block,
+// one per 16-sphere half (a block is walked for a half-wave when either
+// passes): bound row r of chunk k = half r & 1 of block 16 k + (r >> 1).
+static void mf_half_block_bound(MfHost& H, uint32_t r) {
+    const uint32_t k = r / 32, j = r & 31, p0 = 16 * r;
+    mf_bound_row(H, p0, r < 2 * H.nblk ? p0 + 16 : p0, &H.B[(size_t)k * RT_MF_BCHUNK * 8], j);
+}
+
+// Chunk-level bounds (lists of 2..32 bound chunks, 513..16,384 walk
+// positions): one more chunk after the others, row j = the bound of chunk j's
+// 512 walk positions, tested first, so a half-wave only tests the block
+// bounds of the chunks it passes near (rt_dev_intersect.h "Chunk bounds";
+// 10,000 spheres: 20 chunks).
+static void mf_chunk_bound(MfHost& H, uint32_t j) {
+    const uint32_t p0 = 512 * j, p1 = j < H.nchunk ? std::min(p0 + 512, H.npos) : p0;
+    mf_bound_row(H, p0, p1, &H.B[(size_t)H.nchunk * RT_MF_BCHUNK * 8], j);
+}
+
+// The whole layout of n records in walk order `order` (spatial_order's) at
+// scale sq; false when the list does not fit the walk (more than 2,048
+// blocks: the queue entries' 14-bit group index, rt_dev_intersect.h
+// mf_spread) or a row leaves the split's range.
+static bool mf_fill(const float4* sph, uint32_t n, std::vector<uint32_t> order, int sq, MfHost& H) {
+    H = MfHost{};
+    H.sq = sq;
+    H.nblk = (uint32_t)((order.size() + 31) / 32);
+    if (H.nblk > 2048u) return false;
+    H.npos = H.nblk * 32;
+    order.resize(H.npos, 0xFFFFFFFFu);
+    H.order = std::move(order);
+    H.A.assign((size_t)H.nblk * RT_MF_BLK * 8, 0);
+    H.msph.assign(H.npos, make_float4(0.0f, 0.0f, 0.0f, -INFINITY));
+    H.mperm.assign(H.npos, 0u);
+    H.iperm.assign(n, 0u);
+    for (uint32_t p = 0; p < H.npos; ++p)
+        if (!mf_set_pos(H, p, sph)) return false;
+    H.nchunk = (H.nblk + 15) / 16;
+    H.top = H.nchunk >= 2 && H.nchunk <= 32;
+    H.B.assign((size_t)(H.nchunk + (H.top ? 1 : 0)) * RT_MF_BCHUNK * 8, 0);
+    for (uint32_t r = 0; r < H.nchunk * 32; ++r) mf_half_block_bound(H, r);
+    if (H.top)
+        for (uint32_t j = 0; j < 32; ++j) mf_chunk_bound(H, j);
+    H.ok = true;
+    return true;
+}
+
+// The layout from scratch: scale, spatial order (the culled list's: large
+// spheres first, padded to a whole block, the rest in k-d order; only the
+// order, no groups or bounds of the culled list), rows, bounds.
+static bool mf_build(const float4* sph, const float* S, uint32_t n, MfHost& H) {
+    H = MfHost{};
+    if (!n) return false;
+    const int sq = mf_scale(sph, n);
+    if (sq < 0) return false;
+    return mf_fill(sph, n, spatial_order(sph, S, n), sq, H);
+}
+
+// Moved spheres into the layout in place, keeping the walk order: every moved
+// sphere must keep its radius (the large / small split, whose threshold is a
+// median radius, is unchanged then) and stay within its block's box of
+// centres grown by a quarter of the box's largest extent on each side (so
+// the order stays a spatial one and the block's bound grows little), and the
+// scale sq must not change. Then its position's record and row, its
+// half-block's bound row and (with chunk-level bounds) its chunk's row are
+// rebuilt: O(moved) plus one O(N) pass for sq. The result is byte for byte
+// mf_fill of the same order (tests/test_scene_update.py). false: H is
+// untouched and the caller rebuilds everything. touched_*: what to upload.
+static bool mf_update(MfHost& H, const float4* sph, uint32_t n, const std::vector<uint32_t>& moved,
+                      std::vector<uint32_t>& touched_blocks, std::vector<uint32_t>& touched_chunks,
+                      std::vector<uint32_t>& touched_pos) {
+    if (!H.ok || H.iperm.size() != n) return false;
+    for (uint32_t i : moved) {
+        if (i >= n) return false;
+        const uint32_t p = H.iperm[i];
+        const float4 o = H.msph[p], q = sph[i];
+        if (std::memcmp(&o.w, &q.w, 4) != 0) return false;
+        if (!(std::fabs(mf_S(q)) <= 0x1p15)) return false;
+        double lo3[3] = {INFINITY, INFINITY, INFINITY}, hi3[3] = {-INFINITY, -INFINITY, -INFINITY};
+        const uint32_t b = p / 32;
+        for (uint32_t pp = 32 * b; pp < 32 * b + 32; ++pp) {
+            if (H.order[pp] == 0xFFFFFFFFu) continue;
+            const double c[3] = {H.msph[pp].x, H.msph[pp].y, H.msph[pp].z};
             for (int a = 0; a < 3; ++a) {
                 lo3[a] = std::min(lo3[a], c[a]);
                 hi3[a] = std::max(hi3[a], c[a]);
             }
         }
-        double C[3] = {0.0, 0.0, 0.0}, SB = -INFINITY;  // empty: never passes
-        double Lf = 0.0;  // the forward row's L' (empty: 0, never reached)
-        if (any) {
-            for (int a = 0; a < 3; ++a) C[a] = (double)(float)((lo3[a] + hi3[a]) * 0.5);
-            double Lm = 0.0;
-            for (uint32_t p = p0; p < p1; ++p) {
-                if (perm_at(p) == 0xFFFFFFFFu) continue;
-                const float4 q = msph[p];
-                const double dx = q.x - C[0], dy = q.y - C[1], dz = q.z - C[2];
-                Lm = std::max(Lm, std::sqrt(dx * dx + dy * dy + dz * dz) * (1.0 + 0x1p-40) +
-                                      std::sqrt((double)q.w) * (1.0 + 0x1p-18));
-            }
-            // (1 + 2^-4), not the culled list's (1 + 2^-3): rt_dev_intersect.h "Block bounds"
-            const double R2 = (1.0 + 0x1p-4) * Lm * Lm * (1.0 + 0x1p-40) + 0x1p-60;
-            const double CC = C[0] * C[0] + C[1] * C[1] + C[2] * C[2];
-            SB = (double)round_up_f32((R2 - kB * CC) * (1.0 + 0x1p-40) + 0x1p-60);
-            if (!(std::fabs(SB) <= 0x1p15)) SB = INFINITY;  // out of the split's range: always passes
-            // L' = (1 + 2^-3) L + 2^-7 |C|_1 + 2^-14, rounded up; +inf (the
-            // forward row always passes) with the line row's or beyond f16
-            const double C1 = std::fabs(C[0]) + std::fabs(C[1]) + std::fabs(C[2]);
-            Lf = (1.0 + 0x1p-3) * Lm + 0x1p-7 * C1 + 0x1p-14;
-            if (std::isinf(SB) || !(Lf <= 0x1p15)) Lf = INFINITY;
-        }
-        uint16_t row[32];
-        make_row(C, SB, row);
-        row[31] = f16_bits(1.0);  // against the ray's -RN_f16(muB |o|^2)
-        for (int hh = 0; hh < 2; ++hh)
-            for (int half = 0; half < 2; ++half)  // B0: K 0..15, B1: K 16..31
-                std::memcpy(&blk[((size_t)half * 64 + 32 * hh + j) * 8], &row[16 * half + 8 * hh], 16);
-        uint16_t fw[8] = {};
-        for (int a = 0; a < 3; ++a) fw[a] = f16_bits(C[a]);
-        fw[3] = f16_bits(1.0);  // against the ray's c0
-        fw[4] = f16_bits(Lf);   // against the ray's 1; rounded up below
-        {
-            _Float16 hv;
-            std::memcpy(&hv, &fw[4], 2);
-            if ((double)hv < Lf) ++fw[4];  // the next f16 up (Lf > 0)
-        }
-        for (int hh = 0; hh < 2; ++hh) std::memcpy(&blk[(size_t)128 * 8 + (32 * hh + j) * 4], &fw[4 * hh], 8);
-    };
-    for (uint32_t r = 0; r < nchunk * 32; ++r) {
-        const uint32_t k = r / 32, j = r & 31;
-        const uint32_t p0 = 16 * r;  // the half-block's first walk position
-        bound_row(p0, r < 2 * nblk ? p0 + 16 : p0, &hb[(size_t)k * RT_MF_BCHUNK * 8], j);
+        const double ext = std::max(hi3[0] - lo3[0], std::max(hi3[1] - lo3[1], hi3[2] - lo3[2])) * 0.25;
+        const double c[3] = {q.x, q.y, q.z};
+        for (int a = 0; a < 3; ++a)
+            if (!(c[a] >= lo3[a] - ext && c[a] <= hi3[a] + ext)) return false;
     }
-    if (top)
-        for (uint32_t j = 0; j < 32; ++j) {
-            const uint32_t p0 = 512 * j, p1 = j < nchunk ? std::min(p0 + 512, npos) : p0;
-            bound_row(p0, p1, &hb[(size_t)nchunk * RT_MF_BCHUNK * 8], j);
-        }
+    if (mf_scale(sph, n) != H.sq) return false;
+    touched_blocks.clear();
+    touched_chunks.clear();
+    touched_pos.clear();
+    std::vector<uint32_t> halves;
+    for (uint32_t i : moved) {
+        const uint32_t p = H.iperm[i];
+        mf_set_pos(H, p, sph);  // (in range: checked above)
+        touched_pos.push_back(p);
+        touched_blocks.push_back(p / 32);
+        halves.push_back(p / 16);
+        touched_chunks.push_back(p / 512);
+    }
+    auto uniq = [](std::vector<uint32_t>& v) {
+        std::sort(v.begin(), v.end());
+        v.erase(std::unique(v.begin(), v.end()), v.end());
+    };
+    uniq(touched_blocks);
+    uniq(halves);
+    uniq(touched_chunks);
+    uniq(touched_pos);
+    for (uint32_t r : halves) mf_half_block_bound(H, r);
+    if (H.top) {
+        for (uint32_t k : touched_chunks) mf_chunk_bound(H, k);
+        touched_chunks.push_back(H.nchunk);  // the chunk-level chunk changed too
+    }
+    return true;
+}
+
+// Upload the whole layout (build_mfma).
+static int mf_upload_all(rt_ctx* ctx) {
+    const MfHost& H = ctx->mfh;
+    // buffers sized for the largest order n spheres can have: a rebuild after
+    // rt_update_spheres never reallocates (a reserved render allocates nothing)
+    const uint32_t nblk_max = (spatial_order_max(ctx->n) + 31) / 32;
     const size_t nchunk_max = (nblk_max + 15) / 16 + 1;  // + the chunk-level bounds
     int rc = ensure(ctx, &ctx->d_mfA, &ctx->mfA_cap, (size_t)nblk_max * RT_MF_BLK * 16);
     if (!rc) rc = ensure(ctx, &ctx->d_mfB, &ctx->mfB_cap, nchunk_max * RT_MF_BCHUNK * 16);
     if (!rc) rc = ensure(ctx, &ctx->d_mf_sph, &ctx->mf_sph_cap, (size_t)nblk_max * 32 * sizeof(float4));
     if (!rc) rc = ensure(ctx, &ctx->d_mf_perm, &ctx->mf_perm_cap, (size_t)nblk_max * 32 * sizeof(uint32_t));
     if (!rc) rc = ensure(ctx, &ctx->d_mf_shd, &ctx->mf_shd_cap, (size_t)nblk_max * 32 * 2 * sizeof(float4));
-    if (!rc) rc = ensure(ctx, &ctx->d_mf_iperm, &ctx->mf_iperm_cap, (size_t)n * sizeof(uint32_t));
+    if (!rc) rc = ensure(ctx, &ctx->d_mf_iperm, &ctx->mf_iperm_cap, (size_t)ctx->n * sizeof(uint32_t));
     if (rc) return rc;
-    HIP_TRY(ctx, hipMemcpy(ctx->d_mfA, h.data(), h.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
-    HIP_TRY(ctx, hipMemcpy(ctx->d_mfB, hb.data(), hb.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
-    HIP_TRY(ctx, hipMemcpy(ctx->d_mf_sph, msph.data(), msph.size() * sizeof(float4), hipMemcpyHostToDevice));
-    HIP_TRY(ctx, hipMemcpy(ctx->d_mf_perm, mperm.data(), mperm.size() * sizeof(uint32_t),
+    HIP_TRY(ctx, hipMemcpy(ctx->d_mfA, H.A.data(), H.A.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(ctx->d_mfB, H.B.data(), H.B.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(ctx->d_mf_sph, H.msph.data(), H.msph.size() * sizeof(float4), hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(ctx->d_mf_perm, H.mperm.data(), H.mperm.size() * sizeof(uint32_t),
                            hipMemcpyHostToDevice));
-    {  // original index -> walk position, and the walk-order shading records
-        std::vector<uint32_t> iperm(n, 0u);
-        ctx->h_mf_perm.assign(npos, 0xFFFFFFFFu);
-        for (uint32_t p = 0; p < npos; ++p) {
-            const uint32_t i = perm_at(p);
-            ctx->h_mf_perm[p] = i;
-            if (i != 0xFFFFFFFFu) iperm[i] = p;
-        }
-        HIP_TRY(ctx, hipMemcpy(ctx->d_mf_iperm, iperm.data(), iperm.size() * sizeof(uint32_t),
-                               hipMemcpyHostToDevice));
-        rc = upload_shd_mf(ctx);
-        if (rc) return rc;
+    // original index -> walk position, and the walk-order shading records
+    HIP_TRY(ctx, hipMemcpy(ctx->d_mf_iperm, H.iperm.data(), H.iperm.size() * sizeof(uint32_t),
+                           hipMemcpyHostToDevice));
+    return upload_shd_mf(ctx);
+}
+
+static int build_mfma(rt_ctx* ctx) {
+    ctx->mf_ok = false;
+    ctx->mf_moved.clear();
+    ctx->mf_moved_flag.assign(ctx->n, 0);
+    if (!mf_build(ctx->h_sph.data(), ctx->h_S.data(), ctx->n, ctx->mfh)) {
+        ctx->mfh = MfHost{};
+        return RT_OK;  // outside the walk's range: the VALU filter
     }
-    ctx->mf_nblk = nblk;
-    ctx->mf_top = top;
-    ctx->mf_qs = (float)std::ldexp(1.0, sq);
-    ctx->mf_abs = (float)std::ldexp(1.0, sq - 20);
+    const int rc = mf_upload_all(ctx);
+    if (rc) return rc;
+    ++ctx->mf_builds;
+    ctx->mf_nblk = ctx->mfh.nblk;
+    ctx->mf_top = ctx->mfh.top;
+    ctx->mf_qs = (float)std::ldexp(1.0, ctx->mfh.sq);
+    ctx->mf_abs = (float)std::ldexp(1.0, ctx->mfh.sq - 20);
     ctx->mf_ok = true;
+    return RT_OK;
+}
+
+// The spheres rt_update_spheres moved since the layout was built, in place
+// (mf_update) when they allow it: only the touched A blocks (1.5 KB each),
+// bound chunks (2.5 KB each) and walk positions' records and shading records
+// go to the device. Else the whole layout is rebuilt.
+static int mf_apply_moves(rt_ctx* ctx) {
+    std::vector<uint32_t> tb, tc, tp;
+    const bool inplace = ctx->mf_ok &&
+                         mf_update(ctx->mfh, ctx->h_sph.data(), ctx->n, ctx->mf_moved, tb, tc, tp);
+    if (!inplace) return build_mfma(ctx);
+    const MfHost& H = ctx->mfh;
+    for (uint32_t b : tb)
+        HIP_TRY(ctx, hipMemcpy(reinterpret_cast<uint16_t*>(ctx->d_mfA) + (size_t)b * RT_MF_BLK * 8,
+                               &H.A[(size_t)b * RT_MF_BLK * 8], RT_MF_BLK * 16, hipMemcpyHostToDevice));
+    for (uint32_t k : tc)
+        HIP_TRY(ctx, hipMemcpy(reinterpret_cast<uint16_t*>(ctx->d_mfB) + (size_t)k * RT_MF_BCHUNK * 8,
+                               &H.B[(size_t)k * RT_MF_BCHUNK * 8], RT_MF_BCHUNK * 16, hipMemcpyHostToDevice));
+    for (uint32_t p : tp) {
+        HIP_TRY(ctx, hipMemcpy(ctx->d_mf_sph + p, &H.msph[p], sizeof(float4), hipMemcpyHostToDevice));
+        float4 rec[2];
+        shade_records(&ctx->h_rm[H.order[p]], 1, ctx->h_mats, rec);
+        HIP_TRY(ctx, hipMemcpy(ctx->d_mf_shd + 2 * (size_t)p, rec, sizeof(rec), hipMemcpyHostToDevice));
+    }
+    for (uint32_t i : ctx->mf_moved) ctx->mf_moved_flag[i] = 0;
+    ctx->mf_moved.clear();
+    ++ctx->mf_inplace;
     return RT_OK;
 }
 #endif
@@ -1155,7 +1312,7 @@ static int cull_ready(rt_ctx* ctx) {
 static int mfma_ready(rt_ctx* ctx) {
 #ifdef RT_MFMA_FILTER
     if (!ctx->mf_dirty) return RT_OK;
-    int rc = build_mfma(ctx);
+    int rc = mf_apply_moves(ctx);
     if (rc) return rc;
     ctx->mf_dirty = false;
 #else
@@ -1182,6 +1339,14 @@ int rt_update_spheres(rt_ctx* ctx, uint32_t first, const rt_sphere* spheres, uin
     int rc = check_spheres(ctx, spheres, first, count, ctx->m);
     if (rc) return rc;
     for (uint32_t i = 0; i < count; ++i) pack_record(ctx, first + i, spheres[i]);
+#ifdef RT_MFMA_FILTER
+    if (ctx->mf_moved_flag.size() == ctx->n)
+        for (uint32_t i = first; i < first + count; ++i)
+            if (!ctx->mf_moved_flag[i]) {
+                ctx->mf_moved_flag[i] = 1;
+                ctx->mf_moved.push_back(i);
+            }
+#endif
     const size_t g0 = first / RT_GROUP, g1 = (first + count - 1) / RT_GROUP + 1;
     for (size_t g = g0; g < g1; ++g) pack_group(ctx, g);
     rc = quiesce(ctx);
@@ -2080,6 +2245,74 @@ int rt_debug_cull_layout(const rt_sphere* spheres, uint32_t n, uint32_t* counts,
     if (bnd && bnd_cap >= L.bnd.size() * 4) std::memcpy(bnd, L.bnd.data(), L.bnd.size() * sizeof(float4));
     return 0;
 }
+
+// Internal (not in include/rt_hip.h; tests/test_gpu_parity.py): matrix-core
+// layouts this context built whole and updated in place (mf_update).
+int rt_debug_mf_rebuilds(const rt_ctx* ctx, uint64_t* out2) {
+    if (!ctx || !out2) return -1;
+    out2[0] = ctx->mf_builds;
+    out2[1] = ctx->mf_inplace;
+    return 0;
+}
+
+#ifdef RT_MFMA_FILTER
+// Internal, host only (not in include/rt_hip.h; tests/test_scene_update.py):
+// the matrix-core layout of spheres s0, then the spheres idx[0..k) replaced
+// by s1[0..k) as rt_update_spheres + the next render would apply them. ms3:
+// the layout built from scratch for s0, the in-place update, and a build from
+// scratch of the updated list (what the fallback costs), in ms of host time.
+// Returns 1 when the update was applied in place AND its layout equals, byte
+// for byte, the layout filled from scratch in the same walk order; 0 when it
+// falls back to a full rebuild; -1 on a mismatch; -2 when s0 does not take
+// the matrix-core walk.
+int rt_debug_mf_update(const rt_sphere* s0, uint32_t n, const uint32_t* idx, const rt_sphere* s1,
+                       uint32_t k, double* ms3) {
+    if (!s0 || !n || (k && (!idx || !s1))) return -2;
+    std::vector<float4> q(n);
+    std::vector<float> S(n);
+    std::vector<float2> rm(n);
+    for (uint32_t i = 0; i < n; ++i) pack_record_to(s0[i], q[i], S[i], rm[i]);
+    auto now = [] {
+        timespec ts;
+        clock_gettime(CLOCK_MONOTONIC, &ts);
+        return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+    };
+    MfHost H;
+    double t = now();
+    if (!mf_build(q.data(), S.data(), n, H)) return -2;
+    const double t_full0 = now() - t;
+    std::vector<uint32_t> moved;
+    for (uint32_t j = 0; j < k; ++j) {
+        if (idx[j] >= n) return -2;
+        pack_record_to(s1[j], q[idx[j]], S[idx[j]], rm[idx[j]]);
+        moved.push_back(idx[j]);
+    }
+    std::sort(moved.begin(), moved.end());
+    moved.erase(std::unique(moved.begin(), moved.end()), moved.end());
+    std::vector<uint32_t> tb, tc, tp;
+    t = now();
+    const bool inplace = mf_update(H, q.data(), n, moved, tb, tc, tp);
+    const double t_upd = now() - t;
+    MfHost F;
+    t = now();
+    mf_build(q.data(), S.data(), n, F);
+    const double t_full1 = now() - t;
+    if (ms3) {
+        ms3[0] = t_full0;
+        ms3[1] = t_upd;
+        ms3[2] = t_full1;
+    }
+    if (!inplace) return 0;
+    MfHost G;
+    if (!mf_fill(q.data(), n, H.order, H.sq, G)) return -1;
+    const bool same = G.ok == H.ok && G.sq == H.sq && G.nblk == H.nblk && G.npos == H.npos &&
+                      G.nchunk == H.nchunk && G.top == H.top && G.order == H.order && G.A == H.A &&
+                      G.B == H.B && G.mperm == H.mperm && G.iperm == H.iperm &&
+                      G.msph.size() == H.msph.size() &&
+                      std::memcmp(G.msph.data(), H.msph.data(), G.msph.size() * sizeof(float4)) == 0;
+    return same ? 1 : -1;
+}
+#endif
 
 // Internal (not in include/rt_hip.h): the first 16 diagnostic counters of the
 // last waited call; all zero unless the library was built with -DRT_PROFILE.

@@ -802,6 +802,16 @@ __device__ __forceinline__ float4 rec_load(lds_cfloat4* p, uint32_t i) {
     const f4v v = ((lds_f4v*)p)[i];  // one ds_read_b128
     return make_float4(v.x, v.y, v.z, v.w);
 }
+#ifdef RT_DRAIN_DUMP
+// Diagnostic build only (-DRT_DRAIN_DUMP): every 61st drain of the launch
+// (any wave), per lane (ray) its queued entries (low 16 bits) and candidate
+// tests (high 16), RT_DRAIN_DUMP_MAX drains; read back with
+// rt_debug_drain_dump() (tools/drain_dump.py: the drain's lane balance).
+#define RT_DRAIN_DUMP_MAX 65536
+__device__ uint32_t g_drain_dump[RT_DRAIN_DUMP_MAX * 64];
+__device__ unsigned int g_drain_seq;
+__device__ unsigned int g_drain_rec;
+#endif
 template <bool FAST, typename SP, uint32_t CAP = RT_MF_CAP>
 __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, uint32_t cnt1,
                                            SP sph, uint32_t nsph,
@@ -831,6 +841,26 @@ __device__ __forceinline__ void mfma_drain(const uint32_t* cq, uint32_t cnt0, ui
     // (profiles/r03/ab_drain/); loading the next candidate's record ahead of
     // the current test (123 VGPRs) cost 2.2 %.
     const uint32_t total = na + nb;
+#ifdef RT_DRAIN_DUMP
+    {
+        uint32_t seq = 0;
+        if (lane == 0) seq = atomicAdd(&g_drain_seq, 1u);
+        seq = (uint32_t)__builtin_amdgcn_readfirstlane((int)seq);
+        if (seq % 61u == 0u) {
+            uint32_t rec = 0;
+            if (lane == 0) rec = atomicAdd(&g_drain_rec, 1u);
+            rec = (uint32_t)__builtin_amdgcn_readfirstlane((int)rec);
+            if (rec < RT_DRAIN_DUMP_MAX) {
+                uint32_t bits = 0;
+                for (uint32_t k = 0; k < total; ++k) {
+                    const bool s1 = k >= na;
+                    bits += __popc(q[(s1 ? k - na : k) * 64u + (s1 ? j + 32u : j)] & RT_MF_FLAGS);
+                }
+                g_drain_dump[rec * 64u + lane] = total | (bits << 16);
+            }
+        }
+    }
+#endif
     uint32_t i = 0, m = 0, base = 0;
     while (m != 0 || i < total) {
         if (m == 0) {

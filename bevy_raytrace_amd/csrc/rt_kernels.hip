@@ -1029,6 +1029,20 @@ int rt_debug_ray_dump(float* out, uint32_t max_waves) {
 }
 #endif
 
+#ifdef RT_DRAIN_DUMP
+int rt_debug_drain_dump(uint32_t* out, uint32_t max_drains) {
+    unsigned int n = 0;
+    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_drain_rec), sizeof(n)) != hipSuccess) return -1;
+    if (n > RT_DRAIN_DUMP_MAX) n = RT_DRAIN_DUMP_MAX;
+    if (n > max_drains) n = max_drains;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_drain_dump), (size_t)n * 64 * 4) != hipSuccess) return -1;
+    const unsigned int zero = 0;
+    hipMemcpyToSymbol(HIP_SYMBOL(g_drain_rec), &zero, sizeof(zero));
+    hipMemcpyToSymbol(HIP_SYMBOL(g_drain_seq), &zero, sizeof(zero));
+    return (int)n;
+}
+#endif
+
 #ifdef RT_CHUNK_TRACE
 int rt_debug_chunk_trace(unsigned long long* out, unsigned long long* clk, uint32_t n) {
     if (n > RT_CHUNK_TRACE_MAX) n = RT_CHUNK_TRACE_MAX;

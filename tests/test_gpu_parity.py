@@ -5,6 +5,7 @@ algorithmic segment counts, on the same seeded inputs. At full BASELINE sizes
 the oracle checks sampled rows, plus size-independent properties
 (determinism, reuse on/off identity, multi-pass identity, shard assembly).
 """
+import ctypes
 import glob
 import os
 
@@ -614,6 +615,55 @@ def test_update_spheres_and_materials(renderer):
     gi, gt = renderer.intersect(rays)
     ci, ct = O.intersect_batch(sp2, rays)
     assert gi[0] == ci[0] and gt[0] == ct[0]
+
+
+def mf_rebuilds(renderer):
+    out = (ctypes.c_uint64 * 2)()
+    assert renderer.lib.rt_debug_mf_rebuilds(renderer.ctx, out) == 0
+    return int(out[0]), int(out[1])
+
+
+@pytest.mark.parametrize("sc_name", ["rtiow", "tenk"])
+def test_update_spheres_in_place(renderer, sc_name):
+    """Small moves (and a material change) go into the matrix-core layout in
+    place (rt_api.cpp mf_update: the moved rows, their half-block and chunk
+    bound rows, their records and shading records; no new order), and the
+    frames after each edit equal the oracle's of the edited scene -- the
+    10,000-sphere list with its chunk-level bounds included. A move that
+    leaves the block's box takes the whole rebuild, also exact."""
+    sc = scene.rtiow_final_scene() if sc_name == "rtiow" else scene.ten_thousand_scene()
+    sp, mt = arrays(sc)
+    renderer.set_scene(sp, mt)
+    cam = default_camera_block()
+    W, H, S, D = (96, 54, 2, 6)
+    b0, i0 = mf_rebuilds(renderer)
+    rng = np.random.default_rng(11)
+    sp2 = sp.copy()
+    for step in range(3):
+        idx = np.sort(rng.choice(np.arange(len(sp) - 3), 12, replace=False))
+        d = rng.uniform(-0.04, 0.04, (12, 3)).astype(np.float32)
+        sp2["center"][idx] += d
+        sp2["material"][idx[0]] = sp2["material"][idx[-1]]
+        for i in idx:
+            renderer.update_spheres(int(i), sp2[i:i + 1])
+        img, st = renderer.render(cam, W, H, S, D, frame0=step)
+        rows = None if sc_name == "rtiow" else list(range(0, H, 9))
+        if rows is None:
+            ref, segs = O.render(cam, sp2, mt, W, H, S, D, frame0=step)
+            check_exact(img, ref)
+            assert st["segments"] == segs
+        else:
+            ref, _ = O.render_rows(cam, sp2, mt, W, H, S, D, rows, frame0=step)
+            check_exact(img[rows], ref)
+    b1, i1 = mf_rebuilds(renderer)
+    assert (b1 - b0, i1 - i0) == (0, 3)  # every edit in place
+    sp2["center"][5] += np.float32(40.0)  # far from its block: a new order
+    renderer.update_spheres(5, sp2[5:6])
+    img, st = renderer.render(cam, W, H, S, D, frame0=7)
+    assert mf_rebuilds(renderer)[0] == b1 + 1
+    if sc_name == "rtiow":
+        ref, segs = O.render(cam, sp2, mt, W, H, S, D, frame0=7)
+        check_exact(img, ref)
 
 
 def test_update_errors(renderer):
