@@ -143,6 +143,7 @@ struct MfHost {
     std::vector<float4> msph;      // (cx, cy, cz, r^2) in walk order (pads r^2 = -inf)
     std::vector<uint32_t> mperm;   // walk position -> original index (pads 0)
     std::vector<uint32_t> iperm;   // original index -> walk position
+    std::vector<double> bqmax;     // per block max_i max_a c_a^2 of its members (the scale's input)
 };
 
 struct rt_ctx {
@@ -891,22 +892,31 @@ static const int MF_QA[6] = {0, 1, 2, 0, 0, 1}, MF_QB[6] = {0, 1, 2, 1, 2, 2};
 static const double MF_KS = 1.0 - 0x1p-16 - 0x1p-16;           // 1 - m - mu' (RT_MF_MU)
 static const double MF_KB = 1.0 - 0x1p-16 - 0x1p-16 - 0x1p-8;  // 1 - m - mu' - muB (RT_MF_MUB)
 
-// sq of n records: the quadratic features' scale (max |c_a c_b| 2^-sq <= 2^14,
-// <= 10 for |c| <= 2^12), or -1 when a record is outside the f16 split's range
+// A record inside the f16 split's range (|c_i| <= 2^12, r^2 in [0, 2^24]),
+// and its largest quadratic feature max_ab |c_a c_b| = max_a c_a^2.
+static bool mf_in_range(const float4 q) {
+    return std::fabs(q.x) <= 0x1p12f && std::fabs(q.y) <= 0x1p12f && std::fabs(q.z) <= 0x1p12f &&
+           q.w >= 0.0f && q.w <= 0x1p24f;
+}
+static double mf_qmax(const float4 q) {
+    const double x = q.x, y = q.y, z = q.z;
+    return std::max(x * x, std::max(y * y, z * z));
+}
+// sq for the largest quadratic feature: max |c_a c_b| 2^-sq <= 2^14 (<= 10
+// for |c| <= 2^12)
+static int mf_sq_of(double qmax) {
+    int sq = 0;
+    while (std::max(qmax, 1.0) * std::ldexp(1.0, -sq) > 0x1p14) ++sq;
+    return sq;
+}
+// sq of n records, or -1 when a record is outside the split's range
 static int mf_scale(const float4* sph, uint32_t n) {
     double qmax = 1.0;
     for (uint32_t j = 0; j < n; ++j) {
-        const float4 q = sph[j];
-        if (!(std::fabs(q.x) <= 0x1p12f && std::fabs(q.y) <= 0x1p12f && std::fabs(q.z) <= 0x1p12f &&
-              q.w >= 0.0f && q.w <= 0x1p24f))
-            return -1;
-        const double c[3] = {q.x, q.y, q.z};
-        for (int a = 0; a < 3; ++a)
-            for (int b = 0; b < 3; ++b) qmax = std::max(qmax, std::fabs(c[a] * c[b]));
+        if (!mf_in_range(sph[j])) return -1;
+        qmax = std::max(qmax, mf_qmax(sph[j]));
     }
-    int sq = 0;
-    while (qmax * std::ldexp(1.0, -sq) > 0x1p14) ++sq;
-    return sq;
+    return mf_sq_of(qmax);
 }
 
 // S' of a record (the row's constant; the walk takes |S'| <= 2^15)
@@ -1059,6 +1069,9 @@ static bool mf_fill(const float4* sph, uint32_t n, std::vector<uint32_t> order, 
     H.iperm.assign(n, 0u);
     for (uint32_t p = 0; p < H.npos; ++p)
         if (!mf_set_pos(H, p, sph)) return false;
+    H.bqmax.assign(H.nblk, 0.0);
+    for (uint32_t p = 0; p < H.npos; ++p)
+        if (H.order[p] != 0xFFFFFFFFu) H.bqmax[p / 32] = std::max(H.bqmax[p / 32], mf_qmax(H.msph[p]));
     H.nchunk = (H.nblk + 15) / 16;
     H.top = H.nchunk >= 2 && H.nchunk <= 32;
     H.B.assign((size_t)(H.nchunk + (H.top ? 1 : 0)) * RT_MF_BCHUNK * 8, 0);
@@ -1115,7 +1128,27 @@ static bool mf_update(MfHost& H, const float4* sph, uint32_t n, const std::vecto
         for (int a = 0; a < 3; ++a)
             if (!(c[a] >= lo3[a] - ext && c[a] <= hi3[a] + ext)) return false;
     }
-    if (mf_scale(sph, n) != H.sq) return false;
+    // the scale from the per-block maxima, the moved spheres' blocks
+    // recomputed with their new records: O(32 moved + blocks), not O(N)
+    std::vector<uint32_t> blocks;
+    for (uint32_t i : moved) {
+        if (!mf_in_range(sph[i])) return false;
+        blocks.push_back(H.iperm[i] / 32);
+    }
+    std::sort(blocks.begin(), blocks.end());
+    blocks.erase(std::unique(blocks.begin(), blocks.end()), blocks.end());
+    std::vector<double> bq(blocks.size(), 0.0);
+    for (size_t k = 0; k < blocks.size(); ++k)
+        for (uint32_t p = 32 * blocks[k]; p < 32 * blocks[k] + 32; ++p)
+            if (H.order[p] != 0xFFFFFFFFu) bq[k] = std::max(bq[k], mf_qmax(sph[H.order[p]]));
+    double qmax = 1.0;
+    for (uint32_t b = 0, k = 0; b < H.nblk; ++b) {
+        const bool t = k < blocks.size() && blocks[k] == b;
+        qmax = std::max(qmax, t ? bq[k] : H.bqmax[b]);
+        k += t ? 1 : 0;
+    }
+    if (mf_sq_of(qmax) != H.sq) return false;
+    for (size_t k = 0; k < blocks.size(); ++k) H.bqmax[blocks[k]] = bq[k];
     touched_blocks.clear();
     touched_chunks.clear();
     touched_pos.clear();
@@ -2307,7 +2340,7 @@ int rt_debug_mf_update(const rt_sphere* s0, uint32_t n, const uint32_t* idx, con
     if (!mf_fill(q.data(), n, H.order, H.sq, G)) return -1;
     const bool same = G.ok == H.ok && G.sq == H.sq && G.nblk == H.nblk && G.npos == H.npos &&
                       G.nchunk == H.nchunk && G.top == H.top && G.order == H.order && G.A == H.A &&
-                      G.B == H.B && G.mperm == H.mperm && G.iperm == H.iperm &&
+                      G.B == H.B && G.mperm == H.mperm && G.iperm == H.iperm && G.bqmax == H.bqmax &&
                       G.msph.size() == H.msph.size() &&
                       std::memcmp(G.msph.data(), H.msph.data(), G.msph.size() * sizeof(float4)) == 0;
     return same ? 1 : -1;
