@@ -69,7 +69,10 @@ struct Frame {
 struct Tuning {
     size_t scratch_bytes = (size_t)16 << 30;  // block sums per launch (of 288 GB HBM)
     bool split_all = false;       // without primary reuse, every block as single samples
-    bool tail_split = true;       // single-sample tail items at the end of a launch
+    // 1- / 2-sample tail items at the end of a launch: 1 on, 0 off, -1 by the
+    // call (enqueue: off where the whole last pair of every pixel, which the
+    // tail region rounds up to, is more than 4x the samples it is meant for)
+    int32_t tail_split = -1;
     // tail regions (4-, 2-, 1-sample items) x D x lanes. Round 5: 0, 1, 0.5
     // against 0, 1, 1 (profiles/r05/tail/): headline -0.18 %, 10k spheres
     // -1.9 %, 4K -0.1 %, the N = 4 / 2 row shards -0.75 / -0.2 %
@@ -312,7 +315,8 @@ static bool tune_set(Tuning& t, const char* name, const char* v) {
     } else if (!strcmp(name, "split_all")) {
         t.split_all = x != 0;
     } else if (!strcmp(name, "tail_split")) {
-        t.tail_split = x != 0;
+        if (x != -1 && x != 0 && x != 1) return false;
+        t.tail_split = (int32_t)x;
     } else if (!strcmp(name, "item_order")) {
         if (x < 0 || x > 7) return false;
         t.item_order = (uint32_t)x;
@@ -1515,7 +1519,20 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         if (ctx->tune.wg_per_cu) wg_run = std::min<uint32_t>(ctx->tune.wg_per_cu, (uint32_t)bpc);
     }
     const uint64_t lanes = (uint64_t)ctx->cu_count * wg_run * RT_BLOCK_THREADS;
-    bool tail_on = tn.tail_split;
+    // The tail is meant for ~(a4 + a2 + a1) D samples per lane, but it is
+    // made of whole sample pairs of every pixel: one pair is 8 samples per
+    // pixel however few the tail needs. Where that pair is more than 4x the
+    // tail's samples (large frames: 4K one frame per launch 5.3x, the 8K
+    // frame 42x; the headline 2.6x, 10k spheres 2.6x, row shards less) the
+    // tail's 1- and 2-sample items, a slot per sample, cost more than they
+    // balance -- measured, same box (profiles/r06/c5/): off, 4K -0.8 % time
+    // and render writes 3.68 -> 2.55 GB per frame, the 8K frame -0.25 % and
+    // 6.70 -> 2.21 GB; the headline +-0 either way, 10k spheres +1.8 % off.
+    bool tail_on = tn.tail_split != 0;
+    if (tn.tail_split < 0) {
+        const double want = (tn.tail[0] + tn.tail[1] + tn.tail[2]) * p.max_depth * (double)lanes;
+        tail_on = 8.0 * (double)npix <= 4.0 * want;
+    }
     // One tail for every launch. (Launches with about one pixel per lane, the
     // N = 8 row shard of the headline, took 1, 1, 0.25 from the first tail
     // sweep of round 5 -- 26.09 -> 25.43 ms against 0, 1, 1; profiles/r05/tail/

@@ -70,7 +70,9 @@ def summarize(run):
 
 def main():
     raw = json.load(open(sys.argv[1]))
-    out = {}
+    path = os.path.join(ROOT, "profiles", "executed.json")
+    # the workloads of this raw record replace theirs; the others are kept
+    out = json.load(open(path)) if os.path.exists(path) else {}
     for key, run in raw["runs"].items():
         e = summarize(run)
         e["source"] = ("tools/executed.py (RT_PROFILE build of the same sources, one launch of "
@@ -82,7 +84,6 @@ def main():
                      "algorithm's own per-segment arithmetic; setup_bounds + walk are the "
                      "matrix-core filter that replaces its brute-force loop")
         out[key] = e
-    path = os.path.join(ROOT, "profiles", "executed.json")
     json.dump(out, open(path, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
