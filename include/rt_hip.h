@@ -229,13 +229,16 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, uint32_t n,
  * the materials when their count changes, ray_trace_materials.rs:129-164).
  * Replace records [first, first+count) of the current scene; counts N and M
  * are unchanged. Only the touched sphere records and 8-sphere groups are
- * re-packed and uploaded. The matrix-core filter's f16 sphere rows (their
- * scale 2^-sq and their k-d spatial order depend on every centre: O(N log N)
- * on the host for the order, 64 B per sphere uploaded; buffers sized for the
- * worst-case order, so the rebuild never allocates) are rebuilt once, at the
- * next call that walks them (a caller that renders only the culled list never
- * pays for them); the culled list (RT_FLAG_CULL), which depends on every
- * sphere, likewise at the next culled call. rt_update_materials rebuilds the
+ * re-packed and uploaded. The matrix-core filter's layout follows at the next
+ * call that walks it (a caller that renders only the culled list never pays
+ * for it): a moved sphere that keeps its radius and stays near its 32-sphere
+ * block's box, with the features' scale unchanged, is moved in place -- its
+ * f16 row, its half-block's and chunk's bound rows and its records, O(moved +
+ * blocks) on the host (13 us at 10,000 and 60,000 spheres), a few KB uploaded;
+ * otherwise the layout is rebuilt (scale, k-d spatial order O(N log N), 64 B
+ * per sphere uploaded; buffers sized for the worst-case order, so neither path
+ * allocates). The culled list (RT_FLAG_CULL), which depends on every sphere,
+ * is rebuilt at the next culled call. rt_update_materials rebuilds the
  * shading records only (both orders, O(N), 32 B per sphere): no geometry. */
 int rt_update_spheres(rt_ctx* ctx, uint32_t first, const rt_sphere* spheres, uint32_t count);
 int rt_update_materials(rt_ctx* ctx, uint32_t first, const rt_material* materials,

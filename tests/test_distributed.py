@@ -75,3 +75,25 @@ def test_gloo_row_tiling(world, B):
                            nthreads=2)
     assert segs == fsegs
     assert np.array_equal(img, full, equal_nan=True)
+
+
+@pytest.mark.parametrize("H,world", [(225, 2), (225, 3), (1080, 8), (4320, 8), (7, 8), (1, 2)])
+def test_cross_check_rows_cover_every_rank(H, world):
+    """bench.py's N>1 self-check re-renders, per rank, the first, middle and
+    last row it owns (distributed.check_rows): every rank that owns rows is
+    covered, each picked row is owned by the rank it is attributed to, and
+    both ends of every shard are checked."""
+    from bevy_raytrace_amd import abi, distributed as rdist
+    from bevy_raytrace_amd.configs import pick_row_block
+    B = pick_row_block(H, world)
+    rows = [abi.shard_rows(H, B, world, k) for k in range(world)]
+    picks = rdist.check_rows(rows)
+    ys = [y for _, y in picks]
+    assert len(ys) == len(set(ys))
+    owners = {k for k, _ in picks}
+    assert owners == {k for k in range(world) if rows[k]}
+    for k, y in picks:
+        assert y in rows[k]
+    for k, rk in enumerate(rows):
+        if rk:
+            assert (k, rk[0]) in picks and (k, rk[-1]) in picks
