@@ -894,7 +894,7 @@ static void f16_split(double x, uint16_t& hi, uint16_t& lo) {
 
 static const int MF_QA[6] = {0, 1, 2, 0, 0, 1}, MF_QB[6] = {0, 1, 2, 1, 2, 2};
 static const double MF_KS = 1.0 - 0x1p-16 - 0x1p-16;           // 1 - m - mu' (RT_MF_MU)
-static const double MF_KB = 1.0 - 0x1p-16 - 0x1p-16 - 0x1p-8;  // 1 - m - mu' - muB (RT_MF_MUB)
+static const double MF_KB = 1.0 - 0x1p-16 - 0x1p-16 - 0x1p-12;  // 1 - m - mu' - muB (RT_MF_MUB)
 
 // A record inside the f16 split's range (|c_i| <= 2^12, r^2 in [0, 2^24]),
 // and its largest quadratic feature max_ab |c_a c_b| = max_a c_a^2.

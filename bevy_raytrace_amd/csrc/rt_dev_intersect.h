@@ -686,32 +686,48 @@ typedef float f16x __attribute__((ext_vector_type(16)));
 // bounding sphere (a block is walked when either half's passes) (C,
 // L = max_i (|C - c_i| + r_i (1 + 2^-18)), R^2 = (1 + 2^-4) L^2 + 2^-60) whose
 // bound row is a sphere row with S'_B = R^2 - (1 - m - mu' - muB)|C|^2 (rounded
-// up; muB = 2^-8) and K 31 = 1, tested against the walk's own ray column,
-// whose K 31 holds -RN_f16(muB |o|^2) (0 in sphere rows): T0_B = T0 -
-// RN_f16(muB |o|^2) = (1 - m - mu' - muB')|o|^2 - k1^2 - abs' with muB' within
-// 2^-11 muB of muB. A half-wave skips a block whose bounds no ray of the half
-// passes (V_B >= 0 in every lane). Why a skipped block holds no hit: a member
-// sphere i the exact test hits is a candidate of the packed VALU filter (its
-// proof, ray_filter_consts), so by the first step of the culled list's bound
-// proof (rt_api.cpp, above cull_layout) dist_i^2 <= r_i^2 (1 + 2^-17) +
-// (m + 2^-19)|o - c_i|^2 + (mu + 2^-17)(|o|^2 + |c_i|^2) <= r_i^2 (1 + 2^-17) +
-// delta_i with delta_i = 2^-14.3 (|o|^2 + |c_i|^2) (|o - c_i|^2 <= 2|o|^2 +
-// 2|c_i|^2) <= 2^-14.3 |o|^2 + 2^-13.3 (|C|^2 + L^2) (|c_i|^2 <= 2|C|^2 +
-// 2L^2); dist_i <= r_i (1 + 2^-18) + sqrt(delta_i), and the line distance is
-// 1-Lipschitz: dist_C <= L + sqrt(delta_i). With 2ab <= a^2/32 + 32 b^2:
-//   dist_C^2 <= (1 + 2^-5) L^2 + 33 delta_i
-//            <= (1 + 2^-5 + 2^-8.26) L^2 + 2^-8.26 (|o|^2 + |C|^2).
+// up; muB = 2^-12 since round 6, 2^-8 before) and K 31 = 1, tested against the
+// walk's own ray column, whose K 31 holds -RN_f16(muB |o|^2) (0 in sphere
+// rows): T0_B = T0 - RN_f16(muB |o|^2) = (1 - m - mu' - muB')|o|^2 - k1^2 -
+// abs' with muB' within 2^-11 muB of muB (a subnormal f16 errs by <= 2^-25
+// absolute, inside abs'). A half-wave skips a block whose bounds no ray of the
+// half passes (V_B >= 0 in every lane).
+// Why a skipped block holds no hit -- straight from the exact test's f32
+// arithmetic (exact_core; u = 2^-24, no FMA, correctly rounded sqrt): member
+// i (centre c, w = its f32 r^2) is hit only if the computed dis >= 0. With
+// v = fl(o - c) (|v - (o - c)| <= u|o - c|), hb = fl(dot(v, d)) (|hb - v.d| <=
+// 3.0001u|v||d|), fl(lo * lo) = |v|^2 (1 + rho) (|rho| <= 6.001u: dot,
+// sqrt, square), c~ = |v|^2 - w + e_c (|e_c| <= 7.002u|v|^2 + u w), a = |d|^2
+// (1 + eps_a) (|eps_a| <= 6.001u) and the two products and the difference each
+// rounded once, dis~ >= 0 means fl(hb^2) >= fl(a c~) (a nonzero difference of
+// two f32 never rounds to 0), i.e. (v.d)^2 + 7.001u|v|^2|d|^2 >= |d|^2 (|v|^2 -
+// w - 14.005u|v|^2 - 8.003u w), so the line's distance from the point o - v is
+// dist_v^2 = |v|^2 - (v.d)^2/|d|^2 <= w (1 + 2^-21) + 2^-19.61 |v|^2, and
+// from the centre (1-Lipschitz in the point) dist_i <= sqrt(w)(1 + 2^-22) +
+// 2^-9.79 |o - c_i|. (In the walk's domain -- |o_i|, |c_i| <= 2^12, |d|^2 in
+// [2^-100, 2^100] -- nothing overflows; subnormal products add <= 2^-148
+// absolute to dis, <= 2^-48 to dist^2, inside abs'.) Round 5 reached the same
+// step through the packed VALU filter's margins (dist_i^2 <= r_i^2 + 2^-14.3
+// (|o|^2 + |c_i|^2)), 24x looser, hence its muB = 2^-8.
+// The line distance is 1-Lipschitz again: dist_C <= L + s, s = 2^-9.79 |o -
+// c_i| (L >= |C - c_i| + r_i (1 + 2^-18)), and with 2ab <= a^2/32 + 32 b^2,
+// s^2 <= 2^-19.58 (2|o|^2 + 2|c_i|^2) and |c_i|^2 <= 2|C|^2 + 2L^2:
+//   dist_C^2 <= (1 + 2^-5) L^2 + 33 s^2
+//            <= (1 + 2^-5 + 2^-12.54) L^2 + 2^-12.54 (|o|^2 + |C|^2).
 // The bound row's exact value is F_B = hb~_C^2 + R^2 - (1 - m)|o - C|^2 +
 // (mu' + muB')(|o|^2 + |C|^2) + abs' >= R^2 - dist_C^2 + (mu' + muB' - 2^-18)
-// (|o|^2 + |C|^2) >= (2^-5 - 2^-8.26) L^2 + 2^-60 + (2^-8 (1 - 2^-11) -
-// 2^-8.26 - 2^-18)(|o|^2 + |C|^2) (the last factor > 2^-10.7), which exceeds
-// the tile's rounding (<= 2^-16.02 (|o|^2 + |C|^2) + 2^-20.4 |S'_B|, |S'_B| <=
-// R^2 + |C|^2, the analysis above; |C_i| <= 2^12 as the members', |S'_B| <=
-// 2^15 or the bound row always passes): V_B = T0_B - H0_B < 0. The proof's
-// domain: |o_i| <= 2^12 (mfma_wave_ok) and |d|^2 in [2^-100, 2^100] for every
-// live lane, else the wave walks every block. Bound rows of blocks with an
+// (|o|^2 + |C|^2) (hb~ with the computed unit direction, |eta| <= 2^-21) >=
+// (2^-5 - 2^-12.54) L^2 + 2^-60 + (mu' + 2^-12 (1 - 2^-11) - 2^-12.54 -
+// 2^-18)(|o|^2 + |C|^2), which exceeds the tile's rounding (<= 2^-16.02
+// (|o|^2 + |C|^2) + 2^-20.4 |S'_B|, |S'_B| <= R^2 + |C|^2, the analysis
+// above; mu' = 2^-16 covers the 2^-16.02, and 2^-12 (1 - 2^-11) - 2^-12.54 -
+// 2^-18 - 2^-20.4 > 2^-13.9; |C_i| <= 2^12 as the members', |S'_B| <= 2^15 or
+// the bound row always passes): V_B = T0_B - H0_B < 0. The proof's domain:
+// |o_i| <= 2^12 (mfma_wave_ok) and |d|^2 in [2^-100, 2^100] for every live
+// lane, else the wave walks every block. Bound rows of blocks with an
 // out-of-range bound always pass (S'_B hi = +inf), of empty blocks never
-// (-inf).
+// (-inf). tests/test_mfma_filter.py checks it numerically (exact hits of the
+// adversarial ray sets never in a skipped block, five summation orders).
 //
 // Forward bounds. A bound is also skipped for a ray when it lies wholly behind
 // the ray's origin. Any hit of a member sphere i (root >= EPSILON > 0) has
@@ -729,7 +745,7 @@ typedef float f16x __attribute__((ext_vector_type(16)));
 // (tile_or_fwd; tests/test_mfma_filter.py test_forward_bounds_are_conservative
 // checks it numerically in five summation orders).
 #define RT_MF_MU 0x1p-16f
-#define RT_MF_MUB 0x1p-8f  // the block-bound tile's extra margin (see "Block bounds")
+#define RT_MF_MUB 0x1p-12f  // the block-bound tile's extra margin (see "Block bounds")
 #ifndef RT_MF_CAP
 #define RT_MF_CAP 12  // queue entries per lane and half (LDS)
 #endif

@@ -264,7 +264,7 @@ def test_scale_is_the_whole_scenes():
     assert scene_rows("spheres10k")[1] == qscale(full)
 
 
-MUB = 2.0 ** -8  # rt_dev_intersect.h RT_MF_MUB
+MUB = 2.0 ** -12  # rt_dev_intersect.h RT_MF_MUB (2^-8 through round 5)
 
 
 def round_up_f32(v):
