@@ -1008,15 +1008,16 @@ static void mf_bound_row(const MfHost& H, uint32_t p0, uint32_t p1, uint16_t* bl
             Lm = std::max(Lm, std::sqrt(dx * dx + dy * dy + dz * dz) * (1.0 + 0x1p-40) +
                                   std::sqrt((double)q.w) * (1.0 + 0x1p-18));
         }
-        // (1 + 2^-4), not the culled list's (1 + 2^-3): rt_dev_intersect.h "Block bounds"
-        const double R2 = (1.0 + 0x1p-4) * Lm * Lm * (1.0 + 0x1p-40) + 0x1p-60;
+        // (1 + 2^-5 + 2^-10) (round 6; 1 + 2^-4 before, the culled list's
+        // 1 + 2^-3): rt_dev_intersect.h "Block bounds"
+        const double R2 = (1.0 + 0x1p-5 + 0x1p-10) * Lm * Lm * (1.0 + 0x1p-40) + 0x1p-60;
         const double CC = C[0] * C[0] + C[1] * C[1] + C[2] * C[2];
         SB = (double)round_up_f32((R2 - MF_KB * CC) * (1.0 + 0x1p-40) + 0x1p-60);
         if (!(std::fabs(SB) <= 0x1p15)) SB = INFINITY;  // out of the split's range: always passes
-        // L' = (1 + 2^-3) L + 2^-7 |C|_1 + 2^-14, rounded up; +inf (the
+        // L' = (1 + 2^-12) L + 2^-8 |C|_1 + 2^-14, rounded up; +inf (the
         // forward row always passes) with the line row's or beyond f16
         const double C1 = std::fabs(C[0]) + std::fabs(C[1]) + std::fabs(C[2]);
-        Lf = (1.0 + 0x1p-3) * Lm + 0x1p-7 * C1 + 0x1p-14;
+        Lf = (1.0 + 0x1p-12) * Lm + 0x1p-8 * C1 + 0x1p-14;
         if (std::isinf(SB) || !(Lf <= 0x1p15)) Lf = INFINITY;
     }
     uint16_t row[32];

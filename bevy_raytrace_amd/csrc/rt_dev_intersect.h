@@ -684,7 +684,8 @@ typedef float f16x __attribute__((ext_vector_type(16)));
 // Block bounds (mf.B). The list is walked in the culled list's spatial order
 // (rt_api.cpp build_mfma), and each 16-sphere half of a 32-sphere block has a
 // bounding sphere (a block is walked when either half's passes) (C,
-// L = max_i (|C - c_i| + r_i (1 + 2^-18)), R^2 = (1 + 2^-4) L^2 + 2^-60) whose
+// L = max_i (|C - c_i| + r_i (1 + 2^-18)), R^2 = (1 + 2^-5 + 2^-10) L^2 + 2^-60,
+// 1 + 2^-4 through round 5) whose
 // bound row is a sphere row with S'_B = R^2 - (1 - m - mu' - muB)|C|^2 (rounded
 // up; muB = 2^-12 since round 6, 2^-8 before) and K 31 = 1, tested against the
 // walk's own ray column, whose K 31 holds -RN_f16(muB |o|^2) (0 in sphere
@@ -717,10 +718,11 @@ typedef float f16x __attribute__((ext_vector_type(16)));
 // The bound row's exact value is F_B = hb~_C^2 + R^2 - (1 - m)|o - C|^2 +
 // (mu' + muB')(|o|^2 + |C|^2) + abs' >= R^2 - dist_C^2 + (mu' + muB' - 2^-18)
 // (|o|^2 + |C|^2) (hb~ with the computed unit direction, |eta| <= 2^-21) >=
-// (2^-5 - 2^-12.54) L^2 + 2^-60 + (mu' + 2^-12 (1 - 2^-11) - 2^-12.54 -
+// (2^-10 - 2^-12.54) L^2 + 2^-60 + (mu' + 2^-12 (1 - 2^-11) - 2^-12.54 -
 // 2^-18)(|o|^2 + |C|^2), which exceeds the tile's rounding (<= 2^-16.02
 // (|o|^2 + |C|^2) + 2^-20.4 |S'_B|, |S'_B| <= R^2 + |C|^2, the analysis
-// above; mu' = 2^-16 covers the 2^-16.02, and 2^-12 (1 - 2^-11) - 2^-12.54 -
+// above; (2^-10 - 2^-12.54) L^2 covers 2^-20.4 R^2; mu' = 2^-16 covers the
+// 2^-16.02, and 2^-12 (1 - 2^-11) - 2^-12.54 -
 // 2^-18 - 2^-20.4 > 2^-13.9; |C_i| <= 2^12 as the members', |S'_B| <= 2^15 or
 // the bound row always passes): V_B = T0_B - H0_B < 0. The proof's domain:
 // |o_i| <= 2^12 (mfma_wave_ok) and |d|^2 in [2^-100, 2^100] for every live
@@ -736,11 +738,13 @@ typedef float f16x __attribute__((ext_vector_type(16)));
 // -r_i (1 + 2^-20) - 2^-20 (|o| + |c_i|), and dn.(C - o) >= -L - 2^-20 (|o| +
 // |C| + L). The forward row (rt_api.cpp build_mfma; one
 // v_mfma_f32_32x32x8_f16 per half) computes U = dn_hi.C_hi + c0_hi + L'_hi,
-// c0 = fma(2^-7, |o|_1, -k1) (k1 = dn.o), L' = (1 + 2^-3) L + 2^-7 |C|_1 +
+// c0 = fma(2^-9, |o|_1, -k1) (k1 = dn.o), L' = (1 + 2^-12) L + 2^-8 |C|_1 +
 // 2^-14 rounded UP to f16 (+inf, always passing, where the line row does or
 // beyond 2^15). The f16 parts cost <= 2^-9.9 |C|_1 (dn_hi C_hi) and
-// 2^-10.8 |o|_1 (c0_hi), v_rsq and the f32 sums <= 2^-20 (|C|_1 + |o|_1 + L'),
-// all inside the 2^-3 L + 2^-7 (|C|_1 + |o|_1) + 2^-14 slack: a hit's bound
+// 2^-10.9 |o|_1 (c0_hi, |c0| <= |o|_1), v_rsq and the f32 sums <= 2^-20
+// (|C|_1 + |o|_1 + L'), all inside the 2^-12 L + 2^-8 |C|_1 + 2^-9 |o|_1 +
+// 2^-14 slack (round 6; through round 5 2^-3 L + 2^-7 (|C|_1 + |o|_1) + 2^-14,
+// the L term pure slack: the hit condition needs L (1 + 2^-20)): a hit's bound
 // has U > 0, and the tile passes a (ray, bound) pair iff V_B < 0 and U >= +0
 // (tile_or_fwd; tests/test_mfma_filter.py test_forward_bounds_are_conservative
 // checks it numerically in five summation orders).
@@ -1121,7 +1125,7 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
     // Chunk bounds (mf.top: 2..32 bound chunks, e.g. 10,000 spheres in 20):
     // row j of the chunk-level chunk is the bound of bound chunk j's 512 walk
     // positions, built like a block bound (C, L over its members, R^2 =
-    // (1 + 2^-4) L^2, muB, forward row), so the "Block bounds" / "Forward
+    // (1 + 2^-5 + 2^-10) L^2, muB, forward row), so the "Block bounds" / "Forward
     // bounds" proofs hold for it unchanged: a ray with an exact hit in chunk
     // j passes row j. Its tile (the same three MFMAs per half) runs first; a
     // half that no ray of passes chunk j gets no block of chunk j, and a chunk
@@ -1131,13 +1135,13 @@ __device__ __forceinline__ int intersect_world_mfma(const MfScene& mf,
     if (has_b && rt_ballot(live && !(dd >= 0x1p-100f && dd <= 0x1p100f)) == 0) {
         mv0 = mv1 = 0u;
         // the forward column (rt_api.cpp build_mfma; "Forward bounds"), K 0..7
-        // of v_mfma_f32_32x32x8_f16: dn = -e hi x3, c0 = fma(2^-7, |o|_1, -k1)
+        // of v_mfma_f32_32x32x8_f16: dn = -e hi x3, c0 = fma(2^-9, |o|_1, -k1)
         // hi | 1, 0 x3 -- lanes 32..63 of a half's fragment hold the constant
         // K 4..7
         typedef _Float16 h4v __attribute__((ext_vector_type(4)));
         h4v G0, G1;
         {
-            const float c0 = __builtin_fmaf(0x1p-7f, fabsf(o.x) + fabsf(o.y) + fabsf(o.z), -k1);
+            const float c0 = __builtin_fmaf(0x1p-9f, fabsf(o.x) + fabsf(o.y) + fabsf(o.z), -k1);
             const uint32_t u0 = pk(-ex, -ey), u1 = pk(-ez, c0);
             const uint32_t k4 = pk(1.0f, 0.0f), k6 = 0u;
             const auto r0 = __builtin_amdgcn_permlane32_swap(u0, k4, false, false);

@@ -275,7 +275,7 @@ def round_up_f32(v):
 def block_bounds(sp, perm, nblk, size=16, return_forward=False):
     """rt_api.cpp build_mfma's bounds: per `size` walk positions (half a
     32-sphere block) the box centre C (f32) of the members, L = max(|c - C|
-    (1 + 2^-40) + r (1 + 2^-18)), R^2 = (1 + 2^-4) L^2 (1 + 2^-40) + 2^-60 and
+    (1 + 2^-40) + r (1 + 2^-18)), R^2 = (1 + 2^-5 + 2^-10) L^2 (1 + 2^-40) + 2^-60 and
     S'_B = R^2 - (1 - m - mu' - muB)|C|^2 rounded up (+inf beyond 2^15, -inf
     for an empty one); nblk counts bounds."""
     c_all = sp["center"].astype(F).astype(D)
@@ -292,10 +292,10 @@ def block_bounds(sp, perm, nblk, size=16, return_forward=False):
         c = c_all[idx]
         C[b] = ((c.min(0) + c.max(0)) * 0.5).astype(F).astype(D)
         Lm = np.max(np.linalg.norm(c - C[b], axis=1) * (1 + 2.0 ** -40) + np.sqrt(r2_all[idx]) * (1 + 2.0 ** -18))
-        R2 = (1 + 2.0 ** -4) * Lm * Lm * (1 + 2.0 ** -40) + 2.0 ** -60
+        R2 = (1 + 2.0 ** -5 + 2.0 ** -10) * Lm * Lm * (1 + 2.0 ** -40) + 2.0 ** -60
         SB = round_up_f32((R2 - kB * (C[b] ** 2).sum()) * (1 + 2.0 ** -40) + 2.0 ** -60)
         S[b] = SB if abs(SB) <= 2.0 ** 15 else np.inf
-        lf = (1 + 2.0 ** -3) * Lm + 2.0 ** -7 * np.abs(C[b]).sum() + 2.0 ** -14
+        lf = (1 + 2.0 ** -12) * Lm + 2.0 ** -8 * np.abs(C[b]).sum() + 2.0 ** -14
         if np.isinf(S[b]) or not lf <= 2.0 ** 15:
             Lf[b] = np.inf
         else:  # rounded up to f16
@@ -321,11 +321,11 @@ def forward_rows(C, Lf):
 
 def forward_columns(rays):
     """The kernel's forward column (intersect_world_mfma): dn = -e hi x3, c0 =
-    fma(2^-7, |o|_1, -k1) hi, 1 (zero-padded to 32)."""
+    fma(2^-9, |o|_1, -k1) hi, 1 (zero-padded to 32)."""
     o, e, k1, _, _ = ray_constants(rays)
     with np.errstate(invalid="ignore", over="ignore"):
         o1 = ((np.abs(o[:, 0]) + np.abs(o[:, 1])).astype(F) + np.abs(o[:, 2])).astype(F)
-        c0 = fma32(F(2.0 ** -7), o1, -k1)
+        c0 = fma32(F(2.0 ** -9), o1, -k1)
     n = len(rays)
     cols = [np.zeros(n, F)] * 32
     for a in range(3):
