@@ -983,7 +983,12 @@ static bool mf_set_pos(MfHost& H, uint32_t p, const float4* sph) {
 // against the ray column's -RN_f16(muB |o|^2); the forward row is C hi x3, 1 |
 // L' (rounded up), 0 x3 against the ray's dn hi x3, c0 hi | 1, 0 x3
 // (v_mfma_f32_32x32x8_f16 B fragments, 8 bytes per lane at uint2 256 + lane).
-static void mf_bound_row(const MfHost& H, uint32_t p0, uint32_t p1, uint16_t* blk, uint32_t j) {
+// chunk: the row is a chunk-level bound (512 walk positions, L ~ 15-35 for
+// the 10,000-sphere field) -- its own split of the proof's slack (rt_dev_
+// intersect.h "Chunk bounds"): R^2 = (1 + 2^-7 + 2^-9) L^2 and 4 muB (K 31 =
+// 4), where a half-block's (L ~ 3) is R^2 = (1 + 2^-5 + 2^-10) L^2 and muB.
+static void mf_bound_row(const MfHost& H, uint32_t p0, uint32_t p1, uint16_t* blk, uint32_t j,
+                         bool chunk = false) {
     double lo3[3] = {INFINITY, INFINITY, INFINITY}, hi3[3] = {-INFINITY, -INFINITY, -INFINITY};
     bool any = false;
     for (uint32_t p = p0; p < p1; ++p) {
@@ -1010,9 +1015,11 @@ static void mf_bound_row(const MfHost& H, uint32_t p0, uint32_t p1, uint16_t* bl
         }
         // (1 + 2^-5 + 2^-10) (round 6; 1 + 2^-4 before, the culled list's
         // 1 + 2^-3): rt_dev_intersect.h "Block bounds"
-        const double R2 = (1.0 + 0x1p-5 + 0x1p-10) * Lm * Lm * (1.0 + 0x1p-40) + 0x1p-60;
+        const double R2 = (chunk ? 1.0 + 0x1p-7 + 0x1p-9 : 1.0 + 0x1p-5 + 0x1p-10) * Lm * Lm *
+                              (1.0 + 0x1p-40) + 0x1p-60;
         const double CC = C[0] * C[0] + C[1] * C[1] + C[2] * C[2];
-        SB = (double)round_up_f32((R2 - MF_KB * CC) * (1.0 + 0x1p-40) + 0x1p-60);
+        const double kB = chunk ? MF_KB - 3.0 * 0x1p-12 : MF_KB;  // 1 - m - mu' - (4) muB
+        SB = (double)round_up_f32((R2 - kB * CC) * (1.0 + 0x1p-40) + 0x1p-60);
         if (!(std::fabs(SB) <= 0x1p15)) SB = INFINITY;  // out of the split's range: always passes
         // L' = (1 + 2^-12) L + 2^-8 |C|_1 + 2^-14, rounded up; +inf (the
         // forward row always passes) with the line row's or beyond f16
@@ -1022,7 +1029,7 @@ static void mf_bound_row(const MfHost& H, uint32_t p0, uint32_t p1, uint16_t* bl
     }
     uint16_t row[32];
     mf_make_row(C, SB, H.sq, row);
-    row[31] = f16_bits(1.0);  // against the ray's -RN_f16(muB |o|^2)
+    row[31] = f16_bits(chunk ? 4.0 : 1.0);  // against the ray's -RN_f16(muB |o|^2)
     for (int hh = 0; hh < 2; ++hh)
         for (int half = 0; half < 2; ++half)  // B0: K 0..15, B1: K 16..31
             std::memcpy(&blk[((size_t)half * 64 + 32 * hh + j) * 8], &row[16 * half + 8 * hh], 16);
@@ -1053,7 +1060,7 @@ static void mf_half_block_bound(MfHost& H, uint32_t r) {
 // 10,000 spheres: 20 chunks).
 static void mf_chunk_bound(MfHost& H, uint32_t j) {
     const uint32_t p0 = 512 * j, p1 = j < H.nchunk ? std::min(p0 + 512, H.npos) : p0;
-    mf_bound_row(H, p0, p1, &H.B[(size_t)H.nchunk * RT_MF_BCHUNK * 8], j);
+    mf_bound_row(H, p0, p1, &H.B[(size_t)H.nchunk * RT_MF_BCHUNK * 8], j, true);
 }
 
 // The whole layout of n records in walk order `order` (spatial_order's) at
@@ -1789,10 +1796,16 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
     // 64-sample pixel items) -0.33 %, 4K (8,100; 256) -0.5 %; the N = 8
     // shard (1,266) +0.7 %, 10k spheres (2,025) +0.8 %, the 8K frame
     // (129,600; 1,024-sample items) +1.4 %. By the call: on below 4,096
-    // samples per lane or above 256 samples per pixel.
+    // samples per lane or where a frame's paths are long -- spp x depth
+    // above 4,096 sample-bounces (round 6; round 5 had spp > 256, the same at
+    // depth 16). The one-frame 4K launch (256 spp, depth 32: 8,192) ran about
+    // half its runs 3-11 % slow with the rotation off -- waves starved by age
+    // holding long pixel items -- and every run at the fast time with it on:
+    // 6 + 6 runs, 416-462 vs 418.9-419.0 Mcycles (profiles/r06/c16/ab4k/).
     {
         const double spl = (double)npix * p.spp * nframes / (double)std::max<uint64_t>(lanes, 1);
-        K_.prio_mode = tn.prio_mode >= 0 ? (uint32_t)tn.prio_mode : (spl < 4096.0 || p.spp > 256u ? 1u : 0u);
+        const double sd = (double)p.spp * p.max_depth;
+        K_.prio_mode = tn.prio_mode >= 0 ? (uint32_t)tn.prio_mode : (spl < 4096.0 || sd > 4096.0 ? 1u : 0u);
     }
     K_.prio_shift = tn.prio_shift;
     // wide (sphere-parallel) tracing pays ~32 VALU per 64 spheres per ray plus

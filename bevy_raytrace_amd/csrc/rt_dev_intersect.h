@@ -728,7 +728,12 @@ typedef float f16x __attribute__((ext_vector_type(16)));
 // |o_i| <= 2^12 (mfma_wave_ok) and |d|^2 in [2^-100, 2^100] for every live
 // lane, else the wave walks every block. Bound rows of blocks with an
 // out-of-range bound always pass (S'_B hi = +inf), of empty blocks never
-// (-inf). tests/test_mfma_filter.py checks it numerically (exact hits of the
+// (-inf). Chunk-level rows ("Chunk bounds" below, L ~ 15-35 for the
+// 10,000-sphere field, where the (1 + t) L^2 term dominates) split the slack
+// the other way: t = 2^-7, so 129 s^2 <= 2^-10.57 (|o|^2 + |C|^2 + L^2),
+// R^2 = (1 + 2^-7 + 2^-9) L^2 and K 31 = 4 (4 muB = 2^-10 > 2^-10.57 +
+// 2^-18 + 2^-20.4; S'_B with 1 - m - mu' - 4 muB). tests/test_mfma_filter.py
+// checks both numerically (exact hits of the
 // adversarial ray sets never in a skipped block, five summation orders).
 //
 // Forward bounds. A bound is also skipped for a ray when it lies wholly behind

@@ -67,7 +67,7 @@ def sphere_rows(sp, sq):
     return rows_of(c, S, sq)
 
 
-def rows_of(c, S, sq, bound=False):
+def rows_of(c, S, sq, bound=False, k31=1.0):
     """A rows (f32 values of the f16 parts, K = 32) of centres c (n, 3) and
     constants S' (n,); an infinite S' is its hi part alone (build_mfma)."""
     def hl(x):
@@ -91,7 +91,7 @@ def rows_of(c, S, sq, bound=False):
     # K group 0: hi y0..y7, lo y0..y7; group 1: hi y0..y7, hi y8, hi y8, lo y8,
     # 1, 1, S' hi, S' lo, 0 (build_mfma's words w0..w15)
     cols = his[:8] + los[:8] + his[:8] + [his[8], his[8], los[8], one, one, shi, slo,
-                                          one if bound else np.zeros(n, H16)]
+                                          (one * H16(k31)) if bound else np.zeros(n, H16)]
     return np.stack(cols, 1).astype(F)
 
 
@@ -280,7 +280,11 @@ def block_bounds(sp, perm, nblk, size=16, return_forward=False):
     for an empty one); nblk counts bounds."""
     c_all = sp["center"].astype(F).astype(D)
     r2_all = (sp["radius"] * sp["radius"]).astype(F).astype(D)
-    kB = 1.0 - M - MU - MUB
+    # chunk-level rows (size 512) split the proof's slack with t = 2^-7: R^2 =
+    # (1 + 2^-7 + 2^-9) L^2 and 4 muB (their K 31 = 4, rows_of)
+    chunk = size == 512
+    kB = 1.0 - M - MU - (4 * MUB if chunk else MUB)
+    fac = (1 + 2.0 ** -7 + 2.0 ** -9) if chunk else (1 + 2.0 ** -5 + 2.0 ** -10)
     C = np.zeros((nblk, 3))
     S = np.full(nblk, -np.inf)
     Lf = np.zeros(nblk)  # the forward rows' L' (0 for an empty bound)
@@ -292,7 +296,7 @@ def block_bounds(sp, perm, nblk, size=16, return_forward=False):
         c = c_all[idx]
         C[b] = ((c.min(0) + c.max(0)) * 0.5).astype(F).astype(D)
         Lm = np.max(np.linalg.norm(c - C[b], axis=1) * (1 + 2.0 ** -40) + np.sqrt(r2_all[idx]) * (1 + 2.0 ** -18))
-        R2 = (1 + 2.0 ** -5 + 2.0 ** -10) * Lm * Lm * (1 + 2.0 ** -40) + 2.0 ** -60
+        R2 = fac * Lm * Lm * (1 + 2.0 ** -40) + 2.0 ** -60
         SB = round_up_f32((R2 - kB * (C[b] ** 2).sum()) * (1 + 2.0 ** -40) + 2.0 ** -60)
         S[b] = SB if abs(SB) <= 2.0 ** 15 else np.inf
         lf = (1 + 2.0 ** -12) * Lm + 2.0 ** -8 * np.abs(C[b]).sum() + 2.0 ** -14
@@ -354,7 +358,7 @@ def test_block_bounds_are_conservative(name, size):
     perm = abi.cull_layout(full)[0]
     nblk = -(-(len(perm) - 8) // size)  # bounds over whole clusters (+ one pad group)
     C, S = block_bounds(full, perm, nblk, size=size)
-    A = rows_of(C, S, sq, bound=True)
+    A = rows_of(C, S, sq, bound=True, k31=4.0 if size == 512 else 1.0)
     sp = full[:SUBSET.get(name, len(full))]
     rays = _rays(sp, "blk" + name, 6_000 if len(sp) < 1000 else 2_000)
     d = rays[:, 3:].astype(F)
@@ -388,7 +392,7 @@ def test_forward_bounds_are_conservative(name, size):
     perm = abi.cull_layout(full)[0]
     nblk = -(-(len(perm) - 8) // size)
     C, S, Lf = block_bounds(full, perm, nblk, size=size, return_forward=True)
-    A = rows_of(C, S, sq, bound=True)
+    A = rows_of(C, S, sq, bound=True, k31=4.0 if size == 512 else 1.0)
     Af = forward_rows(C, Lf)
     sp = full[:SUBSET.get(name, len(full))]
     rays = _rays(sp, "fwd" + name, 6_000 if len(sp) < 1000 else 2_000)
