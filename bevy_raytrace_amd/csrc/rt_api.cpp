@@ -1886,8 +1886,18 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         // Work chunk per atomic: 64 items (knob wave_chunk). 128 measured, same
         // box: headline -1.7 % but spread 437-448 Mcycles against 449.1-449.9,
         // 4K +15 %, 10k spheres +6 %, the N = 8 shard +8-18 %: a wave holding
-        // a larger chunk ends later (profiles/r05/wave_chunk/).
-        K_.chunk = tn.wave_chunk > 0 ? (uint32_t)tn.wave_chunk : (uint32_t)RT_WAVE_CHUNK;
+        // a larger chunk ends later (profiles/r05/wave_chunk/). Round 6, the
+        // final kernel: headline -2.7 % (5 + 5 runs, 426-437 vs 442-443
+        // Mcycles, profiles/r06/c19_chunk/; 96: -0.8 %) -- so by the call:
+        // 128 for launches whose pixel region holds at least 8 whole frames
+        // and >= 8,192 samples per lane (the multi-frame whole-frame launches:
+        // a wave's refills then stay among neighbouring pixels' frames), 64
+        // for the one-frame, block-only and row-shard launches it slowed.
+        {
+            const double spl = (double)npix * p.spp * ps.nframes / (double)std::max<uint64_t>(lanes, 1);
+            const bool big = rg.fp >= 8 && spl >= 8192.0;
+            K_.chunk = tn.wave_chunk > 0 ? (uint32_t)tn.wave_chunk : (big ? 128u : (uint32_t)RT_WAVE_CHUNK);
+        }
         const uint64_t chunks = (items + K_.chunk - 1) / K_.chunk;
         const uint64_t need_blocks = (chunks + (RT_BLOCK_THREADS / 64) - 1) / (RT_BLOCK_THREADS / 64);
         const uint32_t grid = (uint32_t)(need_blocks < grid_full ? need_blocks : grid_full);
