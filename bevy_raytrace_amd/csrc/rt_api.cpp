@@ -1807,6 +1807,7 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
         const double sd = (double)p.spp * p.max_depth;
         K_.prio_mode = tn.prio_mode >= 0 ? (uint32_t)tn.prio_mode : (spl < 4096.0 || sd > 4096.0 ? 1u : 0u);
     }
+    const uint32_t prio_call = K_.prio_mode;  // (+ the passes with 128-item chunks, below)
     K_.prio_shift = tn.prio_shift;
     // wide (sphere-parallel) tracing pays ~32 VALU per 64 spheres per ray plus
     // a reduction; the ray-parallel walk ~34 per 8-sphere group per wave plus
@@ -1897,6 +1898,11 @@ static int enqueue(rt_ctx* ctx, Frame& f, const rt_camera* cam, const rt_params*
             const double spl = (double)npix * p.spp * ps.nframes / (double)std::max<uint64_t>(lanes, 1);
             const bool big = rg.fp >= 8 && spl >= 8192.0;
             K_.chunk = tn.wave_chunk > 0 ? (uint32_t)tn.wave_chunk : (big ? 128u : (uint32_t)RT_WAVE_CHUNK);
+            // ... and with the s_setprio rotation: the headline with 128-item
+            // chunks and no rotation ran a third of its runs ~3 % slow (the
+            // age-ordered issue again), with it 6 of 6 runs fast (426.5-430.2
+            // vs 427.6-446.9 Mcycles, profiles/r06/c23/)
+            K_.prio_mode = (tn.prio_mode < 0 && big && tn.wave_chunk <= 0) ? 1u : prio_call;
         }
         const uint64_t chunks = (items + K_.chunk - 1) / K_.chunk;
         const uint64_t need_blocks = (chunks + (RT_BLOCK_THREADS / 64) - 1) / (RT_BLOCK_THREADS / 64);
