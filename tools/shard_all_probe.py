@@ -3,7 +3,7 @@
 two launches enqueued back to back) and as bench.py runs it (a launch after a
 host sync and a short idle gap, best of 3), next to the full frame the same
 ways; prints the predicted render-only speedup.
-usage: python tools/shard_all_probe.py [F] [N]"""
+usage: [PROBE_TUNE="knob=v;knob=v"] python tools/shard_all_probe.py [F] [N]"""
 import os
 import sys
 import time
@@ -21,6 +21,8 @@ wl = configs.WORKLOADS["rtiow1080"]
 sc = wl.make_scene()
 cam = default_camera_block()
 r = Renderer(0, lib_path=os.environ.get("PROBE_LIB") or None)
+for kv in filter(None, (os.environ.get("PROBE_TUNE") or "").split(";")):
+    r.tune(*kv.split("=", 1))  # A/B knobs, e.g. PROBE_TUNE="wave_chunk=128;prio_mode=1"
 r.set_scene(sc.objects_gpu(), sc.materials_gpu())
 W, H, S, D = wl.width, wl.height, wl.spp, wl.max_depth
 NO_REUSE = abi.RT_FLAG_NO_PRIMARY_CACHE
